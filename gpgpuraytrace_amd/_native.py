@@ -1,0 +1,102 @@
+"""ctypes binding of the in-tree C-ABI library (include/frosttrace.h).
+
+The product path has no fallback: if librt_hip.so is missing this module
+raises, loudly, instead of computing anything on the CPU.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "librt_hip.so")
+ROOT = os.path.dirname(HERE)
+HEADER = os.path.join(ROOT, "include", "frosttrace.h")
+
+RT_OK = 0
+RT_DEVICE_FLOAT_OUTPUT = 1
+RT_DEVICE_STATS = 2
+RT_TEXTURE_2D = 1
+RT_FORMAT_R8G8B8A8_UINT = 3
+
+
+class RtStats(C.Structure):
+    _fields_ = [("primary_steps", C.c_ulonglong), ("shadow_steps", C.c_ulonglong),
+                ("prepass_steps", C.c_ulonglong), ("hits", C.c_ulonglong)]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+# name -> (restype, argtypes)
+_vp, _i, _u, _sz, _cp = C.c_void_p, C.c_int, C.c_uint, C.c_size_t, C.c_char_p
+SIGNATURES = {
+    "rt_last_error": (_cp, []),
+    "rt_abi_version": (_i, []),
+    "rt_vfs_add_path": (_i, [_cp]),
+    "rt_vfs_clear": (_i, []),
+    "rt_device_create": (_i, [_i, _i, _i, _u, C.POINTER(_vp)]),
+    "rt_device_destroy": (None, [_vp]),
+    "rt_device_present": (_i, [_vp]),
+    "rt_device_flush": (_i, [_vp]),
+    "rt_device_synchronize": (_i, [_vp]),
+    "rt_device_readback": (_i, [_vp, _vp, _sz]),
+    "rt_device_readback_float": (_i, [_vp, _vp]),
+    "rt_device_size": (_i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
+    "rt_device_framebuffer": (_vp, [_vp]),
+    "rt_device_stream": (_vp, [_vp]),
+    "rt_device_set_stream": (_i, [_vp, _vp]),
+    "rt_device_stats": (_i, [_vp, C.POINTER(RtStats), _i]),
+    "rt_texture_create": (_i, [_vp, C.POINTER(_vp)]),
+    "rt_texture_init": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i]),
+    "rt_texture_destroy": (None, [_vp]),
+    "rt_compute_create": (_i, [_vp, C.POINTER(_vp)]),
+    "rt_compute_destroy": (None, [_vp]),
+    "rt_compute_load": (_i, [_vp, _cp, _cp, _cp, _i, _i, _i, C.POINTER(_cp), C.POINTER(_cp), _i]),
+    "rt_compute_swap": (_i, [_vp]),
+    "rt_compute_run": (_i, [_vp, _u, _u, _u]),
+    "rt_compute_set_texture": (_i, [_vp, _i, _vp]),
+    "rt_compute_thread_size": (_i, [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)]),
+    "rt_compute_get_variable": (_vp, [_vp, _cp]),
+    "rt_compute_get_array": (_vp, [_vp, _cp]),
+    "rt_compute_get_buffer": (_vp, [_vp, _cp]),
+    "rt_variable_write": (_i, [_vp, _vp]),
+    "rt_variable_size": (_sz, [_vp]),
+    "rt_variable_name": (_cp, [_vp]),
+    "rt_array_create": (_i, [_vp, _u]),
+    "rt_array_map": (_vp, [_vp]),
+    "rt_array_unmap": (_i, [_vp]),
+    "rt_array_write": (_i, [_vp, _vp]),
+    "rt_array_stride": (_sz, [_vp]),
+    "rt_array_device_pointer": (_vp, [_vp]),
+    "rt_terrain_render": (_i, [_vp, _vp, _i, _i]),
+    "rt_shard_bytes": (_sz, [_vp, _i, _i]),
+    "rt_shard_pack": (_i, [_vp, _i, _i, _vp]),
+    "rt_shard_unpack": (_i, [_vp, _i, _i, _vp]),
+    "rt_noise_generate": (_i, [C.c_uint32, _i, _vp, _vp]),
+    "rt_terrain_set_target_depths": (_i, [_vp, _vp]),
+}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"gpgpuraytrace_amd: native library missing at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C gpgpuraytrace_amd/csrc)")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != RT_OK:
+        msg = lib().rt_last_error().decode(errors="replace")
+        raise NativeError(f"{what}: rc={rc}: {msg}")
+    return rc

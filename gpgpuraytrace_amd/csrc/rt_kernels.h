@@ -1,0 +1,31 @@
+// rt_kernels.h -- host-side launch interface of the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "rt_types.h"
+
+struct RtLaunch {
+    hipStream_t stream;
+    int landscape;
+    const RtConsts* consts;   // device copy of the constant block
+    const uint32_t* perm2d;   // device texPerm2D (128*128 texels)
+    const uint8_t* codes2;    // device packed gradient codes (128 bytes)
+    RtStats* stats;           // nullptr = uninstrumented kernels
+};
+
+void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);
+void rt_launch_cell_depths(hipStream_t s, const float4* camera_results, float2* cells);
+// Trace the region [off, off+ext) in 32x32-pixel tiles; tiles t (row-major over the
+// region) with t % tile_stride == tile_first are traced (tile-cyclic sharding).
+void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t off_x,
+                           uint32_t off_y, uint32_t ext_x, uint32_t ext_y, uint32_t tile_first, uint32_t tile_stride);
+
+#define RT_TILE 32
+inline size_t rt_shard_tiles(int w, int h, int rank, int count)
+{
+    size_t tx = (size_t)(w + RT_TILE - 1) / RT_TILE, ty = (size_t)(h + RT_TILE - 1) / RT_TILE, total = tx * ty;
+    return total > (size_t)rank ? (total - (size_t)rank + (size_t)count - 1) / (size_t)count : 0;
+}
+// pack != 0: framebuffer tiles of shard `rank` -> packed (1024 px per tile); else packed -> framebuffer.
+void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack);

@@ -1,0 +1,905 @@
+// rt_runtime.cpp -- implementation of the C-ABI in include/frosttrace.h.
+//
+// Mirrors the reference's D3D11 adapter semantics (Adapters/ComputeDirect3D.cpp,
+// Adapters/ShaderVariableDirect3D.cpp, Adapters/DeviceDirect3D.cpp,
+// Adapters/TextureDirect3D.cpp) on HIP: a compute object owns a "shader" (here: a
+// precompiled gfx950 kernel family selected by file + landscape + macros) with
+// reflected cbuffer variables whose CPU shadows are uploaded lazily on run(),
+// structured/UAV arrays, and borrowed textures.  swap() replaces the current
+// shader and invalidates its variables, exactly as the reference does.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/frosttrace.h"
+#include "rt_kernels.h"
+#include "rt_math.h"
+#include "rt_noise.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(RT_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+std::mutex g_vfs_mu;
+std::vector<std::string> g_vfs;
+
+int landscape_from_vfs()
+{
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    static const char* names[] = {"nomadplains", "testing", "simple", "greenrocks"};
+    for (auto it = g_vfs.rbegin(); it != g_vfs.rend(); ++it) { // VFS.cpp:19-31 searches newest first
+        for (int l = 0; l < RT_NUM_LANDSCAPES; ++l) {
+            std::string n = names[l];
+            const std::string& p = *it;
+            if (p.size() >= n.size() && p.compare(p.size() - n.size(), n.size(), n) == 0) return l;
+        }
+        if (it->find("benchmark") != std::string::npos) return -2; // Media/benchmark/terrain.hlsl:39-40 does not compile
+    }
+    return RT_NOMADPLAINS; // main.cpp:87 default landscape
+}
+
+// Pinned staging buffer whose reuse waits for the previous async copy.
+struct Staging {
+    void* host = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+    ~Staging()
+    {
+        if (ev) (void)hipEventDestroy(ev);
+        if (host) (void)hipHostFree(host);
+    }
+    int upload(hipStream_t s, void* dst, const void* src, size_t n)
+    {
+        if (n > bytes) {
+            if (pending) HIP_TRY(hipEventSynchronize(ev));
+            if (host) HIP_TRY(hipHostFree(host));
+            HIP_TRY(hipHostMalloc(&host, n));
+            bytes = n;
+            pending = false;
+        }
+        if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (pending) HIP_TRY(hipEventSynchronize(ev));
+        memcpy(host, src, n);
+        HIP_TRY(hipMemcpyAsync(dst, host, n, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(ev, s));
+        pending = true;
+        return RT_OK;
+    }
+};
+
+} // namespace
+
+// ---------------------------------------------------------------------------
+struct rt_device_s {
+    int ordinal = 0, width = 0, height = 0;
+    unsigned flags = 0;
+    hipStream_t own_stream = nullptr, stream = nullptr;
+    uint32_t* fb8 = nullptr;
+    float4* fb32 = nullptr;
+    RtStats* stats = nullptr;
+    float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
+};
+
+struct rt_texture_s {
+    rt_device dev = nullptr;
+    int dims = 0, fmt = 0, w = 0, h = 0;
+    uint32_t* data = nullptr;
+};
+
+struct Shader;
+
+struct rt_variable_s {
+    std::string name;
+    int cbuf = 0, offset = 0, size = 0;
+    Shader* owner = nullptr;
+};
+
+struct rt_array_s {
+    std::string name;
+    int stride = 0;
+    bool uav = false;
+    unsigned elements = 0;
+    void* dev_ptr = nullptr;
+    std::vector<uint8_t> host;
+    Shader* owner = nullptr;
+    rt_device dev = nullptr;
+    Staging staging;
+};
+
+enum { KIND_CAMERARAYS = 0, KIND_TRACESCREEN = 1 };
+enum { CB_XTWEAK = 0, CB_FRAME = 1, CB_PERM = 2, CB_NOISE = 3, CB_DISPATCH = 4, CB_COUNT = 5 };
+static const int kCbSize[CB_COUNT] = {12, 84, 80, 2048, 8};
+
+struct Shader {
+    int kind = KIND_TRACESCREEN;
+    int landscape = RT_NOMADPLAINS;
+    int aa = 1, recording = 0, max_steps = 0;
+    int tx = 16, ty = 16, tz = 1;
+    bool has_cb[CB_COUNT] = {};
+    std::vector<uint8_t> cb[CB_COUNT];
+    bool cb_dirty = true;
+    std::vector<std::unique_ptr<rt_variable_s>> vars;
+    std::vector<std::unique_ptr<rt_array_s>> arrays;
+    rt_texture textures[16] = {};
+    // device-side state
+    RtConsts host_consts{};
+    RtConsts* d_consts = nullptr;
+    uint8_t* d_codes = nullptr;
+    Staging consts_staging, codes_staging;
+    int codes_ok = 0;
+
+    ~Shader()
+    {
+        if (d_consts) (void)hipFree(d_consts);
+        if (d_codes) (void)hipFree(d_codes);
+        for (auto& a : arrays)
+            if (a->dev_ptr) (void)hipFree(a->dev_ptr);
+    }
+    void add_var(const char* n, int cbuf, int off, int size)
+    {
+        auto v = std::make_unique<rt_variable_s>();
+        v->name = n;
+        v->cbuf = cbuf;
+        v->offset = off;
+        v->size = size;
+        v->owner = this;
+        vars.push_back(std::move(v));
+    }
+    void add_array(const char* n, int stride, bool uav, rt_device dev)
+    {
+        auto a = std::make_unique<rt_array_s>();
+        a->name = n;
+        a->stride = stride;
+        a->uav = uav;
+        a->owner = this;
+        a->dev = dev;
+        arrays.push_back(std::move(a));
+    }
+    rt_array_s* array(const char* n)
+    {
+        for (auto& a : arrays)
+            if (a->name == n) return a.get();
+        return nullptr;
+    }
+};
+
+struct rt_compute_s {
+    rt_device dev = nullptr;
+    Shader* shader = nullptr;
+    Shader* new_shader = nullptr;
+    ~rt_compute_s()
+    {
+        delete shader;
+        delete new_shader;
+    }
+};
+
+namespace {
+
+float rd_f(const std::vector<uint8_t>& b, int off)
+{
+    float f;
+    memcpy(&f, b.data() + off, 4);
+    return f;
+}
+
+// Build the constant block from the cbuffer shadows (tracing.hlsl:6-41,
+// sky.hlsl:1-16/:74-80, landscape color constants, antialiasing.hlsl:9-49).
+void build_consts(const Shader& s, const rt_device_s& dev, RtConsts& k)
+{
+    memset(&k, 0, sizeof(k));
+    const auto& fr = s.cb[CB_FRAME];
+    const auto& pm = s.cb[CB_PERM];
+    const auto& xt = s.cb[CB_XTWEAK];
+    for (int i = 0; i < 4; ++i) k.eye[i] = s.has_cb[CB_FRAME] ? rd_f(fr, 4 * i) : 0.0f;
+    // column_major cbuffer packing: HLSL M[r][c] = mem[c*4 + r]
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) k.view_inverse[4 * r + c] = s.has_cb[CB_FRAME] ? rd_f(fr, 16 + 4 * (4 * c + r)) : 0.0f;
+    k.screen[0] = s.has_cb[CB_PERM] ? rd_f(pm, 0) : 0.0f;
+    k.screen[1] = s.has_cb[CB_PERM] ? rd_f(pm, 4) : 0.0f;
+    float proj[16];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) proj[4 * r + c] = s.has_cb[CB_PERM] ? rd_f(pm, 16 + 4 * (4 * c + r)) : 0.0f;
+    k.proj11 = proj[0];
+    k.proj22 = proj[5];
+    k.rcp_w = rtm::rcp(k.screen[0]);
+    k.rcp_h = rtm::rcp(k.screen[1]);
+    for (int i = 0; i < 3; ++i) k.sun[i] = s.has_cb[CB_XTWEAK] ? rd_f(xt, 4 * i) : 0.0f;
+
+    k.step_factor = s.recording ? 1.001f : 1.009f;
+    k.one_minus_step_factor = (float)(1.0 - (double)k.step_factor);
+    k.density_factor = s.recording ? 0.15f : 0.35f;
+    k.min_limit = (float)((double)0.02f * (double)0.03f);
+    for (int n = 1; n <= RT_NP_OCTAVES; ++n) {
+        float S = rtm::pow(1.96f, (float)n);
+        k.np_scale[n] = S;
+        k.np_scale_y[n] = S * 0.35f;
+        k.np_rcp[n] = rtm::rcp(S);
+    }
+    k.np_expo = 0.68f + 0.1f;
+    for (int n = 1; n <= RT_COL_OCTAVES; ++n) {
+        float S = rtm::pow(2.03f, (float)n);
+        k.col_scale[n] = S;
+        k.col_rcp[n] = rtm::rcp(S);
+    }
+    switch (s.landscape) {
+    case RT_TESTING: k.albedo[0] = 0.6f; k.albedo[1] = 0.5f; k.albedo[2] = 0.3f; k.albedo[3] = 0.1f; break;
+    case RT_GREENROCKS: k.albedo[0] = 0.6f; k.albedo[1] = 0.7f; k.albedo[2] = 0.3f; k.albedo[3] = 0.1f; break;
+    default:
+        k.albedo[0] = (float)(193.0 / 255.0);
+        k.albedo[1] = (float)(131.0 / 255.0);
+        k.albedo[2] = (float)(92.0 / 255.0);
+        k.albedo[3] = 0.2f;
+        break;
+    }
+    const float shc[3] = {0.08f, 0.12f, 0.14f};
+    for (int i = 0; i < 3; ++i) {
+        k.shadow_color[i] = shc[i];
+        k.one_minus_shadow[i] = (float)(1.0 - (double)shc[i]);
+    }
+    k.rcp200 = rtm::rcp(200.0f);
+
+    // sky.hlsl constants (folded in double, rounded once)
+    const double wl[3] = {0.650f, 0.570f, 0.475f};
+    const double kr = 0.003f, km = 0.0025f, pi = 3.14159265f, eSun = 12.0f;
+    float outerRadius = (float)(200.0 * (double)1.025f);
+    float fScale = (float)(1.0 / ((double)outerRadius - 200.0));
+    float sos = (float)((double)fScale / (double)0.19f);
+    float fKrESun = (float)(eSun * kr), fKmESun = (float)(eSun * km);
+    float fKr4PI = (float)(kr * 4.0 * pi), fKm4PI = (float)(km * 4.0 * pi);
+    for (int i = 0; i < 3; ++i) {
+        float wl4 = (float)std::pow(wl[i], 4.0);
+        float inv = (float)(1.0 / (double)wl4);
+        k.sky_att[i] = (float)((double)inv * (double)fKr4PI + (double)fKm4PI);
+        k.sky_mie_k[i] = (float)((double)inv * (double)fKrESun);
+    }
+    k.sky_km_esun = fKmESun;
+    float g = -0.99f, g2 = g * g;
+    k.sky_mie_a = (float)(1.5 * ((1.0 - (double)g2) / (2.0 + (double)g2)));
+    k.sky_one_plus_g2 = (float)(1.0 + (double)g2);
+    k.sky_two_g = (float)(2.0 * (double)g);
+    k.sky_rcp_samples = (float)(1.0 / 3.0);
+    k.sky_fscale = fScale;
+    k.sky_sos = sos;
+    // eye-dependent (getRayleighMieColor prologue, sky.hlsl:88-100)
+    float camHeight = rtm::fma(k.eye[1], 0.001f, 200.0f);
+    camHeight = rtm::max(camHeight, 0.0f);
+    k.sky_dist_to_top = outerRadius - camHeight;
+    k.sky_start[0] = k.eye[0] * 0.001f;
+    k.sky_start[1] = camHeight;
+    k.sky_start[2] = k.eye[2] * 0.001f;
+    rtm::f3 sn = rtm::normalize(rtm::mk(k.sky_start[0], k.sky_start[1], k.sky_start[2]));
+    k.sky_start_n[0] = sn.x;
+    k.sky_start_n[1] = sn.y;
+    k.sky_start_n[2] = sn.z;
+    k.sky_depth0 = rtm::exp(sos * (200.0f - camHeight));
+
+    static const float off1[1][2] = {{0, 0}};
+    static const float off2[2][2] = {{4, 4}, {-4, -4}};
+    static const float off4[4][2] = {{-2, -6}, {6, -2}, {-6, 2}, {2, 6}};
+    static const float off8[8][2] = {{1, -3}, {-1, 3}, {5, 1}, {-3, -5}, {-5, 5}, {-7, -1}, {3, 7}, {7, -7}};
+    static const float off16[16][2] = {{1, 1}, {-1, 3}, {-3, 2}, {4, -1}, {-5, -2}, {2, 5}, {5, 3}, {3, -5},
+                                       {-2, 6}, {0, -7}, {-4, -6}, {-6, 4}, {-8, 0}, {7, -4}, {6, 7}, {-7, -8}};
+    const float(*offs)[2] = off1;
+    switch (s.aa) {
+    case 2: offs = off2; break;
+    case 4: offs = off4; break;
+    case 8: offs = off8; break;
+    case 16: offs = off16; break;
+    default: break;
+    }
+    for (int a = 0; a < s.aa; ++a) {
+        k.aa_off[a][0] = offs[a][0] * (1.0f / 16.0f);
+        k.aa_off[a][1] = offs[a][1] * (1.0f / 16.0f);
+    }
+    k.aa_samples = s.aa;
+    k.landscape = s.landscape;
+    k.max_steps = s.max_steps;
+    k.width = dev.width;
+    k.height = dev.height;
+}
+
+// Gradient codes (rt_shader.h NoiseView) from CBNoise.permGradients.  Only the
+// canonical {-1,0,1}^3 two-non-zero gradient set of Noise.cpp:6-24 is accepted.
+int build_codes(const std::vector<uint8_t>& grad_bytes, uint8_t out[128])
+{
+    uint8_t code[128];
+    for (int i = 0; i < 128; ++i) {
+        float g[3];
+        memcpy(g, grad_bytes.data() + 16 * i, 12);
+        int axes[3], n = 0;
+        for (int a = 0; a < 3; ++a) {
+            if (g[a] == 0.0f) continue;
+            if (g[a] != 1.0f && g[a] != -1.0f) n = 99;
+            if (n < 3) axes[n] = a;
+            ++n;
+        }
+        if (n != 2) return fail(RT_ERR_UNSUPPORTED, "permGradients[%d] is not a canonical noise gradient", i);
+        uint8_t c = 0;
+        if (axes[0] == 1) c |= 1u;
+        if (axes[1] == 2) c |= 2u;
+        if (g[axes[0]] < 0.0f) c |= 4u;
+        if (g[axes[1]] < 0.0f) c |= 8u;
+        code[i] = c;
+    }
+    for (int i = 0; i < 128; ++i) out[i] = (uint8_t)(code[i] | (code[(i + 1) & 127] << 4));
+    return RT_OK;
+}
+
+int sync_shader(rt_device dev, Shader* s)
+{
+    if (!s->d_consts) HIP_TRY(hipMalloc(&s->d_consts, sizeof(RtConsts)));
+    if (!s->d_codes) HIP_TRY(hipMalloc(&s->d_codes, 128));
+    if (s->cb_dirty) {
+        build_consts(*s, *dev, s->host_consts);
+        int rc = s->consts_staging.upload(dev->stream, s->d_consts, &s->host_consts, sizeof(RtConsts));
+        if (rc) return rc;
+        uint8_t codes[128];
+        rc = build_codes(s->cb[CB_NOISE], codes);
+        if (rc) {
+            s->codes_ok = 0;
+            return rc;
+        }
+        rc = s->codes_staging.upload(dev->stream, s->d_codes, codes, 128);
+        if (rc) return rc;
+        s->codes_ok = 1;
+        s->cb_dirty = false;
+    }
+    if (!s->codes_ok) return fail(RT_ERR_STATE, "noise gradients not set");
+    return RT_OK;
+}
+
+RtLaunch make_launch(rt_device dev, Shader* s)
+{
+    RtLaunch a;
+    a.stream = dev->stream;
+    a.landscape = s->landscape;
+    a.consts = s->d_consts;
+    a.perm2d = s->textures[0] ? s->textures[0]->data : nullptr;
+    a.codes2 = s->d_codes;
+    a.stats = (dev->flags & RT_DEVICE_STATS) ? dev->stats : nullptr;
+    return a;
+}
+
+int check_texture(Shader* s)
+{
+    rt_texture t = s->textures[0];
+    if (!t || !t->data) return fail(RT_ERR_STATE, "texture stage 0 (texPerm2D) not bound");
+    if (t->w != 128 || t->h != 128 || t->fmt != RT_FORMAT_R8G8B8A8_UINT)
+        return fail(RT_ERR_UNSUPPORTED, "texPerm2D must be a 128x128 R8G8B8A8_UINT texture");
+    return RT_OK;
+}
+
+} // namespace
+
+// ===========================================================================
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_vfs_add_path(const char* path)
+{
+    if (!path) return fail(RT_ERR_INVALID, "null path");
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    g_vfs.emplace_back(path);
+    return RT_OK;
+}
+int rt_vfs_clear(void)
+{
+    std::lock_guard<std::mutex> lk(g_vfs_mu);
+    g_vfs.clear();
+    return RT_OK;
+}
+
+// ---- device ---------------------------------------------------------------
+int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_device* out)
+{
+    if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
+    *out = nullptr;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (ordinal < 0 || ordinal >= n) return fail(RT_ERR_INVALID, "GPU ordinal %d out of range (%d devices)", ordinal, n);
+    HIP_TRY(hipSetDevice(ordinal));
+    auto d = std::make_unique<rt_device_s>();
+    d->ordinal = ordinal;
+    d->width = width;
+    d->height = height;
+    d->flags = flags;
+    HIP_TRY(hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking));
+    d->stream = d->own_stream;
+    HIP_TRY(hipMalloc(&d->fb8, (size_t)width * height * 4));
+    HIP_TRY(hipMemset(d->fb8, 0, (size_t)width * height * 4));
+    if (flags & RT_DEVICE_FLOAT_OUTPUT) {
+        HIP_TRY(hipMalloc(&d->fb32, (size_t)width * height * 16));
+        HIP_TRY(hipMemset(d->fb32, 0, (size_t)width * height * 16));
+    }
+    HIP_TRY(hipMalloc(&d->stats, sizeof(RtStats)));
+    HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
+    HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
+    *out = d.release();
+    return RT_OK;
+}
+
+void rt_device_destroy(rt_device d)
+{
+    if (!d) return;
+    (void)hipSetDevice(d->ordinal);
+    if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
+    if (d->stream && d->stream != d->own_stream) (void)hipStreamSynchronize(d->stream);
+    if (d->fb8) (void)hipFree(d->fb8);
+    if (d->fb32) (void)hipFree(d->fb32);
+    if (d->stats) (void)hipFree(d->stats);
+    if (d->scratch_cam) (void)hipFree(d->scratch_cam);
+    if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
+    delete d;
+}
+
+int rt_device_present(rt_device d)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_device_flush(rt_device d)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    // HIP submits at launch; flush only surfaces asynchronous launch errors.
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_device_synchronize(rt_device d)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}
+
+int rt_device_readback(rt_device d, void* dst, size_t row_pitch)
+{
+    if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
+    if (row_pitch == 0) row_pitch = (size_t)d->width * 4;
+    if (row_pitch < (size_t)d->width * 4) return fail(RT_ERR_INVALID, "row pitch smaller than a row");
+    HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->fb8, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
+                             hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}
+
+int rt_device_readback_float(rt_device d, float* dst)
+{
+    if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
+    if (!d->fb32) return fail(RT_ERR_STATE, "device created without RT_DEVICE_FLOAT_OUTPUT");
+    HIP_TRY(hipMemcpyAsync(dst, d->fb32, (size_t)d->width * d->height * 16, hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}
+
+int rt_device_size(rt_device d, int* w, int* h)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (w) *w = d->width;
+    if (h) *h = d->height;
+    return RT_OK;
+}
+
+void* rt_device_framebuffer(rt_device d) { return d ? (void*)d->fb8 : nullptr; }
+void* rt_device_stream(rt_device d) { return d ? (void*)d->stream : nullptr; }
+
+int rt_device_set_stream(rt_device d, void* s)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    d->stream = s ? (hipStream_t)s : d->own_stream;
+    return RT_OK;
+}
+
+int rt_device_stats(rt_device d, rt_stats* out, int reset)
+{
+    if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
+    RtStats h;
+    HIP_TRY(hipMemcpyAsync(&h, d->stats, sizeof(h), hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    out->primary_steps = h.primary_steps;
+    out->shadow_steps = h.shadow_steps;
+    out->prepass_steps = h.prepass_steps;
+    out->hits = h.hits;
+    if (reset) HIP_TRY(hipMemsetAsync(d->stats, 0, sizeof(RtStats), d->stream));
+    return RT_OK;
+}
+
+// ---- textures -------------------------------------------------------------
+int rt_texture_create(rt_device d, rt_texture* out)
+{
+    if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
+    auto t = new rt_texture_s();
+    t->dev = d;
+    *out = t;
+    return RT_OK;
+}
+
+int rt_texture_init(rt_texture t, int dims, int fmt, int w, int h, const void* data, int binding, int cpu)
+{
+    (void)binding;
+    (void)cpu;
+    if (!t || !data || w <= 0) return fail(RT_ERR_INVALID, "bad texture arguments");
+    if (dims != RT_TEXTURE_2D) return fail(RT_ERR_UNSUPPORTED, "only 2D textures are used on the hot path");
+    if (fmt == RT_FORMAT_UNKNOWN) return fail(RT_ERR_UNSUPPORTED, "unknown texture format");
+    if (t->data) HIP_TRY(hipFree(t->data));
+    size_t bytes = (size_t)w * h * 4;
+    HIP_TRY(hipMalloc(&t->data, bytes));
+    HIP_TRY(hipMemcpy(t->data, data, bytes, hipMemcpyHostToDevice));
+    t->dims = dims;
+    t->fmt = fmt;
+    t->w = w;
+    t->h = h;
+    return RT_OK;
+}
+
+void rt_texture_destroy(rt_texture t)
+{
+    if (!t) return;
+    if (t->data) (void)hipFree(t->data);
+    delete t;
+}
+
+// ---- compute --------------------------------------------------------------
+int rt_compute_create(rt_device d, rt_compute* out)
+{
+    if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
+    auto c = new rt_compute_s();
+    c->dev = d;
+    *out = c;
+    return RT_OK;
+}
+
+void rt_compute_destroy(rt_compute c)
+{
+    if (!c) return;
+    (void)hipStreamSynchronize(c->dev->stream);
+    delete c;
+}
+
+int rt_compute_load(rt_compute c, const char* directory, const char* file, const char* entry, int tx, int ty, int tz,
+                    const char* const* mn, const char* const* mv, int n)
+{
+    (void)directory;
+    if (!c || !file) return fail(RT_ERR_INVALID, "bad arguments");
+    if (entry && strcmp(entry, "CSMain") != 0) return fail(RT_ERR_NOT_FOUND, "entry point %s not found", entry);
+    std::string f = file;
+    int kind;
+    if (f == "tracescreen.hlsl") kind = KIND_TRACESCREEN;
+    else if (f == "camerarays.hlsl") kind = KIND_CAMERARAYS;
+    else return fail(RT_ERR_NOT_FOUND, "shader file %s not found", file);
+    int land = landscape_from_vfs();
+    if (land == -2) return fail(RT_ERR_NOT_FOUND, "benchmark landscape does not compile (terrain.hlsl:39-40)");
+    if (tx <= 0 || ty <= 0 || tz <= 0 || tx * ty * tz > 1024)
+        return fail(RT_ERR_INVALID, "thread group %dx%dx%d exceeds 1024 threads", tx, ty, tz);
+    auto s = std::make_unique<Shader>();
+    s->kind = kind;
+    s->landscape = land;
+    s->tx = tx;
+    s->ty = ty;
+    s->tz = tz;
+    for (int i = 0; i < n; ++i) {
+        if (!mn || !mv || !mn[i] || !mv[i]) continue;
+        std::string k = mn[i], v = mv[i];
+        if (k == "RECORDING") s->recording = atoi(v.c_str()) != 0;
+        else if (k == "AA_SAMPLES") {
+            int aa = atoi(v.c_str());
+            if (aa != 1 && aa != 2 && aa != 4 && aa != 8 && aa != 16)
+                return fail(RT_ERR_INVALID, "Unsupported AA sample count (antialiasing.hlsl:47)");
+            s->aa = aa;
+        } else if (k == "RT_MAX_STEPS") s->max_steps = std::max(0, atoi(v.c_str()));
+    }
+    // Reflection (what fxc reports for these shaders; tracing.hlsl:6-22, noise.hlsl:130-133,
+    // tracescreen.hlsl:8-14, camerarays.hlsl:3).
+    if (kind == KIND_TRACESCREEN) {
+        s->has_cb[CB_XTWEAK] = s->has_cb[CB_FRAME] = s->has_cb[CB_PERM] = s->has_cb[CB_NOISE] = s->has_cb[CB_DISPATCH] = true;
+        s->add_var("SunDirection", CB_XTWEAK, 0, 12);
+        s->add_var("ThreadOffset", CB_DISPATCH, 0, 8);
+        s->add_array("CellDistance", 8, false, c->dev);
+    } else {
+        s->has_cb[CB_FRAME] = s->has_cb[CB_PERM] = s->has_cb[CB_NOISE] = true;
+        s->add_array("CameraResults", 16, true, c->dev);
+    }
+    s->add_var("Eye", CB_FRAME, 0, 16);
+    s->add_var("ViewInverse", CB_FRAME, 16, 64);
+    s->add_var("Time", CB_FRAME, 80, 4);
+    s->add_var("ScreenSize", CB_PERM, 0, 8);
+    s->add_var("Projection", CB_PERM, 16, 64);
+    s->add_var("permGradients", CB_NOISE, 0, 2048);
+    for (int i = 0; i < CB_COUNT; ++i)
+        if (s->has_cb[i]) s->cb[i].assign(kCbSize[i], 0); // ConstantBufferD3D zero-fills (ShaderVariableDirect3D.cpp:10-11)
+    delete c->new_shader;
+    c->new_shader = s.release();
+    return RT_OK;
+}
+
+int rt_compute_swap(rt_compute c)
+{
+    if (!c) return fail(RT_ERR_INVALID, "null compute");
+    if (!c->new_shader) return 0;
+    if (c->shader) {
+        (void)hipStreamSynchronize(c->dev->stream); // kernels may still read the old shader's buffers
+        delete c->shader;
+    }
+    c->shader = c->new_shader;
+    c->new_shader = nullptr;
+    return 1;
+}
+
+int rt_compute_thread_size(rt_compute c, int* x, int* y, int* z)
+{
+    if (!c) return fail(RT_ERR_INVALID, "null compute");
+    Shader* s = c->shader ? c->shader : c->new_shader;
+    if (!s) return fail(RT_ERR_STATE, "no shader");
+    if (x) *x = s->tx;
+    if (y) *y = s->ty;
+    if (z) *z = s->tz;
+    return RT_OK;
+}
+
+rt_variable rt_compute_get_variable(rt_compute c, const char* name)
+{
+    if (!c || !c->shader || !name) return nullptr;
+    for (auto& v : c->shader->vars)
+        if (v->name == name) return v.get();
+    return nullptr;
+}
+
+rt_array rt_compute_get_array(rt_compute c, const char* name)
+{
+    if (!c || !c->shader || !name) return nullptr;
+    return c->shader->array(name);
+}
+
+void* rt_compute_get_buffer(rt_compute c, const char* name)
+{
+    (void)c;
+    (void)name;
+    return nullptr; // ComputeDirect3D.cpp:138-141: CBuffer == 0 masks every resource out
+}
+
+int rt_compute_set_texture(rt_compute c, int stage, rt_texture t)
+{
+    if (!c || stage < 0 || stage >= 16) return fail(RT_ERR_INVALID, "bad arguments");
+    if (!c->shader) return fail(RT_ERR_STATE, "no current shader");
+    c->shader->textures[stage] = t;
+    return RT_OK;
+}
+
+int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
+{
+    if (!c) return fail(RT_ERR_INVALID, "null compute");
+    Shader* s = c->shader;
+    if (!s) return RT_OK; // ComputeDirect3D.cpp:532
+    rt_device dev = c->dev;
+    int rc = check_texture(s);
+    if (rc) return rc;
+    rc = sync_shader(dev, s);
+    if (rc) return rc;
+    RtLaunch a = make_launch(dev, s);
+    if (dz == 0) return RT_OK;
+    if (s->kind == KIND_CAMERARAYS) {
+        rt_array_s* cr = s->array("CameraResults");
+        if (!cr->dev_ptr || cr->elements < 1024) return fail(RT_ERR_STATE, "CameraResults not created with 1024 elements");
+        uint32_t ex = std::min<uint64_t>((uint64_t)dx * s->tx, RT_CAMERA_RES);
+        uint32_t ey = std::min<uint64_t>((uint64_t)dy * s->ty, RT_CAMERA_RES);
+        if (ex == RT_CAMERA_RES && ey == RT_CAMERA_RES) {
+            rt_launch_camerarays(a, (float4*)cr->dev_ptr);
+        } else {
+            // partial prepass dispatch: trace into scratch, copy the covered cells
+            rt_launch_camerarays(a, dev->scratch_cam);
+            HIP_TRY(hipMemcpy2DAsync(cr->dev_ptr, RT_CAMERA_RES * 16, dev->scratch_cam, RT_CAMERA_RES * 16, ex * 16, ey,
+                                     hipMemcpyDeviceToDevice, dev->stream));
+        }
+    } else {
+        rt_array_s* cd = s->array("CellDistance");
+        if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
+        uint32_t off[2];
+        memcpy(off, s->cb[CB_DISPATCH].data(), 8);
+        uint64_t ex = (uint64_t)dx * s->tx, ey = (uint64_t)dy * s->ty;
+        ex = std::min<uint64_t>(ex, dev->width > (int)off[0] ? dev->width - off[0] : 0);
+        ey = std::min<uint64_t>(ey, dev->height > (int)off[1] ? dev->height - off[1] : 0);
+        rt_launch_tracescreen(a, (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, off[0], off[1], (uint32_t)ex,
+                              (uint32_t)ey, 0, 1);
+    }
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+// ---- variables / arrays ---------------------------------------------------
+int rt_variable_write(rt_variable v, const void* data)
+{
+    if (!v || !data) return fail(RT_ERR_INVALID, "bad arguments");
+    Shader* s = v->owner;
+    memcpy(s->cb[v->cbuf].data() + v->offset, data, v->size);
+    if (v->cbuf != CB_DISPATCH) s->cb_dirty = true; // ThreadOffset is a launch argument
+    return RT_OK;
+}
+size_t rt_variable_size(rt_variable v) { return v ? (size_t)v->size : 0; }
+const char* rt_variable_name(rt_variable v) { return v ? v->name.c_str() : nullptr; }
+
+int rt_array_create(rt_array a, unsigned elements)
+{
+    if (!a || elements == 0) return fail(RT_ERR_INVALID, "bad arguments");
+    if (a->dev_ptr) return fail(RT_ERR_STATE, "array %s already created", a->name.c_str()); // UAVBufferD3D::create
+    size_t bytes = (size_t)elements * a->stride;
+    HIP_TRY(hipMalloc(&a->dev_ptr, bytes));
+    HIP_TRY(hipMemset(a->dev_ptr, 0, bytes));
+    a->elements = elements;
+    if (a->uav) a->host.assign(bytes, 0);
+    return RT_OK;
+}
+
+void* rt_array_map(rt_array a)
+{
+    if (!a) {
+        fail(RT_ERR_INVALID, "null array");
+        return nullptr;
+    }
+    if (!a->uav) {
+        fail(RT_ERR_UNSUPPORTED, "map not supported on SRV array %s", a->name.c_str());
+        return nullptr;
+    }
+    if (!a->dev_ptr) {
+        fail(RT_ERR_STATE, "array %s not created", a->name.c_str());
+        return nullptr;
+    }
+    hipStream_t s = a->dev->stream;
+    if (hipMemcpyAsync(a->host.data(), a->dev_ptr, a->host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess) {
+        fail(RT_ERR_HIP, "map readback failed");
+        return nullptr;
+    }
+    return a->host.data();
+}
+
+int rt_array_unmap(rt_array a)
+{
+    if (!a) return fail(RT_ERR_INVALID, "null array");
+    if (!a->uav) return fail(RT_ERR_UNSUPPORTED, "unmap not supported on SRV array %s", a->name.c_str());
+    if (!a->dev_ptr) return fail(RT_ERR_STATE, "array not created");
+    return a->staging.upload(a->dev->stream, a->dev_ptr, a->host.data(), a->host.size());
+}
+
+int rt_array_write(rt_array a, const void* data)
+{
+    if (!a || !data) return fail(RT_ERR_INVALID, "bad arguments");
+    if (a->uav) return fail(RT_ERR_UNSUPPORTED, "write not supported on UAV array %s", a->name.c_str());
+    if (!a->dev_ptr) return fail(RT_ERR_STATE, "array %s not created", a->name.c_str());
+    return a->staging.upload(a->dev->stream, a->dev_ptr, data, (size_t)a->elements * a->stride);
+}
+
+size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
+void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
+
+// ---- Terrain::render on the device -------------------------------------------
+int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
+{
+    if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
+    if (!cam->shader || !scr->shader) return fail(RT_ERR_STATE, "both computes need a current shader (swap)");
+    if (cam->shader->kind != KIND_CAMERARAYS || scr->shader->kind != KIND_TRACESCREEN)
+        return fail(RT_ERR_INVALID, "expected (camerarays, tracescreen)");
+    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
+    rt_device dev = cam->dev;
+    int rc;
+    if ((rc = check_texture(cam->shader)) || (rc = check_texture(scr->shader))) return rc;
+    if ((rc = sync_shader(dev, cam->shader)) || (rc = sync_shader(dev, scr->shader))) return rc;
+    rt_array_s* cr = cam->shader->array("CameraResults");
+    rt_array_s* cd = scr->shader->array("CellDistance");
+    if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
+    float4* crp = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : dev->scratch_cam;
+    rt_launch_camerarays(make_launch(dev, cam->shader), crp);
+    rt_launch_cell_depths(dev->stream, crp, (float2*)cd->dev_ptr);
+    rt_launch_tracescreen(make_launch(dev, scr->shader), (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, 0, 0,
+                          (uint32_t)dev->width, (uint32_t)dev->height, (uint32_t)shard_rank, (uint32_t)shard_count);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+size_t rt_shard_bytes(rt_device d, int rank, int count)
+{
+    if (!d || count < 1 || rank < 0 || rank >= count) return 0;
+    size_t tiles = rt_shard_tiles(d->width, d->height, rank, count);
+    return tiles * RT_TILE * RT_TILE * 4;
+}
+
+int rt_shard_pack(rt_device d, int rank, int count, void* dst)
+{
+    if (!d || !dst || count < 1 || rank < 0 || rank >= count) return fail(RT_ERR_INVALID, "bad arguments");
+    rt_launch_shard_copy(d->stream, d->fb8, (uint32_t*)dst, d->width, d->height, rank, count, 1);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_shard_unpack(rt_device d, int rank, int count, const void* src)
+{
+    if (!d || !src || count < 1 || rank < 0 || rank >= count) return fail(RT_ERR_INVALID, "bad arguments");
+    rt_launch_shard_copy(d->stream, d->fb8, (uint32_t*)src, d->width, d->height, rank, count, 0);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_noise_generate(uint32_t seed, int rand_kind, uint8_t* perm2d, float* grad)
+{
+    if (!perm2d || !grad) return fail(RT_ERR_INVALID, "null output");
+    if (rand_kind != 0 && rand_kind != 1) return fail(RT_ERR_INVALID, "rand_kind must be 0 (MSVC) or 1 (glibc)");
+    rt_noise::generate(seed, rand_kind, perm2d, grad);
+    return RT_OK;
+}
+
+} // extern "C"
+
+// ---- host-side Terrain helpers (engine code that stays on the CPU in the
+// reference's flow; used by the compatibility render path) ----------------
+namespace {
+float host_depth(const float* cr, int x, int y)
+{
+    if (x < 0) x = 0;
+    if (x >= RT_CAMERA_RES) x = RT_CAMERA_RES - 1;
+    if (y < 0) y = 0;
+    if (y >= RT_CAMERA_RES) y = RT_CAMERA_RES - 1;
+    return cr[(y * RT_CAMERA_RES + x) * 4 + 3];
+}
+float host_depth_interp(const float* cr, int x, int y)
+{
+    if (x < 0) { float m = host_depth(cr, x + 1, y); float d = host_depth(cr, x + 2, y) - m; return m - d; }
+    if (x >= RT_CAMERA_RES) { float m = host_depth(cr, x - 1, y); float d = host_depth(cr, x - 2, y) - m; return m - d; }
+    if (y < 0) { float m = host_depth(cr, x, y + 1); float d = host_depth(cr, x, y + 2) - m; return m - d; }
+    if (y >= RT_CAMERA_RES) { float m = host_depth(cr, x, y - 1); float d = host_depth(cr, x, y - 2) - m; return m - d; }
+    return host_depth(cr, x, y);
+}
+} // namespace
+
+extern "C" int rt_terrain_set_target_depths(const float* cr, float* cells)
+{
+    // Terrain.cpp:398-439 (Terrain::getDepth/getDepthInterp :356-396)
+    if (!cr || !cells) return fail(RT_ERR_INVALID, "null arguments");
+    for (int x = 0; x < RT_CAMERA_RES * RT_CAMERA_RES; ++x) {
+        int xpos = x % RT_CAMERA_RES, ypos = x / RT_CAMERA_RES;
+        float dmin = host_depth_interp(cr, xpos, ypos);
+        float dmax = dmin;
+        for (int xp = -2; xp <= 2; ++xp)
+            for (int yp = -2; yp <= 2; ++yp) {
+                float d = host_depth_interp(cr, xpos + xp, ypos + yp);
+                dmin = std::min(d, dmin);
+                dmax = std::max(d, dmax);
+            }
+        dmin = dmin * 0.96f - 0.01f;
+        dmax = dmax * 1.22f + 0.4f;
+        dmin = std::max(RT_CAMERA_NEAR, dmin);
+        dmax = std::min(RT_CAMERA_FAR, dmax);
+        cells[2 * x] = dmin;
+        cells[2 * x + 1] = dmax;
+    }
+    return RT_OK;
+}

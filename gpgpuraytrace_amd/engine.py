@@ -1,0 +1,414 @@
+"""Host-side mirror of the reference engine's dispatch-and-readback surface over
+the C-ABI (include/frosttrace.h).
+
+Class/method names follow the reference interfaces so an engine-side caller
+reads the same:  DeviceFactory.construct -> Device (IDevice, Factories/IDevice.h),
+Device.create_compute -> Compute (ICompute, Factories/ICompute.h), ShaderVariable /
+ShaderArray (Graphics/IShaderVariable.h), Texture (Factories/ITexture.h), Noise
+(Graphics/Noise.cpp), Terrain (Graphics/Terrain.cpp).  Errors follow the
+reference: bool returns / None for missing names; HIP failures raise.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _native
+from ._native import check, lib
+
+CAMERA_VIEW_RES = 32    # Gameplay/Flyby.h:6
+CAMERA_THREAD_RES = 16  # Gameplay/Flyby.h:7
+
+
+class DeviceAPI:
+    NONE, DIRECT3D, OPENGL, HIP = 0, 1, 2, 3   # IDevice.h:5-10 + the HIP slot
+
+
+def vfs_add_path(path):
+    """VFS::addPath (Common/VFS.cpp); "Media/<landscape>" selects the landscape."""
+    check(lib().rt_vfs_add_path(path.encode()), "vfs_add_path")
+
+
+def vfs_clear():
+    lib().rt_vfs_clear()
+
+
+class ShaderVariable:
+    """IShaderVariable: write() copies exactly the reflected size into the cbuffer shadow."""
+
+    def __init__(self, handle, compute):
+        self._h, self._compute = handle, compute
+        self.name = lib().rt_variable_name(handle).decode()
+        self.size = int(lib().rt_variable_size(handle))
+
+    def write(self, data):
+        buf = bytes(np.ascontiguousarray(data).tobytes() if not isinstance(data, (bytes, bytearray)) else data)
+        if len(buf) < self.size:
+            raise ValueError(f"{self.name}: need {self.size} bytes, got {len(buf)}")
+        check(lib().rt_variable_write(self._h, buf), f"write {self.name}")
+
+
+class ShaderArray:
+    """IShaderArray: create(n), map()/unmap() on UAV arrays, write() on SRV arrays."""
+
+    def __init__(self, handle, compute):
+        self._h, self._compute = handle, compute
+        self.stride = int(lib().rt_array_stride(handle))
+        self.elements = 0
+
+    def create(self, elements):
+        rc = lib().rt_array_create(self._h, int(elements))
+        if rc == 0:
+            self.elements = int(elements)
+        return rc == 0
+
+    def map(self):
+        """Blocking device->host copy; returns a float32 view (elements x stride/4) or None."""
+        p = lib().rt_array_map(self._h)
+        if not p:
+            return None
+        n = self.elements * self.stride // 4
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_float)), shape=(n,)).reshape(self.elements, -1)
+
+    def unmap(self):
+        check(lib().rt_array_unmap(self._h), "unmap")
+
+    def write(self, data):
+        a = np.ascontiguousarray(data)
+        if a.nbytes < self.elements * self.stride:
+            raise ValueError("array write smaller than the array")
+        return lib().rt_array_write(self._h, a.ctypes.data) == 0
+
+    def device_pointer(self):
+        return lib().rt_array_device_pointer(self._h)
+
+
+class Texture:
+    """ITexture over a device allocation."""
+
+    def __init__(self, device):
+        h = C.c_void_p()
+        check(lib().rt_texture_create(device._h, C.byref(h)), "texture_create")
+        self._h = h.value
+
+    def create(self, dimensions, fmt, width, height, data, binding=0, cpu_flags=0):
+        a = np.ascontiguousarray(data)
+        return lib().rt_texture_init(self._h, dimensions, fmt, width, height, a.ctypes.data, binding, cpu_flags) == 0
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rt_texture_destroy(self._h)
+        except Exception:
+            pass
+
+
+class Compute:
+    """ICompute (Factories/ICompute.h:16-59)."""
+
+    def __init__(self, device):
+        self.device = device
+        h = C.c_void_p()
+        check(lib().rt_compute_create(device._h, C.byref(h)), "compute_create")
+        self._h = h.value
+        self.thread_size = (0, 0, 0)
+
+    def create(self, directory, file_name, main, thread_size, macros=()):
+        names = (C.c_char_p * max(1, len(macros)))(*[k.encode() for k, _ in macros])
+        vals = (C.c_char_p * max(1, len(macros)))(*[str(v).encode() for _, v in macros])
+        tx, ty, tz = thread_size
+        rc = lib().rt_compute_load(self._h, directory.encode(), file_name.encode(), main.encode(), tx, ty, tz,
+                                   names, vals, len(macros))
+        if rc == 0:
+            self.thread_size = (tx, ty, tz)
+        return rc == 0
+
+    def swap(self):
+        return lib().rt_compute_swap(self._h) == 1
+
+    def run(self, dx, dy, dz=1):
+        check(lib().rt_compute_run(self._h, dx, dy, dz), "run")
+
+    def get_variable(self, name):
+        h = lib().rt_compute_get_variable(self._h, name.encode())
+        return ShaderVariable(h, self) if h else None
+
+    def get_array(self, name):
+        h = lib().rt_compute_get_array(self._h, name.encode())
+        return ShaderArray(h, self) if h else None
+
+    def get_buffer(self, name):
+        return None  # the reference's getBuffer always returns nullptr (ComputeDirect3D.cpp:138-141)
+
+    def set_texture(self, stage, texture):
+        check(lib().rt_compute_set_texture(self._h, stage, texture._h if texture else None), "set_texture")
+
+    def get_thread_size(self):
+        return self.thread_size
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().rt_compute_destroy(self._h)
+        except Exception:
+            pass
+
+
+class Device:
+    """IDevice over rt_device (DeviceDirect3D's role)."""
+
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False):
+        self.width, self.height, self.gpu = int(width), int(height), int(gpu)
+        self.flags = (_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
+        self._h = None
+
+    def create(self):
+        h = C.c_void_p()
+        rc = lib().rt_device_create(self.gpu, self.width, self.height, self.flags, C.byref(h))
+        if rc != 0:
+            return False
+        self._h = h.value
+        return True
+
+    def present(self):
+        check(lib().rt_device_present(self._h), "present")
+
+    def flush(self):
+        check(lib().rt_device_flush(self._h), "flush")
+
+    def synchronize(self):
+        check(lib().rt_device_synchronize(self._h), "synchronize")
+
+    def create_compute(self):
+        return Compute(self)
+
+    def create_texture(self):
+        return Texture(self)
+
+    def readback(self):
+        out = np.empty((self.height, self.width, 4), np.uint8)
+        check(lib().rt_device_readback(self._h, out.ctypes.data, self.width * 4), "readback")
+        return out
+
+    def readback_float(self):
+        out = np.empty((self.height, self.width, 4), np.float32)
+        check(lib().rt_device_readback_float(self._h, out.ctypes.data), "readback_float")
+        return out
+
+    def stats(self, reset=True):
+        s = _native.RtStats()
+        check(lib().rt_device_stats(self._h, C.byref(s), 1 if reset else 0), "stats")
+        return {n: int(getattr(s, n)) for n, _ in s._fields_}
+
+    def framebuffer_pointer(self):
+        return lib().rt_device_framebuffer(self._h)
+
+    def stream(self):
+        return lib().rt_device_stream(self._h)
+
+    def set_stream(self, stream_ptr):
+        check(lib().rt_device_set_stream(self._h, stream_ptr), "set_stream")
+
+    def destroy(self):
+        if self._h:
+            lib().rt_device_destroy(self._h)
+            self._h = None
+
+
+class DeviceFactory:
+    @staticmethod
+    def construct(api, width, height, gpu=0, **kw):
+        """DeviceFactory::construct (DeviceFactory.cpp:6-29): nullptr (None) on failure."""
+        if api != DeviceAPI.HIP:
+            return None
+        d = Device(width, height, gpu, **kw)
+        return d if d.create() else None
+
+
+class Noise:
+    """Graphics/Noise.cpp:39-94 via rt_noise_generate (seed 300 unless random)."""
+    TEXTURE_SIZE = 128
+    RAND_MSVC, RAND_GLIBC = 0, 1
+
+    def __init__(self):
+        self.permutations2D = None
+        self.permutations1D = None
+
+    def generate(self, random=False, seed=None, rand_kind=RAND_MSVC):
+        import time
+        if seed is None:
+            seed = int(time.time()) & 0xFFFFFFFF if random else 300
+        p2 = np.empty(128 * 128 * 4, np.uint8)
+        g = np.empty(128 * 4, np.float32)
+        check(lib().rt_noise_generate(seed, rand_kind, p2.ctypes.data, g.ctypes.data), "noise_generate")
+        self.permutations2D, self.permutations1D = p2, g
+
+
+def set_target_depths_host(camera_results):
+    cr = np.ascontiguousarray(camera_results, np.float32).reshape(1024, 4)
+    cd = np.empty((1024, 2), np.float32)
+    check(lib().rt_terrain_set_target_depths(cr.ctypes.data, cd.ctypes.data), "set_target_depths")
+    return cd
+
+
+class Terrain:
+    """Graphics/Terrain.{h,cpp}: creates the two computes, binds variables by name after
+    swap, and renders a frame.  render() keeps the reference's call sequence (prepass ->
+    CameraResults map/unmap -> host setTargetDepths -> CellDistance write -> tiled runs);
+    render_device() is the same frame with the round trip kept on the GPU."""
+
+    def __init__(self, device, theme="nomadplains", record_mode=False, aa_samples=1, max_steps=0,
+                 noise_seed=300, rand_kind=Noise.RAND_MSVC):
+        vfs_add_path("Media/" + theme)  # Terrain.cpp:23
+        self.device, self.theme, self.record_mode = device, theme, record_mode
+        self.aa_samples, self.max_steps = aa_samples, max_steps
+        self.noise_seed, self.rand_kind = noise_seed, rand_kind
+        self.compute = self.camera_compute = None
+        self.camera = None
+        self.camera_view = np.zeros((CAMERA_VIEW_RES * CAMERA_VIEW_RES, 4), np.float32)
+        self.sun = np.zeros(3, np.float32)
+
+    def create(self):  # Terrain.cpp:69-89
+        self.calculate_tile_sizes()
+        self.compute = self.device.create_compute()
+        self.camera_compute = self.device.create_compute()
+        self.noise = Noise()
+        self.noise.generate(seed=self.noise_seed, rand_kind=self.rand_kind)
+        self.tex_noise_2d = self.device.create_texture()
+        ok = self.tex_noise_2d.create(_native.RT_TEXTURE_2D, _native.RT_FORMAT_R8G8B8A8_UINT, 128, 128,
+                                      self.noise.permutations2D)
+        if not ok:
+            raise RuntimeError("texture create failed: " + lib().rt_last_error().decode())
+
+    def reload(self):  # Terrain.cpp:91-103
+        macros = [("RECORDING", "1")] if self.record_mode else []
+        if self.aa_samples != 1:
+            macros.append(("AA_SAMPLES", str(self.aa_samples)))
+        if self.max_steps:
+            macros.append(("RT_MAX_STEPS", str(self.max_steps)))
+        ok1 = self.compute.create("shaders", "tracescreen.hlsl", "CSMain", (self.thread_x, self.thread_y, 1), macros)
+        ok2 = self.camera_compute.create("shaders", "camerarays.hlsl", "CSMain",
+                                         (CAMERA_THREAD_RES, CAMERA_THREAD_RES, 1), macros)
+        return ok1 and ok2
+
+    def calculate_tile_sizes(self):  # Terrain.cpp:208-242
+        resx, resy = self.device.width, self.device.height
+        divisor = 4 if self.record_mode else 1
+        tpx, tpy = 1024 // divisor, 512 // divisor
+        self.tiles_x = -(-resx // tpx)
+        self.tiles_y = -(-resy // tpy)
+        self.tile_x, self.tile_y = resx // self.tiles_x, resy // self.tiles_y
+        self.thread_x = self.thread_y = 16
+        while self.tile_x % self.thread_x:
+            self.thread_x += 1
+        while self.tile_y % self.thread_y:
+            self.thread_y += 1
+        self.dispatch_x, self.dispatch_y = self.tile_x // self.thread_x, self.tile_y // self.thread_y
+
+    def set_camera(self, camera):
+        self.camera = camera
+
+    def update_shaders(self):  # Terrain.cpp:138-206
+        cam = self.camera
+        proj = _cbuffer_matrix(cam.projection_hlsl())
+        screen = np.array([cam.width, cam.height], np.float32)
+        if self.compute.swap():
+            self.var_view = self.compute.get_variable("ViewInverse")
+            self.var_eye = self.compute.get_variable("Eye")
+            self.var_sun = self.compute.get_variable("SunDirection")
+            self.var_thread_offset = self.compute.get_variable("ThreadOffset")
+            self.var_cell_distance = self.compute.get_array("CellDistance")
+            if self.var_cell_distance:
+                self.var_cell_distance.create(CAMERA_VIEW_RES * CAMERA_VIEW_RES)
+            for name, val in (("Projection", proj), ("ScreenSize", screen), ("permGradients", self.noise.permutations1D)):
+                v = self.compute.get_variable(name)
+                if v:
+                    v.write(val)
+            self.compute.set_texture(0, self.tex_noise_2d)
+            self._write_frame_vars()
+        if self.camera_compute.swap():
+            self.var_cam_view = self.camera_compute.get_variable("ViewInverse")
+            self.var_cam_eye = self.camera_compute.get_variable("Eye")
+            self.var_cam_results = self.camera_compute.get_array("CameraResults")
+            if self.var_cam_results:
+                self.var_cam_results.create(CAMERA_VIEW_RES * CAMERA_VIEW_RES)
+            for name, val in (("Projection", proj), ("ScreenSize", screen), ("permGradients", self.noise.permutations1D)):
+                v = self.camera_compute.get_variable(name)
+                if v:
+                    v.write(val)
+            self.camera_compute.set_texture(0, self.tex_noise_2d)
+            self._write_frame_vars()
+
+    def _write_frame_vars(self):
+        """Variables set before the first dispatch (avoids the frame-1 zero-constant
+        artefact of the reference)."""
+        if self.camera is None:
+            return
+        self.update_terrain()
+        self.set_time_of_day_vec(self.sun)
+
+    def update_terrain(self, time=0.0):  # Terrain.cpp:302-311
+        vinv = _cbuffer_matrix(self.camera.view_inverse_hlsl())
+        eye = self.camera.eye()
+        for v in (getattr(self, "var_view", None), getattr(self, "var_cam_view", None)):
+            if v:
+                v.write(vinv)
+        for v in (getattr(self, "var_eye", None), getattr(self, "var_cam_eye", None)):
+            if v:
+                v.write(eye)
+
+    def set_time_of_day(self, time_of_day):  # Terrain.cpp:285-300
+        from .camera import sun_direction
+        self.set_time_of_day_vec(sun_direction(time_of_day))
+
+    def set_time_of_day_vec(self, sun):
+        self.sun = np.asarray(sun, np.float32)
+        v = getattr(self, "var_sun", None)
+        if v:
+            v.write(self.sun)
+
+    def get_camera_results(self):  # Terrain.cpp:441-452
+        fd = self.var_cam_results.map()
+        if fd is None:
+            return
+        self.camera_view[:] = fd
+        self.var_cam_results.unmap()
+        if self.var_cell_distance:
+            self.var_cell_distance.write(set_target_depths_host(self.camera_view))
+
+    def render(self):  # Terrain.cpp:105-136 (reference call sequence)
+        self.update_shaders()
+        n = -(-CAMERA_VIEW_RES // CAMERA_THREAD_RES)
+        self.camera_compute.run(n, n, 1)
+        self.get_camera_results()
+        if self.var_thread_offset:
+            for x in range(self.tiles_x):
+                for y in range(self.tiles_y):
+                    off = np.array([x * self.dispatch_x * self.thread_x, y * self.dispatch_y * self.thread_y], np.uint32)
+                    self.var_thread_offset.write(off)
+                    self.compute.run(self.dispatch_x, self.dispatch_y, 1)
+                    self.device.flush()
+        else:
+            self.compute.run(self.dispatch_x * self.tiles_x, self.dispatch_y * self.tiles_y, 1)
+
+    def render_device(self, shard_rank=0, shard_count=1):
+        """Terrain::render with setTargetDepths on the GPU: no host round trip, all on one stream."""
+        self.update_shaders()
+        check(lib().rt_terrain_render(self.camera_compute._h, self.compute._h, shard_rank, shard_count),
+              "terrain_render")
+
+
+def _cbuffer_matrix(m):
+    """Bytes of XMMatrixTranspose(M) -- what the engine writes for a float4x4 cbuffer variable."""
+    return np.ascontiguousarray(np.asarray(m, np.float32).T)
+
+
+def shard_bytes(device, rank, count):
+    return int(lib().rt_shard_bytes(device._h, rank, count))
+
+
+def shard_pack(device, rank, count, dst_ptr):
+    check(lib().rt_shard_pack(device._h, rank, count, dst_ptr), "shard_pack")
+
+
+def shard_unpack(device, rank, count, src_ptr):
+    check(lib().rt_shard_unpack(device._h, rank, count, src_ptr), "shard_unpack")

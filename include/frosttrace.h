@@ -1,0 +1,165 @@
+/*
+ * frosttrace.h -- C-ABI drop-in boundary of the MI355X-native terrain ray-marcher.
+ *
+ * Every entry point replaces one call of the reference engine's dispatch-and-
+ * readback surface (paths relative to /root/reference/gpuraytrace):
+ *
+ *   IDevice         Factories/IDevice.h:16-54, DeviceFactory.cpp:6-29
+ *   ICompute        Factories/ICompute.h:16-59 (implemented by Adapters/ComputeDirect3D.cpp)
+ *   IShaderVariable Graphics/IShaderVariable.h:7-40 (ShaderVariableDirect3D.cpp:195-202)
+ *   IShaderArray    Graphics/IShaderVariable.h:42-61 (UAVBufferD3D :92-193, StructuredBufferD3D :204-281)
+ *   ITexture        Factories/ITexture.h:38-63 (TextureDirect3D.cpp:40-164)
+ *   VFS::addPath    Common/VFS.h (landscape selection, Terrain.cpp:23)
+ *
+ * Conventions: plain C types only; opaque handles; functions return RT_OK (0) or
+ * a negative RT_ERR_* code and set a thread-local message (rt_last_error()).
+ * Lookups that the reference answers with nullptr (missing variable/array)
+ * return NULL here too.  All GPU work is enqueued on the device's HIP stream;
+ * calls that hand data to the host (rt_array_map, rt_device_readback*) block.
+ */
+#ifndef FROSTTRACE_H
+#define FROSTTRACE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,    /* bad handle / argument */
+    RT_ERR_HIP = -2,        /* HIP runtime error (message carries hipGetErrorString) */
+    RT_ERR_NOT_FOUND = -3,  /* unknown shader file / entry / landscape */
+    RT_ERR_UNSUPPORTED = -4,/* operation the reference also rejects (e.g. map on an SRV array) */
+    RT_ERR_STATE = -5       /* e.g. run() before create()/swap(), missing texture */
+};
+
+/* DeviceDirect3D.cpp:113-126 swap-chain format R8G8B8A8_UNORM is always
+ * produced; RT_DEVICE_FLOAT_OUTPUT additionally keeps the pre-quantisation
+ * float4 colour (texOut's float4 value, tracescreen.hlsl:75) for parity. */
+enum { RT_DEVICE_FLOAT_OUTPUT = 1u, RT_DEVICE_STATS = 2u };
+
+/* ITexture.h:7-33 enum values */
+enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };
+enum { RT_FORMAT_UNKNOWN = 0, RT_FORMAT_R8G8B8A8_SNORM = 1, RT_FORMAT_R8G8B8A8_UNORM = 2, RT_FORMAT_R8G8B8A8_UINT = 3 };
+
+typedef struct rt_device_s* rt_device;
+typedef struct rt_compute_s* rt_compute;
+typedef struct rt_texture_s* rt_texture;
+typedef struct rt_variable_s* rt_variable;
+typedef struct rt_array_s* rt_array;
+
+typedef struct {
+    unsigned long long primary_steps; /* traceRay iterations, primary rays */
+    unsigned long long shadow_steps;  /* traceRay iterations, shadow rays */
+    unsigned long long prepass_steps; /* traceRay iterations, camerarays */
+    unsigned long long hits;          /* primary hits == shadow rays */
+} rt_stats;
+
+/* ---- diagnostics ---- */
+const char* rt_last_error(void);
+int rt_abi_version(void);
+
+/* ---- VFS (Common/VFS.cpp:19-31; Terrain.cpp:23 adds "Media/<landscape>") ----
+ * The most recently added "Media/<name>" path selects the landscape whose
+ * shaders rt_compute_create() loads (nomadplains, testing, simple, greenrocks). */
+int rt_vfs_add_path(const char* path);
+int rt_vfs_clear(void);
+
+/* ---- IDevice ----
+ * rt_device_create  <- DeviceFactory::construct + DeviceDirect3D::create (DeviceDirect3D.cpp:77-227):
+ *                      `ordinal` is the -g adapter index (:128-141), width/height the window size.
+ * rt_device_present <- IDevice::present (DeviceDirect3D.cpp:234-257): frame boundary.
+ * rt_device_flush   <- IDevice::flush (DeviceDirect3D.cpp:259-262).
+ * rt_device_readback<- the present() staging readback (:244-256): RGBA8 rows, `row_pitch` bytes apart. */
+int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_device* out);
+void rt_device_destroy(rt_device dev);
+int rt_device_present(rt_device dev);
+int rt_device_flush(rt_device dev);
+int rt_device_synchronize(rt_device dev);
+int rt_device_readback(rt_device dev, void* dst, size_t row_pitch);
+int rt_device_readback_float(rt_device dev, float* dst); /* W*H*4 floats, needs RT_DEVICE_FLOAT_OUTPUT */
+int rt_device_size(rt_device dev, int* width, int* height);
+void* rt_device_framebuffer(rt_device dev);       /* device pointer, W*H uint32 RGBA8 */
+void* rt_device_stream(rt_device dev);            /* hipStream_t */
+int rt_device_set_stream(rt_device dev, void* hip_stream); /* NULL = the device's own stream */
+int rt_device_stats(rt_device dev, rt_stats* out, int reset); /* needs RT_DEVICE_STATS */
+
+/* ---- ITexture (IDevice::createTexture + ITexture::create(dims, fmt, w, h, data, binding, cpu)) ---- */
+int rt_texture_create(rt_device dev, rt_texture* out);
+int rt_texture_init(rt_texture tex, int dimensions, int format, int width, int height, const void* data,
+                    int binding, int cpu_access);
+void rt_texture_destroy(rt_texture tex);
+
+/* ---- ICompute ----
+ * rt_compute_create     <- IDevice::createCompute (DeviceDirect3D.cpp:264-267)
+ * rt_compute_load       <- ICompute::create(directory, file, entry, ThreadSize, macros)
+ *                          (ComputeDirect3D.cpp:403-465).  Files: "tracescreen.hlsl",
+ *                          "camerarays.hlsl"; macros RECORDING, AA_SAMPLES and the build
+ *                          extension RT_MAX_STEPS.  A failed load keeps the previous shader.
+ * rt_compute_swap       <- ICompute::swap (:508-528): 1 if a new shader became current;
+ *                          invalidates the handles from rt_compute_get_*.
+ * rt_compute_run        <- ICompute::run (:530-581): dispatch (dx,dy,dz) groups of the
+ *                          compiled thread size; silent no-op without a current shader.
+ * rt_compute_set_texture<- ICompute::setTexture (:583-614), borrowed (not owned).
+ * rt_compute_get_*      <- getVariable/getArray/getBuffer by reflected name (NULL if absent;
+ *                          getBuffer is always NULL, as the reference's CBuffer=0 mask makes it). */
+int rt_compute_create(rt_device dev, rt_compute* out);
+void rt_compute_destroy(rt_compute cs);
+int rt_compute_load(rt_compute cs, const char* directory, const char* file, const char* entry, int tx, int ty, int tz,
+                    const char* const* macro_names, const char* const* macro_values, int n_macros);
+int rt_compute_swap(rt_compute cs);
+int rt_compute_run(rt_compute cs, unsigned dispatch_x, unsigned dispatch_y, unsigned dispatch_z);
+int rt_compute_set_texture(rt_compute cs, int stage, rt_texture tex);
+int rt_compute_thread_size(rt_compute cs, int* x, int* y, int* z);
+rt_variable rt_compute_get_variable(rt_compute cs, const char* name);
+rt_array rt_compute_get_array(rt_compute cs, const char* name);
+void* rt_compute_get_buffer(rt_compute cs, const char* name);
+
+/* ---- IShaderVariable ---- write copies exactly the reflected size (cbuffer shadow, uploaded lazily on run) */
+int rt_variable_write(rt_variable var, const void* data);
+size_t rt_variable_size(rt_variable var);
+const char* rt_variable_name(rt_variable var);
+
+/* ---- IShaderArray ----
+ * create: allocate `elements` x reflected stride.  UAV arrays (CameraResults): map = blocking
+ * device->host copy, unmap = host->device copy back; write unsupported.  SRV arrays
+ * (CellDistance): write = full upload; map/unmap unsupported.  As UAVBufferD3D/StructuredBufferD3D. */
+int rt_array_create(rt_array arr, unsigned elements);
+void* rt_array_map(rt_array arr);
+int rt_array_unmap(rt_array arr);
+int rt_array_write(rt_array arr, const void* data);
+size_t rt_array_stride(rt_array arr);
+void* rt_array_device_pointer(rt_array arr);
+
+/* ---- Terrain::render without the host round trip (Terrain.cpp:105-136) ----
+ * Runs camera_cs (prepass) -> setTargetDepths on the device (Terrain.cpp:398-439) ->
+ * screen_cs over the whole screen, all enqueued on the device stream.  Equivalent to the
+ * reference sequence run(2,2,1); CameraResults map/unmap; setTargetDepths; CellDistance
+ * write; tiled run(...).  With shard_count > 1 only screen tiles t (32x32 pixels,
+ * row-major tile index) with t % shard_count == shard_rank are traced. */
+int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
+/* Tile-cyclic shard transport: pack this rank's tiles from the framebuffer into a
+ * contiguous device buffer (RGBA8, 32x32-pixel tiles in tile order), or unpack a rank's
+ * packed tiles into the framebuffer.  Byte counts from rt_shard_bytes. */
+size_t rt_shard_bytes(rt_device dev, int shard_rank, int shard_count);
+int rt_shard_pack(rt_device dev, int shard_rank, int shard_count, void* dst_device);
+int rt_shard_unpack(rt_device dev, int shard_rank, int shard_count, const void* src_device);
+
+/* ---- host helpers (Noise.cpp:39-94, Camera.cpp, Terrain.cpp:285-311) ----
+ * rt_noise_generate: the engine's noise tables; rand_kind 0 = MSVC CRT rand (the
+ * reference's shipping platform), 1 = glibc rand.  perm2d: 128*128*4 bytes,
+ * grad: 128*4 floats. */
+int rt_noise_generate(uint32_t seed, int rand_kind, uint8_t* perm2d, float* grad);
+/* Terrain::setTargetDepths (Terrain.cpp:398-439) on the host: CameraResults float4[1024] ->
+ * CellDistance float2[1024], for engines that keep the reference's readback round trip. */
+int rt_terrain_set_target_depths(const float* camera_results, float* cell_distance);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
