@@ -20,7 +20,7 @@ RT_FORMAT_R8G8B8A8_UINT = 3
 
 class RtStats(C.Structure):
     _fields_ = [("primary_steps", C.c_ulonglong), ("shadow_steps", C.c_ulonglong),
-                ("prepass_steps", C.c_ulonglong), ("hits", C.c_ulonglong)]
+                ("prepass_steps", C.c_ulonglong), ("hits", C.c_ulonglong), ("noise_calls", C.c_ulonglong)]
 
 
 class NativeError(RuntimeError):
@@ -48,6 +48,8 @@ SIGNATURES = {
     "rt_device_stream": (_vp, [_vp]),
     "rt_device_set_stream": (_i, [_vp, _vp]),
     "rt_device_stats": (_i, [_vp, C.POINTER(RtStats), _i]),
+    "rt_device_set_profiling": (_i, [_vp, _i]),
+    "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "rt_texture_create": (_i, [_vp, C.POINTER(_vp)]),
     "rt_texture_init": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i]),
     "rt_texture_destroy": (None, [_vp]),

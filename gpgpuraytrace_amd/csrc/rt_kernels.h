@@ -5,13 +5,33 @@
 
 #include "rt_types.h"
 
+// Compacted primary hit (split pipeline): 48 bytes.
+struct RtHit {
+    uint32_t sample;  // (py*W + px)*AA + aa
+    float density;    // RayResult.density (> 0)
+    float pad0, pad1;
+    float4 pd;        // RayResult.pd (hit position, dist)
+    float4 fog;       // RayResult.fcolord
+};
+
+// work counters (one 64-byte block, zeroed per launch)
+enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2 };
+#define RT_CTR_BYTES 64
+
+enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1 };
+
 struct RtLaunch {
     hipStream_t stream;
     int landscape;
     const RtConsts* consts;   // device copy of the constant block
     const uint32_t* perm2d;   // device texPerm2D (128*128 texels)
-    const uint8_t* codes2;    // device packed gradient codes (128 bytes)
+    const float4* grad;       // device CBNoise.permGradients (128 float4)
     RtStats* stats;           // nullptr = uninstrumented kernels
+    uint32_t* queue;          // RT_CTR_BYTES of device work counters
+    int num_cus;              // compute units (persistent grid size)
+    int pipeline;             // RT_PIPELINE_*
+    float4* samples;          // split pipeline: W*H*AA saturated sample colours
+    RtHit* hits;              // split pipeline: W*H*AA compacted hit records
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);

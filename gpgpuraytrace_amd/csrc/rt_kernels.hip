@@ -1,13 +1,16 @@
-// rt_kernels.hip -- HIP kernels for gfx950 (MI355X): camera prepass, cell
-// depths, and the per-pixel screen trace.
+// rt_kernels.hip -- HIP kernels for gfx950 (MI355X).
 //
 //   k_camerarays   <- Media/common/shaders/camerarays.hlsl:12-21
-//   k_cell_depths  <- Graphics/Terrain.cpp:356-439 (setTargetDepths, host code
-//                     in the reference; on the device here so the frame needs
-//                     no GPU->CPU->GPU round trip)
+//   k_cell_depths  <- Graphics/Terrain.cpp:356-439 (setTargetDepths: host code in
+//                     the reference; on the device here so a frame needs no
+//                     GPU->CPU->GPU round trip)
 //   k_tracescreen  <- Media/common/shaders/tracescreen.hlsl:16-76
+//   k_shard_copy   -- tile-cyclic shard pack/unpack for the multi-GPU gather
 //
-// Launch interface (rt_launch_*) is plain C++ used by rt_runtime.cpp.
+// tracescreen is a persistent kernel: one 1024-thread workgroup per CU keeps the
+// noise tables (96 KiB) in LDS and every wave pulls 8x8-pixel work units from a
+// device-wide atomic queue, so a finished wave takes new work instead of idling
+// until the slowest wave of its workgroup retires.
 #include <hip/hip_runtime.h>
 
 #include "rt_kernels.h"
@@ -18,11 +21,33 @@ using rtm::f3;
 
 namespace {
 
-__device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* perm2d, const uint8_t* codes2)
+// LDS image: lane-private gradients (32 KiB) then the perm2D lattice (64 KiB).
+constexpr int kGradWords = 128 * 16 * 4;
+constexpr int kPermWords = 128 * 128;
+constexpr int kNoiseLdsWords = kGradWords + kPermWords;
+
+__device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __restrict__ perm2d,
+                                               const float4* __restrict__ grad)
+{
+    float4* g = reinterpret_cast<float4*>(lds);
+    for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) {
+        float4 v = grad[i >> 4];
+        v.w = -0.0f; // see rts::gdot
+        g[i] = v;
+    }
+    uint4* p = reinterpret_cast<uint4*>(lds + kGradWords);
+    const uint4* src = reinterpret_cast<const uint4*>(perm2d);
+    for (int i = threadIdx.x; i < kPermWords / 4; i += blockDim.x) p[i] = src[i];
+    __syncthreads();
+}
+
+__device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
 {
     Ctx c;
-    c.nz.perm2d = perm2d;
-    c.nz.codes2 = codes2;
+    c.nz.grad = reinterpret_cast<const float4*>(lds);
+    c.nz.perm2d = lds + kGradWords;
+    c.nz.slot = threadIdx.x & 15u;
+    c.nz.calls = 0;
     c.k = k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
     c.sun = rtm::mk(k->sun[0], k->sun[1], k->sun[2]);
@@ -33,17 +58,14 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* perm2
 // camerarays.hlsl:12-21.  One thread per prepass cell (32x32).
 template <int L, bool STATS>
 __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                   const uint8_t* __restrict__ codes2, float4* __restrict__ out,
+                                                   const float4* __restrict__ grad, float4* __restrict__ out,
                                                    RtStats* stats)
 {
-    __shared__ uint32_t s_perm[128 * 128];
-    __shared__ uint8_t s_codes[128];
-    for (int i = threadIdx.x; i < 128 * 128; i += blockDim.x) s_perm[i] = perm2d[i];
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) s_codes[i] = codes2[i];
-    __syncthreads();
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return;
-    Ctx c = make_ctx(k, s_perm, s_codes);
+    Ctx c = make_ctx(k, lds);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
     const float r31 = rtm::rcp(31.0f);
     uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
@@ -53,7 +75,10 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
     RayResult rr = trace_ray<L, false, true>(c, p, RT_CAMERA_NEAR, RT_CAMERA_FAR, 2.0f, dir, 0);
     if (rr.density < 0.0f) rr.pd.w = RT_CAMERA_FAR;
     out[i] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
-    if constexpr (STATS) atomicAdd(&stats->prepass_steps, (unsigned long long)rr.steps);
+    if constexpr (STATS) {
+        atomicAdd(&stats->prepass_steps, (unsigned long long)rr.steps);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -126,7 +151,8 @@ __device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn,
     f3 color;
     if (rr.density > 0.0f) {
         *hit += 1;
-        f3 n = get_normal<L>(c, rr.pd);
+        f4 npd = {rr.pd.x, rr.pd.y, rr.pd.z, rr.density}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
+        f3 n = get_normal<L>(c, npd);
         f3 hp = rtm::mk(rr.pd.x, rr.pd.y, rr.pd.z);
         ShadePre sp = shade_pre<L>(c, hp, n, pdn, rr.pd.w);
         RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
@@ -148,47 +174,24 @@ __device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn,
     return color;
 }
 
-// tracescreen.hlsl:50-76.  Block = 64 threads = one wave = one 8x8 pixel tile
-// of the dispatch region [off, off + extent).  LDS holds the 64 KiB lattice
-// and the 128-byte gradient code table for the block's lifetime.
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                     const uint8_t* __restrict__ codes2,
-                                                     const float2* __restrict__ cells, uint32_t* __restrict__ out8,
-                                                     float4* __restrict__ out32, uint32_t off_x, uint32_t off_y,
-                                                     uint32_t ext_x, uint32_t ext_y, uint32_t tiles_x,
-                                                     uint32_t tile_first, uint32_t tile_stride, RtStats* stats)
+// tracescreen.hlsl:50-76 for one pixel (all AA samples)
+template <int L>
+__device__ __forceinline__ void shade_pixel(const Ctx& c, uint32_t px, uint32_t py, const float2* __restrict__ cells,
+                                            uint32_t* __restrict__ out8, float4* __restrict__ out32, float* psteps,
+                                            float* ssteps, int* hits)
 {
-    __shared__ uint32_t s_perm[128 * 128];
-    __shared__ uint8_t s_codes[128];
-    for (int i = threadIdx.x; i < 128 * 128; i += blockDim.x) s_perm[i] = perm2d[i];
-    for (int i = threadIdx.x; i < 128; i += blockDim.x) s_codes[i] = codes2[i];
-    __syncthreads();
-
-    // 1024-thread block = 16 waves = a 32x32 pixel tile, each wave an 8x8 sub-tile
-    int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t lx = (uint32_t)((wave & 3) * 8 + (lane & 7));
-    uint32_t ly = (uint32_t)((wave >> 2) * 8 + (lane >> 3));
-    uint32_t tile = blockIdx.x * tile_stride + tile_first;
-    uint32_t gx = (tile % tiles_x) * 32 + lx, gy = (tile / tiles_x) * 32 + ly;
-    if (gx >= ext_x || gy >= ext_y) return;
-    uint32_t px = gx + off_x, py = gy + off_y;
-    if (px >= (uint32_t)k->width || py >= (uint32_t)k->height) return; // UAV writes outside texOut are dropped
-
-    Ctx c = make_ctx(k, s_perm, s_codes);
+    const RtConsts* k = c.k;
     float pxf = (float)px, pyf = (float)py;
     float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
     uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
     float plane_x = cells[cell].x, plane_y = RT_CAMERA_FAR;
     float col0 = 0.0f, col1 = 0.0f, col2 = 0.0f;
-    float psteps = 0.0f, ssteps = 0.0f;
-    int hit = 0;
     const int aa = k->aa_samples;
     for (int a = 0; a < aa; ++a) {
         f3 p, dir;
         get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
         f3 pdn = rtm::normalize(dir);
-        f3 s = trace_sample<L>(c, p, dir, pdn, plane_x, plane_y, &psteps, &ssteps, &hit);
+        f3 s = trace_sample<L>(c, p, dir, pdn, plane_x, plane_y, psteps, ssteps, hits);
         col0 = col0 + rtm::sat(s.x);
         col1 = col1 + rtm::sat(s.y);
         col2 = col2 + rtm::sat(s.z);
@@ -200,10 +203,241 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
     size_t o = (size_t)py * (size_t)k->width + px;
     out8[o] = unorm8(col0) | (unorm8(col1) << 8) | (unorm8(col2) << 16) | 0xff000000u;
     if (out32) out32[o] = make_float4(col0, col1, col2, 1.0f);
+}
+
+// Persistent screen trace.  Work unit u (0..n_units): 32x32 shard tile
+// T = (u/16)*tile_stride + tile_first (row-major over the region, tiles32_x per
+// row), 8x8 sub-tile u%16; lane l traces pixel (l&7, l>>3) of the sub-tile.
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                      const float4* __restrict__ grad, const float2* __restrict__ cells,
+                                                      uint32_t* __restrict__ out8, float4* __restrict__ out32,
+                                                      uint32_t off_x, uint32_t off_y, uint32_t ext_x, uint32_t ext_y,
+                                                      uint32_t tiles32_x, uint32_t tile_first, uint32_t tile_stride,
+                                                      uint32_t n_units, uint32_t* __restrict__ queue, RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
+    float psteps = 0.0f, ssteps = 0.0f;
+    int hits = 0;
+    for (;;) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(queue, 1u);
+        u = __builtin_amdgcn_readfirstlane(u);
+        if (u >= n_units) break;
+        uint32_t T = (u >> 4) * tile_stride + tile_first, sub = u & 15u;
+        uint32_t gx = (T % tiles32_x) * 32u + (sub & 3u) * 8u + (lane & 7u);
+        uint32_t gy = (T / tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
+        if (gx < ext_x && gy < ext_y) {
+            uint32_t px = gx + off_x, py = gy + off_y;
+            if (px < W && py < H) shade_pixel<L>(c, px, py, cells, out8, out32, &psteps, &ssteps, &hits);
+        }
+    }
     if constexpr (STATS) {
         atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        atomicAdd(&stats->hits, (unsigned long long)hit);
+        atomicAdd(&stats->hits, (unsigned long long)hits);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+// ===========================================================================
+// Split (wavefront) screen pipeline: the same tracescreen.hlsl:16-76 frame in
+// three passes so each kernel body stays small and every shading lane works on a
+// hit.  P: primary march; misses get their sky colour at once, hits are appended
+// to a compacted queue (wave-aggregated atomics).  S: normal + colour + shadow
+// march + sky blend over the compacted hits.  R: in-order AA average + UNORM8.
+struct UnitMap {
+    uint32_t off_x, off_y, ext_x, ext_y, tiles32_x, tile_first, tile_stride, n_units;
+};
+
+__device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_t lane, uint32_t W, uint32_t H,
+                                           uint32_t* px, uint32_t* py)
+{
+    uint32_t T = (u >> 4) * m.tile_stride + m.tile_first, sub = u & 15u;
+    uint32_t gx = (T % m.tiles32_x) * 32u + (sub & 3u) * 8u + (lane & 7u);
+    uint32_t gy = (T / m.tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
+    *px = gx + m.off_x;
+    *py = gy + m.off_y;
+    return gx < m.ext_x && gy < m.ext_y && *px < W && *py < H;
+}
+
+__device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane)
+{
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(counter, 1u);
+    return __builtin_amdgcn_readfirstlane(u);
+}
+
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                  const float4* __restrict__ grad, const float2* __restrict__ cells,
+                                                  UnitMap m, float4* __restrict__ samples, RtHit* __restrict__ hits,
+                                                  uint32_t* __restrict__ counters, RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
+    const int aa = k->aa_samples;
+    float psteps = 0.0f;
+    uint32_t nhits = 0;
+    for (;;) {
+        uint32_t u = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+        if (u >= m.n_units) break;
+        uint32_t px, py;
+        bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
+        float pxf = (float)px, pyf = (float)py;
+        float plane_x = 0.0f;
+        if (valid) {
+            float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
+            uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
+            plane_x = cells[cell].x;
+        }
+        for (int a = 0; a < aa; ++a) {
+            bool hit = false;
+            RtHit rec;
+            uint32_t s = (py * W + px) * (uint32_t)aa + (uint32_t)a;
+            if (valid) {
+                f3 p, dir;
+                get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
+                RayResult rr = trace_ray<L, true, false>(c, p, plane_x, RT_CAMERA_FAR, 1.0f, dir, k->max_steps);
+                psteps += rr.steps;
+                if (rr.density > 0.0f) {
+                    hit = true;
+                    rec.sample = s;
+                    rec.density = rr.density;
+                    rec.pd = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+                    rec.fog = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
+                } else {
+                    // tracescreen.hlsl:22-27, :36-38 (miss branch)
+                    f3 pdn = rtm::normalize(dir);
+                    float skyAmount = rr.pd.w * 0.0005f;
+                    skyAmount = rtm::sat(skyAmount * skyAmount);
+                    SkyColor scat = get_rayleigh_mie(c, pdn);
+                    float space = get_space_color(c, pdn);
+                    f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
+                                     (scat.mie.z + scat.rayleigh.z) + space);
+                    f3 col = rtm::mk(rtm::lerp(sky.x, rr.fc.x, rr.fc.w), rtm::lerp(sky.y, rr.fc.y, rr.fc.w),
+                                     rtm::lerp(sky.z, rr.fc.z, rr.fc.w));
+                    col = rtm::mk(rtm::lerp(col.x, sky.x, skyAmount), rtm::lerp(col.y, sky.y, skyAmount),
+                                  rtm::lerp(col.z, sky.z, skyAmount));
+                    samples[s] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+                }
+            }
+            // wave-aggregated append of this wave's hits
+            uint64_t bal = __ballot(hit);
+            uint32_t cnt = (uint32_t)__popcll(bal);
+            if (cnt) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&counters[RT_CTR_HITS], cnt);
+                base = __builtin_amdgcn_readfirstlane(base);
+                if (hit) {
+                    uint32_t idx = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                    hits[idx] = rec;
+                }
+                nhits += hit ? 1u : 0u;
+            }
+        }
+    }
+    if constexpr (STATS) {
+        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
+        atomicAdd(&stats->hits, (unsigned long long)nhits);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                const float4* __restrict__ grad, float4* __restrict__ samples,
+                                                const RtHit* __restrict__ hits, uint32_t* __restrict__ counters,
+                                                RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width;
+    const uint32_t aa = (uint32_t)k->aa_samples;
+    const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
+    const uint32_t n_units = (n_hits + 63u) / 64u;
+    float ssteps = 0.0f;
+    for (;;) {
+        uint32_t u = wave_fetch(&counters[RT_CTR_SHADE], lane);
+        if (u >= n_units) break;
+        uint32_t i = u * 64u + lane;
+        if (i >= n_hits) continue;
+        RtHit rec = hits[i];
+        uint32_t s = rec.sample, pix = s / aa, a = s - pix * aa;
+        uint32_t px = pix % W, py = pix / W;
+        f3 p, dir;
+        get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
+        f3 pdn = rtm::normalize(dir);
+        // tracescreen.hlsl:22-35 (hit branch)
+        float skyAmount = rec.pd.w * 0.0005f;
+        skyAmount = rtm::sat(skyAmount * skyAmount);
+        f4 pd = {rec.pd.x, rec.pd.y, rec.pd.z, rec.density};
+        f3 n = get_normal<L>(c, pd);
+        f3 hp = rtm::mk(rec.pd.x, rec.pd.y, rec.pd.z);
+        ShadePre sp = shade_pre<L>(c, hp, n, pdn, rec.pd.w);
+        RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
+        ssteps += sr.steps;
+        f3 col = shade_post(c, sp, sr.density, sr.fc.w);
+        col = rtm::mk(rtm::lerp(col.x, rec.fog.x, rec.fog.w), rtm::lerp(col.y, rec.fog.y, rec.fog.w),
+                      rtm::lerp(col.z, rec.fog.z, rec.fog.w));
+        SkyColor scat = get_rayleigh_mie(c, pdn);
+        col = rtm::mk(rtm::lerp(col.x, scat.rayleigh.x, skyAmount), rtm::lerp(col.y, scat.rayleigh.y, skyAmount),
+                      rtm::lerp(col.z, scat.rayleigh.z, skyAmount));
+        samples[s] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+    }
+    if constexpr (STATS) {
+        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+// tracescreen.hlsl:67-75: color = sum of saturated samples in AA order, / AA, UNORM8 store
+__global__ void __launch_bounds__(64) k_resolve(const RtConsts* __restrict__ k, UnitMap m,
+                                                const float4* __restrict__ samples, uint32_t* __restrict__ out8,
+                                                float4* __restrict__ out32)
+{
+    uint32_t px, py;
+    if (!unit_pixel(m, blockIdx.x, threadIdx.x, (uint32_t)k->width, (uint32_t)k->height, &px, &py)) return;
+    const uint32_t aa = (uint32_t)k->aa_samples;
+    size_t o = (size_t)py * (size_t)k->width + px;
+    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+    for (uint32_t a = 0; a < aa; ++a) {
+        float4 v = samples[o * aa + a];
+        c0 = c0 + v.x;
+        c1 = c1 + v.y;
+        c2 = c2 + v.z;
+    }
+    float ia = rtm::rcp((float)aa);
+    c0 = c0 * ia;
+    c1 = c1 * ia;
+    c2 = c2 * ia;
+    out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
+    if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
+}
+
+// Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
+__global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, uint32_t* __restrict__ packed, int w,
+                                                    int h, int rank, int count, int pack)
+{
+    int tiles_x = (w + 31) / 32;
+    int kk = blockIdx.x;
+    int tile = kk * count + rank;
+    int tx0 = (tile % tiles_x) * 32, ty0 = (tile / tiles_x) * 32;
+    for (int i = threadIdx.x; i < 1024; i += 256) {
+        int x = tx0 + (i & 31), y = ty0 + (i >> 5);
+        if (x >= w || y >= h) continue;
+        size_t f = (size_t)y * w + x, p = (size_t)kk * 1024 + i;
+        if (pack) packed[p] = fb[f];
+        else fb[f] = packed[p];
     }
 }
 
@@ -212,9 +446,9 @@ void launch_camerarays_l(const RtLaunch& a, float4* out)
 {
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64), block(64);
     if (a.stats)
-        hipLaunchKernelGGL((k_camerarays<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.codes2, out, a.stats);
+        hipLaunchKernelGGL((k_camerarays<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats);
     else
-        hipLaunchKernelGGL((k_camerarays<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.codes2, out, a.stats);
+        hipLaunchKernelGGL((k_camerarays<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats);
 }
 
 template <int L>
@@ -223,31 +457,52 @@ void launch_tracescreen_l(const RtLaunch& a, const float2* cells, uint32_t* out8
 {
     uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
     if (first >= total) return;
-    uint32_t n = (total - first + stride - 1) / stride;
-    dim3 grid(n), block(1024);
+    uint32_t n_tiles = (total - first + stride - 1) / stride;
+    uint32_t n_units = n_tiles * 16u;
+    uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
+    uint32_t need = (n_units + 15u) / 16u; // 16 waves per block
+    if (need < blocks) blocks = need;
+    (void)hipMemsetAsync(a.queue, 0, sizeof(uint32_t), a.stream);
+    dim3 grid(blocks), block(1024);
     if (a.stats)
-        hipLaunchKernelGGL((k_tracescreen<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.codes2, cells, out8,
-                           out32, ox, oy, ex, ey, tiles_x, first, stride, a.stats);
+        hipLaunchKernelGGL((k_tracescreen<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, cells, out8,
+                           out32, ox, oy, ex, ey, tiles_x, first, stride, n_units, a.queue, a.stats);
     else
-        hipLaunchKernelGGL((k_tracescreen<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.codes2, cells,
-                           out8, out32, ox, oy, ex, ey, tiles_x, first, stride, a.stats);
+        hipLaunchKernelGGL((k_tracescreen<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
+                           out8, out32, ox, oy, ex, ey, tiles_x, first, stride, n_units, a.queue, a.stats);
 }
 
-// Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
-__global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, uint32_t* __restrict__ packed, int w,
-                                                    int h, int rank, int count, int pack)
+template <int L>
+void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t ox, uint32_t oy,
+                    uint32_t ex, uint32_t ey, uint32_t first, uint32_t stride)
 {
-    int tiles_x = (w + 31) / 32;
-    int k = blockIdx.x;
-    int tile = k * count + rank;
-    int tx0 = (tile % tiles_x) * 32, ty0 = (tile / tiles_x) * 32;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        int x = tx0 + (i & 31), y = ty0 + (i >> 5);
-        if (x >= w || y >= h) continue;
-        size_t f = (size_t)y * w + x, p = (size_t)k * 1024 + i;
-        if (pack) packed[p] = fb[f];
-        else fb[f] = packed[p];
+    UnitMap m;
+    uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
+    if (first >= total) return;
+    m.off_x = ox;
+    m.off_y = oy;
+    m.ext_x = ex;
+    m.ext_y = ey;
+    m.tiles32_x = tiles_x;
+    m.tile_first = first;
+    m.tile_stride = stride;
+    m.n_units = ((total - first + stride - 1) / stride) * 16u;
+    uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
+    uint32_t need = (m.n_units + 15u) / 16u;
+    uint32_t pblocks = need < blocks ? need : blocks;
+    (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
+    if (a.stats) {
+        hipLaunchKernelGGL((k_primary<L, true>), dim3(pblocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
+                           cells, m, a.samples, a.hits, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade<L, true>), dim3(blocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
+                           a.samples, a.hits, a.queue, a.stats);
+    } else {
+        hipLaunchKernelGGL((k_primary<L, false>), dim3(pblocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
+                           cells, m, a.samples, a.hits, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade<L, false>), dim3(blocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
+                           a.samples, a.hits, a.queue, a.stats);
     }
+    hipLaunchKernelGGL(k_resolve, dim3(m.n_units), dim3(64), 0, a.stream, a.consts, m, a.samples, out8, out32);
 }
 
 } // namespace
@@ -271,11 +526,20 @@ void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out
                            uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first, uint32_t stride)
 {
     if (ex == 0 || ey == 0 || stride == 0) return;
+    if (a.pipeline == RT_PIPELINE_MEGA) {
+        switch (a.landscape) {
+        case RT_TESTING: launch_tracescreen_l<RT_TESTING>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+        case RT_SIMPLE: launch_tracescreen_l<RT_SIMPLE>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+        case RT_GREENROCKS: launch_tracescreen_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+        default: launch_tracescreen_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+        }
+        return;
+    }
     switch (a.landscape) {
-    case RT_TESTING: launch_tracescreen_l<RT_TESTING>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    case RT_SIMPLE: launch_tracescreen_l<RT_SIMPLE>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    case RT_GREENROCKS: launch_tracescreen_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    default: launch_tracescreen_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+    case RT_TESTING: launch_split_l<RT_TESTING>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+    case RT_SIMPLE: launch_split_l<RT_SIMPLE>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+    case RT_GREENROCKS: launch_split_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+    default: launch_split_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
     }
 }
 

@@ -104,7 +104,44 @@ struct rt_device_s {
     float4* fb32 = nullptr;
     RtStats* stats = nullptr;
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
+    uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
+    int num_cus = 256;
+    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" selects the single-kernel path
+    float4* samples = nullptr;     // split pipeline buffers, sized for samples_cap samples
+    RtHit* hits = nullptr;
+    size_t samples_cap = 0;
+    // dominant-kernel timing (rt_device_set_profiling)
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+    size_t ev_used = 0;
+    // children (IDevice::createCompute / createTexture); destroyed with the device
+    std::vector<struct rt_compute_s*> computes;
+    std::vector<struct rt_texture_s*> textures;
 };
+
+namespace {
+// bracket one tracescreen launch with a pair of events when profiling is on
+struct KernelTimer {
+    rt_device_s* d;
+    hipEvent_t stop = nullptr;
+    explicit KernelTimer(rt_device_s* dev) : d(dev)
+    {
+        if (!d->profiling) return;
+        if (d->ev_used == d->ev_pool.size()) {
+            hipEvent_t a, b;
+            if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return;
+            d->ev_pool.emplace_back(a, b);
+        }
+        auto& pr = d->ev_pool[d->ev_used++];
+        (void)hipEventRecord(pr.first, d->stream);
+        stop = pr.second;
+    }
+    ~KernelTimer()
+    {
+        if (stop) (void)hipEventRecord(stop, d->stream);
+    }
+};
+} // namespace
 
 struct rt_texture_s {
     rt_device dev = nullptr;
@@ -150,14 +187,13 @@ struct Shader {
     // device-side state
     RtConsts host_consts{};
     RtConsts* d_consts = nullptr;
-    uint8_t* d_codes = nullptr;
-    Staging consts_staging, codes_staging;
-    int codes_ok = 0;
+    float4* d_grad = nullptr;
+    Staging consts_staging, grad_staging;
 
     ~Shader()
     {
         if (d_consts) (void)hipFree(d_consts);
-        if (d_codes) (void)hipFree(d_codes);
+        if (d_grad) (void)hipFree(d_grad);
         for (auto& a : arrays)
             if (a->dev_ptr) (void)hipFree(a->dev_ptr);
     }
@@ -325,53 +361,19 @@ void build_consts(const Shader& s, const rt_device_s& dev, RtConsts& k)
     k.height = dev.height;
 }
 
-// Gradient codes (rt_shader.h NoiseView) from CBNoise.permGradients.  Only the
-// canonical {-1,0,1}^3 two-non-zero gradient set of Noise.cpp:6-24 is accepted.
-int build_codes(const std::vector<uint8_t>& grad_bytes, uint8_t out[128])
-{
-    uint8_t code[128];
-    for (int i = 0; i < 128; ++i) {
-        float g[3];
-        memcpy(g, grad_bytes.data() + 16 * i, 12);
-        int axes[3], n = 0;
-        for (int a = 0; a < 3; ++a) {
-            if (g[a] == 0.0f) continue;
-            if (g[a] != 1.0f && g[a] != -1.0f) n = 99;
-            if (n < 3) axes[n] = a;
-            ++n;
-        }
-        if (n != 2) return fail(RT_ERR_UNSUPPORTED, "permGradients[%d] is not a canonical noise gradient", i);
-        uint8_t c = 0;
-        if (axes[0] == 1) c |= 1u;
-        if (axes[1] == 2) c |= 2u;
-        if (g[axes[0]] < 0.0f) c |= 4u;
-        if (g[axes[1]] < 0.0f) c |= 8u;
-        code[i] = c;
-    }
-    for (int i = 0; i < 128; ++i) out[i] = (uint8_t)(code[i] | (code[(i + 1) & 127] << 4));
-    return RT_OK;
-}
-
 int sync_shader(rt_device dev, Shader* s)
 {
     if (!s->d_consts) HIP_TRY(hipMalloc(&s->d_consts, sizeof(RtConsts)));
-    if (!s->d_codes) HIP_TRY(hipMalloc(&s->d_codes, 128));
+    if (!s->d_grad) HIP_TRY(hipMalloc(&s->d_grad, 128 * sizeof(float4)));
     if (s->cb_dirty) {
+        // cbuffer shadows -> device (ConstantBufferD3D::update on run, ShaderVariableDirect3D.cpp:59-66)
         build_consts(*s, *dev, s->host_consts);
         int rc = s->consts_staging.upload(dev->stream, s->d_consts, &s->host_consts, sizeof(RtConsts));
         if (rc) return rc;
-        uint8_t codes[128];
-        rc = build_codes(s->cb[CB_NOISE], codes);
-        if (rc) {
-            s->codes_ok = 0;
-            return rc;
-        }
-        rc = s->codes_staging.upload(dev->stream, s->d_codes, codes, 128);
+        rc = s->grad_staging.upload(dev->stream, s->d_grad, s->cb[CB_NOISE].data(), 128 * sizeof(float4));
         if (rc) return rc;
-        s->codes_ok = 1;
         s->cb_dirty = false;
     }
-    if (!s->codes_ok) return fail(RT_ERR_STATE, "noise gradients not set");
     return RT_OK;
 }
 
@@ -382,8 +384,13 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.landscape = s->landscape;
     a.consts = s->d_consts;
     a.perm2d = s->textures[0] ? s->textures[0]->data : nullptr;
-    a.codes2 = s->d_codes;
+    a.grad = s->d_grad;
     a.stats = (dev->flags & RT_DEVICE_STATS) ? dev->stats : nullptr;
+    a.queue = dev->queue;
+    a.num_cus = dev->num_cus;
+    a.pipeline = dev->pipeline;
+    a.samples = dev->samples;
+    a.hits = dev->hits;
     return a;
 }
 
@@ -393,6 +400,23 @@ int check_texture(Shader* s)
     if (!t || !t->data) return fail(RT_ERR_STATE, "texture stage 0 (texPerm2D) not bound");
     if (t->w != 128 || t->h != 128 || t->fmt != RT_FORMAT_R8G8B8A8_UINT)
         return fail(RT_ERR_UNSUPPORTED, "texPerm2D must be a 128x128 R8G8B8A8_UINT texture");
+    return RT_OK;
+}
+
+// Split-pipeline buffers (one sample colour and one potential hit record per AA sample).
+int ensure_split_buffers(rt_device dev, int aa)
+{
+    size_t need = (size_t)dev->width * dev->height * (size_t)aa;
+    if (need <= dev->samples_cap) return RT_OK;
+    HIP_TRY(hipStreamSynchronize(dev->stream));
+    if (dev->samples) HIP_TRY(hipFree(dev->samples));
+    if (dev->hits) HIP_TRY(hipFree(dev->hits));
+    dev->samples = nullptr;
+    dev->hits = nullptr;
+    dev->samples_cap = 0;
+    HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->hits, need * sizeof(RtHit)));
+    dev->samples_cap = need;
     return RT_OK;
 }
 
@@ -443,6 +467,9 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMalloc(&d->stats, sizeof(RtStats)));
     HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
+    if (const char* p = getenv("RT_PIPELINE")) d->pipeline = strcmp(p, "mega") == 0 ? RT_PIPELINE_MEGA : RT_PIPELINE_SPLIT;
+    HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
     return RT_OK;
 }
@@ -453,10 +480,22 @@ void rt_device_destroy(rt_device d)
     (void)hipSetDevice(d->ordinal);
     if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
     if (d->stream && d->stream != d->own_stream) (void)hipStreamSynchronize(d->stream);
+    for (auto* c : d->computes) delete c; // children die with their device
+    for (auto* t : d->textures) {
+        if (t->data) (void)hipFree(t->data);
+        delete t;
+    }
     if (d->fb8) (void)hipFree(d->fb8);
     if (d->fb32) (void)hipFree(d->fb32);
     if (d->stats) (void)hipFree(d->stats);
     if (d->scratch_cam) (void)hipFree(d->scratch_cam);
+    if (d->queue) (void)hipFree(d->queue);
+    if (d->samples) (void)hipFree(d->samples);
+    if (d->hits) (void)hipFree(d->hits);
+    for (auto& pr : d->ev_pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
     if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
     delete d;
 }
@@ -531,7 +570,31 @@ int rt_device_stats(rt_device d, rt_stats* out, int reset)
     out->shadow_steps = h.shadow_steps;
     out->prepass_steps = h.prepass_steps;
     out->hits = h.hits;
+    out->noise_calls = h.noise_calls;
     if (reset) HIP_TRY(hipMemsetAsync(d->stats, 0, sizeof(RtStats), d->stream));
+    return RT_OK;
+}
+
+int rt_device_set_profiling(rt_device d, int enable)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    d->profiling = enable != 0;
+    return RT_OK;
+}
+
+int rt_device_kernel_time(rt_device d, double* total_ms, int* launches)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    double tot = 0.0;
+    for (size_t i = 0; i < d->ev_used; ++i) {
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, d->ev_pool[i].first, d->ev_pool[i].second));
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (int)d->ev_used;
+    d->ev_used = 0;
     return RT_OK;
 }
 
@@ -541,6 +604,7 @@ int rt_texture_create(rt_device d, rt_texture* out)
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
     auto t = new rt_texture_s();
     t->dev = d;
+    d->textures.push_back(t);
     *out = t;
     return RT_OK;
 }
@@ -566,6 +630,8 @@ int rt_texture_init(rt_texture t, int dims, int fmt, int w, int h, const void* d
 void rt_texture_destroy(rt_texture t)
 {
     if (!t) return;
+    auto& v = t->dev->textures;
+    v.erase(std::remove(v.begin(), v.end(), t), v.end());
     if (t->data) (void)hipFree(t->data);
     delete t;
 }
@@ -576,6 +642,7 @@ int rt_compute_create(rt_device d, rt_compute* out)
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
     auto c = new rt_compute_s();
     c->dev = d;
+    d->computes.push_back(c);
     *out = c;
     return RT_OK;
 }
@@ -584,6 +651,8 @@ void rt_compute_destroy(rt_compute c)
 {
     if (!c) return;
     (void)hipStreamSynchronize(c->dev->stream);
+    auto& v = c->dev->computes;
+    v.erase(std::remove(v.begin(), v.end(), c), v.end());
     delete c;
 }
 
@@ -706,6 +775,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     if (rc) return rc;
     rc = sync_shader(dev, s);
     if (rc) return rc;
+    if (s->kind == KIND_TRACESCREEN && (rc = ensure_split_buffers(dev, s->aa))) return rc;
     RtLaunch a = make_launch(dev, s);
     if (dz == 0) return RT_OK;
     if (s->kind == KIND_CAMERARAYS) {
@@ -729,6 +799,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
         uint64_t ex = (uint64_t)dx * s->tx, ey = (uint64_t)dy * s->ty;
         ex = std::min<uint64_t>(ex, dev->width > (int)off[0] ? dev->width - off[0] : 0);
         ey = std::min<uint64_t>(ey, dev->height > (int)off[1] ? dev->height - off[1] : 0);
+        KernelTimer kt(dev);
         rt_launch_tracescreen(a, (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, off[0], off[1], (uint32_t)ex,
                               (uint32_t)ey, 0, 1);
     }
@@ -814,14 +885,18 @@ int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_
     int rc;
     if ((rc = check_texture(cam->shader)) || (rc = check_texture(scr->shader))) return rc;
     if ((rc = sync_shader(dev, cam->shader)) || (rc = sync_shader(dev, scr->shader))) return rc;
+    if ((rc = ensure_split_buffers(dev, scr->shader->aa))) return rc;
     rt_array_s* cr = cam->shader->array("CameraResults");
     rt_array_s* cd = scr->shader->array("CellDistance");
     if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
     float4* crp = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : dev->scratch_cam;
     rt_launch_camerarays(make_launch(dev, cam->shader), crp);
     rt_launch_cell_depths(dev->stream, crp, (float2*)cd->dev_ptr);
-    rt_launch_tracescreen(make_launch(dev, scr->shader), (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, 0, 0,
-                          (uint32_t)dev->width, (uint32_t)dev->height, (uint32_t)shard_rank, (uint32_t)shard_count);
+    {
+        KernelTimer kt(dev);
+        rt_launch_tracescreen(make_launch(dev, scr->shader), (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, 0, 0,
+                              (uint32_t)dev->width, (uint32_t)dev->height, (uint32_t)shard_rank, (uint32_t)shard_count);
+    }
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }

@@ -17,55 +17,67 @@ using rtm::f3;
 using rtm::fma;
 
 // ---------------------------------------------------------------------------
-// Noise lattice view.  perm2d: texPerm2D texels (R8G8B8A8_UINT, texel (x,y)
-// at x + y*128); codes2: for lattice index i (0..127) two 4-bit gradient codes:
-// low nibble = code(i), high nibble = code((i+1)&127) (the "+ONE_PIXEL" corner).
-// A gradient code c encodes the two non-zero gradient components (R8):
-//   bit0: first term is y (else x); bit1: second term is z (else y);
-//   bit2: first term negated;       bit3: second term negated.
+// Noise lattice view (both tables live in LDS for the kernel's lifetime).
+//   perm2d: texPerm2D texels (R8G8B8A8_UINT), texel (x,y) at x + y*128 (64 KiB).
+//   grad:   CBNoise.permGradients as float4, stored lane-private: entry i for
+//           lane slot s (= lane & 15) at grad[i*16 + s] (32 KiB).  A ds_read_b128
+//           wave instruction serves 16-lane groups; giving each lane of a group its
+//           own 16-byte bank slot makes every gradient fetch conflict-free however
+//           random the 8 corner indices are.
 struct NoiseView {
     const uint32_t* perm2d;
-    const uint8_t* codes2;
+    const float4* grad;
+    uint32_t slot;
+    mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
 };
-
-__device__ __forceinline__ float gdot(uint32_t c, float x, float y, float z)
-{
-    float a = (c & 1u) ? y : x;
-    float b = (c & 2u) ? z : y;
-    float an = rtm::fbits(rtm::bits(a) ^ ((c << 29) & 0x80000000u));
-    float bn = rtm::fbits(rtm::bits(b) ^ ((c << 28) & 0x80000000u));
-    return an + bn;
-}
 
 __device__ __forceinline__ float fade(float t)
 {
     return ((t * t) * t) * fma(t, fma(t, 6.0f, -15.0f), 10.0f);
 }
 
-// noise.hlsl:153-179 (live `#if 1` block), gradperm :145-150
+// gradperm (noise.hlsl:145-150): dot(permGradients[i % 128].xyz, p), HLSL dot (R4).
+// The LDS copy stores w = -0.0, and fma(gx, x, -0.0) == gx*x bit for bit (x + -0 == x
+// for every non-NaN x, signed zeros included), so consuming w costs nothing and keeps
+// the fetch a full ds_read_b128 (4 LDS cycles) instead of the b96 form (8 cycles).
+__device__ __forceinline__ float gdot(const float4& g, float x, float y, float z)
+{
+    return fma(g.z, z, fma(g.y, y, fma(g.x, x, g.w)));
+}
+
+// noise.hlsl:153-179 (live `#if 1` block)
 __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py, float pz)
 {
+    nz.calls += 1;
     float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
     int32_t Px = (int32_t)fx, Py = (int32_t)fy, Pz = (int32_t)fz;
     float x = px - fx, y = py - fy, z = pz - fz;
     float ux = fade(x), uy = fade(y), uz = fade(z);
+    // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
     uint32_t X = (uint32_t)Px & 127u, Y = (uint32_t)Py & 127u, Z = (uint32_t)Pz & 127u;
     uint32_t t = nz.perm2d[X + (Y << 7)];
-    // Pu = texel + Z, per byte, then & 127 for the table lookup (i % 128)
-    uint32_t a0 = ((t & 0xffu) + Z) & 127u;
-    uint32_t a1 = (((t >> 8) & 0xffu) + Z) & 127u;
-    uint32_t b0 = (((t >> 16) & 0xffu) + Z) & 127u;
-    uint32_t b1 = ((t >> 24) + Z) & 127u;
-    uint32_t ca0 = nz.codes2[a0], ca1 = nz.codes2[a1], cb0 = nz.codes2[b0], cb1 = nz.codes2[b1];
+    // Pu = texel + Pu.z per channel (bytes <= 127+127+1: no carry), % 128
+    uint32_t zz = Z * 0x01010101u;
+    uint32_t w0 = (t + zz) & 0x7f7f7f7fu;               // Pu.x, Pu.y, Pu.z, Pu.w
+    uint32_t w1 = (t + zz + 0x01010101u) & 0x7f7f7f7fu; // Pu.* + ONE_PIXEL
+    const float4* gb = nz.grad + nz.slot;
+    const float4 ga0 = gb[(w0 & 0xffu) << 4];
+    const float4 ga1 = gb[((w0 >> 8) & 0xffu) << 4];
+    const float4 gb0 = gb[((w0 >> 16) & 0xffu) << 4];
+    const float4 gb1 = gb[(w0 >> 24) << 4];
+    const float4 ha0 = gb[(w1 & 0xffu) << 4];
+    const float4 ha1 = gb[((w1 >> 8) & 0xffu) << 4];
+    const float4 hb0 = gb[((w1 >> 16) & 0xffu) << 4];
+    const float4 hb1 = gb[(w1 >> 24) << 4];
     float x1 = x + -1.0f, y1 = y + -1.0f, z1 = z + -1.0f;
-    float g000 = gdot(ca0, x, y, z);
-    float g100 = gdot(cb0, x1, y, z);
-    float g010 = gdot(ca1, x, y1, z);
-    float g110 = gdot(cb1, x1, y1, z);
-    float g001 = gdot(ca0 >> 4, x, y, z1);
-    float g101 = gdot(cb0 >> 4, x1, y, z1);
-    float g011 = gdot(ca1 >> 4, x, y1, z1);
-    float g111 = gdot(cb1 >> 4, x1, y1, z1);
+    float g000 = gdot(ga0, x, y, z);
+    float g100 = gdot(gb0, x1, y, z);
+    float g010 = gdot(ga1, x, y1, z);
+    float g110 = gdot(gb1, x1, y1, z);
+    float g001 = gdot(ha0, x, y, z1);
+    float g101 = gdot(hb0, x1, y, z1);
+    float g011 = gdot(ha1, x, y1, z1);
+    float g111 = gdot(hb1, x1, y1, z1);
     float l0 = rtm::lerp(rtm::lerp(g000, g100, ux), rtm::lerp(g010, g110, ux), uy);
     float l1 = rtm::lerp(rtm::lerp(g001, g101, ux), rtm::lerp(g011, g111, ux), uy);
     return rtm::lerp(l0, l1, uz);
@@ -90,6 +102,7 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
     // N = 1 .. floor(detail); detail <= 17.79 so N <= 17 (RT_NP_OCTAVES)
+    #pragma unroll 1
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
         if (!((float)N <= detail)) break;
         float S = c.k->np_scale[N];
@@ -300,7 +313,10 @@ __device__ __forceinline__ f3 get_normal(const Ctx& c, f4 pd)
     float dist = rtm::length(rtm::sub(p, c.eye));
     float nd = dist * 0.005f;
     float dx = get_density<L>(c, rtm::mk(p.x - nd, p.y - 0.0f, p.z - 0.0f)) - pd.w;
+    // serialise the three independent density evaluations (register pressure)
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z), "+v"(nd) : "v"(dx));
     float dy = get_density<L>(c, rtm::mk(p.x - 0.0f, p.y - nd, p.z - 0.0f)) - pd.w;
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z), "+v"(nd) : "v"(dy));
     float dz = get_density<L>(c, rtm::mk(p.x - 0.0f, p.y - 0.0f, p.z - nd)) - pd.w;
     return rtm::normalize(rtm::mk(dx, dy, dz));
 }
@@ -331,7 +347,10 @@ __device__ __forceinline__ float get_space_color(const Ctx& c, f3 dir)
     dir = mod_ray_dir(dir);
     if (dir.y <= 0.0f) return 0.0f;
     float space = noise3d(c.nz, dir.x * 500.0f, dir.y * 500.0f, dir.z * 500.0f);
+    // serialise the three independent lattice evaluations (register pressure)
+    asm volatile("" : "+v"(dir.x), "+v"(dir.y), "+v"(dir.z) : "v"(space));
     space = space - fma(noise3d(c.nz, dir.x * 150.2f, dir.y * 150.2f, dir.z * 150.2f), 0.5f, 0.13f);
+    asm volatile("" : "+v"(dir.x), "+v"(dir.y), "+v"(dir.z) : "v"(space));
     space = space - fma(noise3d(c.nz, dir.x * 200.2f, dir.y * 200.2f, dir.z * 200.2f), 0.5f, 0.5f);
     return (space * 1.0f) * rtm::sat(fma(-c.sun.y, 2.7f, -0.5f));
 }
@@ -420,6 +439,7 @@ __device__ __forceinline__ ShadePre shade_pre(const Ctx& c, f3 p, f3 n, f3 d, fl
         float s = 0.0f;
         if constexpr (L == RT_NOMADPLAINS) {
             f3 q = rtm::mk(p.y * 0.5f, p.x * 0.01f, p.z * 0.01f);
+            #pragma unroll 1
             for (int N = 1; N <= 20; ++N) {
                 float S = c.k->col_scale[N];
                 s = fma(rtm::abs(noise3d(c.nz, q.x * S, q.y * S, q.z * S)), c.k->col_rcp[N], s);

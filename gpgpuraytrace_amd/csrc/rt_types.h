@@ -54,4 +54,5 @@ struct RtStats {
     unsigned long long shadow_steps;
     unsigned long long prepass_steps;
     unsigned long long hits;
+    unsigned long long noise_calls;
 };

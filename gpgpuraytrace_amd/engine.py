@@ -89,6 +89,7 @@ class Texture:
         h = C.c_void_p()
         check(lib().rt_texture_create(device._h, C.byref(h)), "texture_create")
         self._h = h.value
+        self._device = device
 
     def create(self, dimensions, fmt, width, height, data, binding=0, cpu_flags=0):
         a = np.ascontiguousarray(data)
@@ -96,7 +97,7 @@ class Texture:
 
     def __del__(self):
         try:
-            if self._h:
+            if self._h and self._device._h:   # a destroyed device already freed its textures
                 lib().rt_texture_destroy(self._h)
         except Exception:
             pass
@@ -147,7 +148,7 @@ class Compute:
 
     def __del__(self):
         try:
-            if self._h:
+            if self._h and self.device._h:    # a destroyed device already freed its computes
                 lib().rt_compute_destroy(self._h)
         except Exception:
             pass

@@ -58,6 +58,7 @@ typedef struct {
     unsigned long long shadow_steps;  /* traceRay iterations, shadow rays */
     unsigned long long prepass_steps; /* traceRay iterations, camerarays */
     unsigned long long hits;          /* primary hits == shadow rays */
+    unsigned long long noise_calls;   /* noise3d evaluations (BASELINE.md algorithmic work unit) */
 } rt_stats;
 
 /* ---- diagnostics ---- */
@@ -88,6 +89,11 @@ void* rt_device_framebuffer(rt_device dev);       /* device pointer, W*H uint32 
 void* rt_device_stream(rt_device dev);            /* hipStream_t */
 int rt_device_set_stream(rt_device dev, void* hip_stream); /* NULL = the device's own stream */
 int rt_device_stats(rt_device dev, rt_stats* out, int reset); /* needs RT_DEVICE_STATS */
+/* HIP-event timing of the dominant kernel (tracescreen) on the device stream:
+ * enable, then rt_device_kernel_time returns the summed elapsed ms and launch count
+ * since the last call (synchronises). */
+int rt_device_set_profiling(rt_device dev, int enable);
+int rt_device_kernel_time(rt_device dev, double* total_ms, int* launches);
 
 /* ---- ITexture (IDevice::createTexture + ITexture::create(dims, fmt, w, h, data, binding, cpu)) ---- */
 int rt_texture_create(rt_device dev, rt_texture* out);

@@ -22,9 +22,8 @@
  *      maximumNumber/minimumNumber); saturate(x) = min(max(x,0),1);
  *  R7  compile-time constants (`const static`) are folded in double from the
  *      float literals and rounded once to float;
- *  R8  gradperm's dot with a gradient in {-1,0,1}^3 sums the two non-zero
- *      signed components in x,y,z order (value-identical to the full dot: the
- *      products are exact and the zero component adds nothing).
+ *  R8  (noise) gradperm is HLSL dot() under R4 with the permGradients values
+ *      as given (any gradient table, not only Noise.cpp's {-1,0,1} set);
  *  R9  output quantisation to R8G8B8A8_UNORM: rint(saturate(c) * 255).
  */
 #include "rt_oracle.h"
@@ -270,21 +269,11 @@ static void ctx_init(ctx* c, const ro_noise* nz, const ro_frame* fr)
     c->density_calls = 0;
 }
 
-/* noise.hlsl:145-150 gradperm, R8 */
+/* noise.hlsl:145-150 gradperm: dot(permGradients[x % 128].xyz, p) under R4 */
 static inline float gradperm(const ctx* c, uint32_t i, float x, float y, float z)
 {
     const float* g = c->nz->grad + (i % 128u) * 4;
-    float q[3] = {x, y, z};
-    float acc = 0.0f;
-    int first = 1;
-    for (int k = 0; k < 3; ++k) {
-        if (g[k] != 0.0f) {
-            float t = g[k] * q[k];
-            acc = first ? t : acc + t;
-            first = 0;
-        }
-    }
-    return acc;
+    return fmaf(g[2], z, fmaf(g[1], y, g[0] * x));
 }
 
 /* noise.hlsl:139-142 */
@@ -749,7 +738,8 @@ static f3 trace_sample(ctx* c, const sky_consts* k, f3 pp, f3 pdir, f3 pdn, floa
     f3 color;
     if (rr.density > 0.0f) {
         *hits += 1;
-        f3 n = get_normal(c, rr.pd);
+        f4 npd = {rr.pd.x, rr.pd.y, rr.pd.z, rr.density}; /* getNormal(float4(rr.pd.xyz, rr.density)) :31 */
+        f3 n = get_normal(c, npd);
         color = get_color(c, v3(rr.pd.x, rr.pd.y, rr.pd.z), n, pdn, rr.pd.w, shadow_steps);
         color = v3(lerp(color.x, rr.fcolord.x, rr.fcolord.w), lerp(color.y, rr.fcolord.y, rr.fcolord.w),
                    lerp(color.z, rr.fcolord.z, rr.fcolord.w));
