@@ -78,6 +78,8 @@ SIGNATURES = {
     "rt_shard_unpack": (_i, [_vp, _i, _i, _vp]),
     "rt_noise_generate": (_i, [C.c_uint32, _i, _vp, _vp]),
     "rt_terrain_set_target_depths": (_i, [_vp, _vp]),
+    "rt_debug_math": (_i, [_vp, _i, _vp, _vp, _vp, _i]),
+    "rt_debug_noise": (_i, [_vp, _vp, _vp, _i, _i]),
 }
 
 

@@ -49,3 +49,7 @@ inline size_t rt_shard_tiles(int w, int h, int rank, int count)
 }
 // pack != 0: framebuffer tiles of shard `rank` -> packed (1024 px per tile); else packed -> framebuffer.
 void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack);
+
+// diagnostics (primitive-level parity tests)
+void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n);
+void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int n, int density);

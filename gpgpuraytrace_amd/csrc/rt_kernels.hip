@@ -549,3 +549,64 @@ void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, 
     if (n == 0) return;
     hipLaunchKernelGGL(k_shard_copy, dim3((unsigned)n), dim3(256), 0, s, fb, packed, w, h, rank, count, pack);
 }
+
+// ---------------------------------------------------------------------------
+// Diagnostics: device evaluation of the numeric primitives, noise3d and
+// getDensity for the primitive-level parity tests (tests/test_gpu_parity.py).
+namespace {
+
+__global__ void k_debug_math(int op, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y,
+                             int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float x = a[i], v = 0.0f;
+    switch (op) {
+    case 0: v = rtm::exp2(x); break;
+    case 1: v = rtm::log2(x); break;
+    case 2: v = rtm::exp(x); break;
+    case 3: v = rtm::sin(x); break;
+    case 4: v = rtm::cos(x); break;
+    case 5: v = rtm::sqrt(x); break;
+    case 6: v = rtm::rcp(x); break;
+    case 7: v = rtm::rcp(rtm::sqrt(x)); break;
+    case 8: v = rtm::pow(x, b[i]); break;
+    case 9: v = rtm::max(x, b[i]); break;
+    case 10: v = rtm::min(x, b[i]); break;
+    case 11: v = rtm::pow_nonneg(x, b[i]); break;
+    default: v = 0.0f; break;
+    }
+    y[i] = v;
+}
+
+template <int L>
+__global__ void __launch_bounds__(256) k_debug_noise(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                     const float4* __restrict__ grad, const float* __restrict__ xyz,
+                                                     float* __restrict__ out, int n, int density)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ctx c = make_ctx(k, lds);
+    f3 p = rtm::mk(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
+    out[i] = density ? get_density<L>(c, p) : noise3d(c.nz, p.x, p.y, p.z);
+}
+
+} // namespace
+
+void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n)
+{
+    hipLaunchKernelGGL(k_debug_math, dim3((n + 255) / 256), dim3(256), 0, s, op, a, b, y, n);
+}
+
+void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int n, int density)
+{
+    dim3 g((n + 255) / 256), b(256);
+    switch (a.landscape) {
+    case RT_TESTING: hipLaunchKernelGGL(k_debug_noise<RT_TESTING>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
+    case RT_SIMPLE: hipLaunchKernelGGL(k_debug_noise<RT_SIMPLE>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
+    case RT_GREENROCKS: hipLaunchKernelGGL(k_debug_noise<RT_GREENROCKS>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
+    default: hipLaunchKernelGGL(k_debug_noise<RT_NOMADPLAINS>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
+    }
+}

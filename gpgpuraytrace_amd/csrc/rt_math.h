@@ -212,7 +212,8 @@ RT_HD void sincos(float x, float* s, float* c)
     float sv = fma(r * u, ps, r);
     float pc = fma(fma(fma(0x1.9906cap-16f, u, -0x1.6c0786p-10f), u, 0x1.55553ap-5f), u, -0.5f);
     float cv = fma(u, pc, 1.0f);
-    int q = ((int)k) & 3;
+    // quadrant k mod 4 with exact float ops (no out-of-range float->int conversion)
+    int q = (int)(k - 4.0f * floor(k * 0.25f));
     float so = (q & 1) ? cv : sv;
     float co = (q & 1) ? sv : cv;
     if (q == 2 || q == 3) so = -so;

@@ -978,3 +978,45 @@ extern "C" int rt_terrain_set_target_depths(const float* cr, float* cells)
     }
     return RT_OK;
 }
+
+// ---- diagnostics ------------------------------------------------------------
+extern "C" int rt_debug_math(rt_device d, int op, const float* a, const float* b, float* y, int n)
+{
+    if (!d || !a || !y || n <= 0) return fail(RT_ERR_INVALID, "bad arguments");
+    float *da = nullptr, *db = nullptr, *dy = nullptr;
+    size_t bytes = (size_t)n * 4;
+    HIP_TRY(hipMalloc(&da, bytes));
+    HIP_TRY(hipMalloc(&db, bytes));
+    HIP_TRY(hipMalloc(&dy, bytes));
+    HIP_TRY(hipMemcpy(da, a, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(db, b ? b : a, bytes, hipMemcpyHostToDevice));
+    rt_launch_debug_math(d->stream, op, da, db, dy, n);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    HIP_TRY(hipMemcpy(y, dy, bytes, hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(da));
+    HIP_TRY(hipFree(db));
+    HIP_TRY(hipFree(dy));
+    return RT_OK;
+}
+
+// Evaluate noise3d (density = 0) or the compute's landscape getDensity (density = 1)
+// at n points with the compute's current tables and constants.
+extern "C" int rt_debug_noise(rt_compute c, const float* xyz, float* out, int n, int density)
+{
+    if (!c || !c->shader || !xyz || !out || n <= 0) return fail(RT_ERR_INVALID, "bad arguments");
+    rt_device dev = c->dev;
+    int rc;
+    if ((rc = check_texture(c->shader)) || (rc = sync_shader(dev, c->shader))) return rc;
+    float *dx = nullptr, *dy = nullptr;
+    HIP_TRY(hipMalloc(&dx, (size_t)n * 12));
+    HIP_TRY(hipMalloc(&dy, (size_t)n * 4));
+    HIP_TRY(hipMemcpyAsync(dx, xyz, (size_t)n * 12, hipMemcpyHostToDevice, dev->stream));
+    rt_launch_debug_noise(make_launch(dev, c->shader), dx, dy, n, density);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, dy, (size_t)n * 4, hipMemcpyDeviceToHost, dev->stream));
+    HIP_TRY(hipStreamSynchronize(dev->stream));
+    HIP_TRY(hipFree(dx));
+    HIP_TRY(hipFree(dy));
+    return RT_OK;
+}

@@ -165,6 +165,16 @@ int rt_noise_generate(uint32_t seed, int rand_kind, uint8_t* perm2d, float* grad
  * CellDistance float2[1024], for engines that keep the reference's readback round trip. */
 int rt_terrain_set_target_depths(const float* camera_results, float* cell_distance);
 
+/* ---- diagnostics (primitive-level parity tests; no reference counterpart) ----
+ * rt_debug_math: device evaluation of the numeric primitives of DESIGN.md §Numerics
+ *   (op 0 exp2, 1 log2, 2 exp, 3 sin, 4 cos, 5 sqrt, 6 rcp, 7 rsqrt, 8 pow, 9 max,
+ *   10 min, 11 pow for x >= 0); host arrays of n floats (b may be NULL for unary ops).
+ * rt_debug_noise: noise3d (density = 0, noise.hlsl:153-179) or the compute's landscape
+ *   getDensity (density = 1) at n points (xyz interleaved), with the compute's
+ *   current tables and constants. */
+int rt_debug_math(rt_device dev, int op, const float* a, const float* b, float* out, int n);
+int rt_debug_noise(rt_compute cs, const float* xyz, float* out, int n, int density);
+
 #ifdef __cplusplus
 }
 #endif

@@ -125,7 +125,8 @@ static void sincos_red(float x, float* s, float* c)
     float sv = fmaf(r * u, ps, r);
     float pc = fmaf(fmaf(fmaf(0x1.9906cap-16f, u, -0x1.6c0786p-10f), u, 0x1.55553ap-5f), u, -0.5f);
     float cv = fmaf(u, pc, 1.0f);
-    int q = ((int)k) & 3;
+    /* quadrant k mod 4 with exact float ops (no out-of-range float->int conversion) */
+    int q = (int)(k - 4.0f * floorf(k * 0.25f));
     switch (q) {
     case 0: *s = sv; *c = cv; break;
     case 1: *s = cv; *c = -sv; break;

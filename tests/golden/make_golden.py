@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures (run in the build container).
+
+1. noise_reference_glibc_seed300.npz -- the tables produced by the REFERENCE's own
+   gpuraytrace/Graphics/Noise.cpp (Noise::generate(false), seed 300), compiled in place
+   from /root/reference by oracle/Makefile (`make -C oracle ref`) and run here (glibc
+   rand).  Data only: perm2D bytes + gradient floats.
+2. scene_constants.npz -- frame constants (matrices as the shader sees them) of the
+   fixed benchmark scene, so kernel parity never depends on the camera maths.
+3. oracle_frames.npz -- small frames rendered by the C oracle (oracle/rt_oracle.c):
+   regression pins of the restatement itself (self-generated, NOT reference outputs).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import oracle_lib as O  # noqa: E402
+from gpgpuraytrace_amd import camera as cam  # noqa: E402
+
+POSES = {"reset": cam.INITIAL_ROTATION_EULER, "lookdown": cam.LOOKDOWN_ROTATION_EULER}
+FRAMES = [  # (landscape, pose, W, H, aa, max_steps)
+    ("nomadplains", "reset", 64, 48, 1, 0),
+    ("nomadplains", "lookdown", 64, 48, 1, 0),
+    ("nomadplains", "reset", 48, 32, 4, 0),
+    ("nomadplains", "reset", 64, 48, 1, 64),
+    ("testing", "reset", 64, 48, 1, 0),
+    ("testing", "lookdown", 64, 48, 1, 0),
+    ("simple", "reset", 48, 32, 1, 0),
+    ("greenrocks", "reset", 48, 32, 1, 0),
+]
+
+
+def frame_key(land, pose, w, h, aa, ms):
+    return f"{land}_{pose}_{w}x{h}_aa{aa}_ms{ms}"
+
+
+def consts_for(w, h, pose):
+    return cam.frame_constants(w, h, euler=POSES[pose])
+
+
+def main():
+    ref_bin = os.path.join(ROOT, "oracle", "_ref", "ref_noise_dump")
+    if not os.path.exists(ref_bin):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    raw = subprocess.run([ref_bin], capture_output=True, check=True).stdout
+    np.savez_compressed(os.path.join(HERE, "noise_reference_glibc_seed300.npz"),
+                        perm2d=np.frombuffer(raw[:65536], np.uint8), grad=np.frombuffer(raw[65536:], np.float32))
+
+    sc = {}
+    for pose in POSES:
+        for (w, h) in ((64, 48), (48, 32), (256, 256), (1920, 1080)):
+            c = consts_for(w, h, pose)
+            for k in ("eye", "view_inverse", "projection", "sun"):
+                sc[f"{pose}_{w}x{h}_{k}"] = np.asarray(c[k], np.float32)
+    np.savez_compressed(os.path.join(HERE, "scene_constants.npz"), **sc)
+
+    nz = O.noise_tables()
+    out = {}
+    for land, pose, w, h, aa, ms in FRAMES:
+        fr = O.make_frame(consts_for(w, h, pose), landscape=O.LANDSCAPES[land], aa=aa, max_steps=ms)
+        r = O.render(nz, fr)
+        key = frame_key(land, pose, w, h, aa, ms)
+        out[key + "_rgba32f"] = r["rgba32f"]
+        out[key + "_rgba8"] = r["rgba8"]
+        out[key + "_steps"] = r["primary_steps"]
+        out[key + "_camera_results"] = r["camera_results"]
+        out[key + "_cell_distance"] = r["cell_distance"]
+        s = r["stats"]
+        out[key + "_stats"] = np.array([s["noise3d_calls"], s["prepass_steps"], s["primary_steps"],
+                                        s["shadow_steps"], s["primary_rays"], s["primary_hits"]], np.uint64)
+        print(key, s)
+    np.savez_compressed(os.path.join(HERE, "oracle_frames.npz"), **out)
+
+
+if __name__ == "__main__":
+    main()

@@ -12,7 +12,7 @@ import numpy as np
 f32 = np.float32
 RESET_EYE = (0.0, 100.0, 0.0)
 RESET_EULER = (-3.0, -4.6, 0.0)      # Camera.cpp:10
-LOOKDOWN_EULER = (-2.3, -4.6, 0.0)   # build's second, hit-heavy pose (documented in DESIGN.md)
+LOOKDOWN_EULER = (-3.6, -4.6, 0.0)   # build's second, hit-heavy pose
 TIME_OF_DAY = 0.3                    # Raytracer.cpp:31
 
 

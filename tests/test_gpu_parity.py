@@ -1,0 +1,286 @@
+"""GPU parity tests (MI355X): the HIP path through the C-ABI vs the oracle /
+golden fixtures.  Bar: bit-exact float32 colours and UNORM8 pixels, identical
+step / noise3d counts.  Run on the GPU box with `pytest -m gpu`."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import golden_index as GI
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+class FixedCamera:
+    """Feeds the fixture's frame constants through the Terrain/ShaderVariable path."""
+
+    def __init__(self, consts):
+        self.c = consts
+        self.width, self.height = consts["width"], consts["height"]
+
+    def view_inverse_hlsl(self):
+        return np.asarray(self.c["view_inverse"], np.float32)
+
+    def projection_hlsl(self):
+        return np.asarray(self.c["projection"], np.float32)
+
+    def eye(self):
+        return np.asarray(self.c["eye"], np.float32)
+
+
+def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
+         pipeline="split"):
+    import gpgpuraytrace_amd as G
+    os.environ["RT_PIPELINE"] = pipeline
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
+                                    stats=stats)
+    assert dev is not None, G.lib().rt_last_error()
+    ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
+                    rand_kind=rand_kind)
+    ter.create()
+    assert ter.reload(), G.lib().rt_last_error()
+    ter.set_camera(FixedCamera(consts))
+    ter.set_time_of_day_vec(consts["sun"])
+    ter.update_shaders()
+    return dev, ter
+
+
+def bits_equal(a, b):
+    a32, b32 = np.asarray(a, np.float32).view(np.uint32), np.asarray(b, np.float32).view(np.uint32)
+    both_nan = np.isnan(np.asarray(a, np.float32)) & np.isnan(np.asarray(b, np.float32))
+    return np.all((a32 == b32) | both_nan)
+
+
+# --- numeric primitives -----------------------------------------------------------------
+def _special():
+    return np.array([0.0, -0.0, 1.0, -1.0, 0.5, 2.0, 1e-38, 1e-45, 3.4e38, np.inf, -np.inf, np.nan, 127.5, -149.9,
+                     1.41421354, 0.70710677], np.float32)
+
+
+@pytest.mark.parametrize("gop,oop,rng_lo,rng_hi,logspace", [
+    (0, 0, -160, 140, False), (1, 1, -90, 90, True), (2, 2, -100, 90, False), (3, 3, -3e3, 3e3, False),
+    (4, 4, -3e3, 3e3, False), (5, 5, -90, 90, True), (6, 6, -90, 90, True), (7, 7, -90, 90, True)])
+def test_unary_primitives_bitexact(gop, oop, rng_lo, rng_hi, logspace):
+    import gpgpuraytrace_amd as G
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, 8, 8)
+    rng = np.random.default_rng(gop)
+    x = rng.uniform(rng_lo, rng_hi, 200000)
+    x = (np.exp(x) if logspace else x).astype(np.float32)
+    x = np.concatenate([x, _special(), -_special()])
+    y = np.empty_like(x)
+    assert G.lib().rt_debug_math(dev._h, gop, x.ctypes.data, None, y.ctypes.data, x.size) == 0
+    assert bits_equal(y, O.unary(oop, x))
+    dev.destroy()
+
+
+@pytest.mark.parametrize("gop,oop", [(8, 0), (9, 1), (10, 2), (11, 0)])
+def test_binary_primitives_bitexact(gop, oop):
+    import gpgpuraytrace_amd as G
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, 8, 8)
+    rng = np.random.default_rng(10 + gop)
+    a = np.exp(rng.uniform(-40, 40, 200000)).astype(np.float32)
+    b = rng.uniform(-4, 41, 200000).astype(np.float32)
+    if gop != 11:
+        a = np.concatenate([a * np.sign(rng.uniform(-1, 1, a.size)).astype(np.float32), _special()])
+        b = np.concatenate([b, _special()[::-1]])
+    else:
+        b = np.abs(b) + np.float32(0.01)  # pow for x >= 0, y > 0 (the hot-path form)
+    y = np.empty_like(a)
+    assert G.lib().rt_debug_math(dev._h, gop, a.ctypes.data, b.ctypes.data, y.ctypes.data, a.size) == 0
+    assert bits_equal(y, O.binary(oop, a, b))
+    dev.destroy()
+
+
+# --- noise3d and getDensity ---------------------------------------------------------------
+@pytest.mark.parametrize("seed,kind", [(300, 0), (777, 1)])
+def test_noise3d_bitexact(seed, kind):
+    import gpgpuraytrace_amd as G
+    consts = GI.consts(64, 48, "reset")
+    dev, ter = make(consts, seed=seed, rand_kind=kind)
+    rng = np.random.default_rng(5)
+    p = np.concatenate([rng.uniform(-500, 500, (100000, 3)), rng.uniform(-2e6, 2e6, (20000, 3)),
+                        rng.integers(-300, 300, (2000, 3))]).astype(np.float32)
+    out = np.empty(len(p), np.float32)
+    assert G.lib().rt_debug_noise(ter.compute._h, p.ctypes.data, out.ctypes.data, len(p), 0) == 0
+    assert bits_equal(out, O.noise3d(O.noise_tables(seed, kind), p))
+    dev.destroy()
+
+
+@pytest.mark.parametrize("land", ["nomadplains", "testing", "simple", "greenrocks"])
+def test_density_bitexact(land):
+    import gpgpuraytrace_amd as G
+    consts = GI.consts(64, 48, "reset")
+    dev, ter = make(consts, land=land)
+    rng = np.random.default_rng(6)
+    p = np.concatenate([rng.uniform(-3000, 3000, (30000, 3)) * [1, 0.05, 1] + [0, 50, 0],
+                        rng.uniform(-20, 20, (5000, 3)) + [0, 100, 0]]).astype(np.float32)
+    out = np.empty(len(p), np.float32)
+    assert G.lib().rt_debug_noise(ter.compute._h, p.ctypes.data, out.ctypes.data, len(p), 1) == 0
+    fr = O.make_frame(consts, landscape=O.LANDSCAPES[land])
+    assert bits_equal(out, O.density(O.noise_tables(), fr, p))
+    dev.destroy()
+
+
+# --- whole frames vs the golden oracle frames ----------------------------------------------
+@pytest.mark.parametrize("pipeline", ["split", "mega"])
+@pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
+def test_frame_bitexact_device_path(spec, pipeline):
+    gold = GI.load()
+    land, pose, w, h, aa, ms = spec
+    key = GI.frame_key(*spec)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True, pipeline=pipeline)
+    ter.render_device()
+    dev.present()
+    img, img8 = dev.readback_float(), dev.readback()
+    st = dev.stats()
+    assert bits_equal(img, gold[key + "_rgba32f"])
+    assert np.array_equal(img8, gold[key + "_rgba8"])
+    ref = gold[key + "_stats"]  # noise3d, prepass, primary, shadow, rays, hits
+    assert (st["noise_calls"], st["prepass_steps"], st["primary_steps"], st["shadow_steps"], st["hits"]) == \
+        (ref[0], ref[1], ref[2], ref[3], ref[5])
+    assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
+    dev.destroy()
+
+
+def _device_cells(ter):
+    """CellDistance as computed on the device (SRV arrays have no map(), so copy directly)."""
+    import gpgpuraytrace_amd as G
+    p = ter.var_cell_distance.device_pointer()
+    out = np.empty((1024, 2), np.float32)
+    G.lib().rt_device_synchronize(ter.device._h)
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert lib.hipMemcpy(out.ctypes.data, p, out.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return out
+
+
+@pytest.mark.parametrize("spec", [GI.FRAMES[0], GI.FRAMES[1], GI.FRAMES[4]], ids=["np_reset", "np_down", "testing"])
+def test_frame_bitexact_reference_call_sequence(spec):
+    """Terrain::render's own sequence: run(2,2,1) -> CameraResults map/unmap -> host
+    setTargetDepths -> CellDistance write -> per-tile ThreadOffset write + run + flush."""
+    gold = GI.load()
+    land, pose, w, h, aa, ms = spec
+    key = GI.frame_key(*spec)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms)
+    ter.render()
+    dev.present()
+    assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])
+    assert np.array_equal(ter.camera_view, gold[key + "_camera_results"])
+    dev.destroy()
+
+
+def test_tiled_dispatch_1280x720_rows():
+    """2x2 tiles of 640x360 with 16x18 groups (Terrain.cpp:208-242) through the compat path."""
+    consts = _consts_1080p_like(1280, 720)
+    dev, ter = make(consts)
+    assert (ter.tiles_x, ter.tiles_y, ter.thread_x, ter.thread_y) == (2, 2, 16, 18)
+    ter.render()
+    img = dev.readback_float()
+    fr = O.make_frame(consts, rows=(0, 720, 48))
+    ref = np.zeros((720, 1280, 4), np.float32)
+    cd = np.zeros(2048, np.float32)
+    cr = np.zeros(4096, np.float32)
+    O.lib().ro_camerarays(C.byref(O.noise_tables()), C.byref(fr), O._fp(cr), None)
+    O.lib().ro_set_target_depths(O._fp(cr), O._fp(cd))
+    O.lib().ro_tracescreen(C.byref(O.noise_tables()), C.byref(fr), O._fp(cd), O._fp(ref), None, None, None)
+    assert bits_equal(img[0::48], ref[0::48])
+    dev.destroy()
+
+
+def _consts_1080p_like(w, h, pose="reset"):
+    from gpgpuraytrace_amd import camera
+    euler = camera.INITIAL_ROTATION_EULER if pose == "reset" else camera.LOOKDOWN_ROTATION_EULER
+    return camera.frame_constants(w, h, euler=euler)
+
+
+@pytest.mark.parametrize("pose", ["reset", "lookdown"])
+def test_1080p_full_frame_rows_and_properties(pose):
+    """BASELINE size: bit-exact on a row sample vs the oracle, plus whole-frame properties
+    (prepass + cells exact, every pixel written, alpha 255)."""
+    gold_scene = GI.consts(1920, 1080, pose)
+    dev, ter = make(gold_scene, stats=True)
+    ter.render_device()
+    img = dev.readback_float()
+    img8 = dev.readback()
+    st = dev.stats()
+    fr = O.make_frame(gold_scene, rows=(0, 1080, 54))
+    ref = np.zeros((1080, 1920, 4), np.float32)
+    cr = np.zeros(4096, np.float32)
+    cd = np.zeros(2048, np.float32)
+    ost = O.Stats()
+    O.lib().ro_camerarays(C.byref(O.noise_tables()), C.byref(fr), O._fp(cr), C.byref(ost))
+    O.lib().ro_set_target_depths(O._fp(cr), O._fp(cd))
+    O.lib().ro_tracescreen(C.byref(O.noise_tables()), C.byref(fr), O._fp(cd), O._fp(ref), None, None, C.byref(ost))
+    assert bits_equal(img[0::54], ref[0::54])
+    assert np.array_equal(_device_cells(ter), cd.reshape(1024, 2))
+    assert np.all(img8[..., 3] == 255) and np.all(img[..., 3] == 1.0)
+    assert st["prepass_steps"] == ost.prepass_steps
+    dev.destroy()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_shards_assemble_to_full_frame(world):
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    consts = GI.consts(256, 256, "reset")
+    full_dev, full_ter = make(consts)
+    full_ter.render_device()
+    full = full_dev.readback()
+    devs = [make(consts) for _ in range(world)]
+    maxb = max(E.shard_bytes(d, r, world) for r, (d, _) in enumerate(devs))
+    bufs = [torch.zeros(maxb, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    for r, (d, t) in enumerate(devs):
+        t.render_device(r, world)
+        E.shard_pack(d, r, world, bufs[r].data_ptr())
+        d.synchronize()
+    d0 = devs[0][0]
+    for r in range(1, world):
+        E.shard_unpack(d0, r, world, bufs[r].data_ptr())
+    assert np.array_equal(d0.readback(), full)
+    for d, _ in devs:
+        d.destroy()
+    full_dev.destroy()
+
+
+@pytest.mark.parametrize("land", ["nomadplains", "greenrocks"])
+def test_recording_macro_bitexact(land):
+    consts = GI.consts(48, 32, "reset")
+    dev, ter = make(consts, land=land, recording=True)
+    ter.render_device()
+    r = O.render(O.noise_tables(), O.make_frame(consts, landscape=O.LANDSCAPES[land], recording=1))
+    assert bits_equal(dev.readback_float(), r["rgba32f"])
+    dev.destroy()
+
+
+def test_random_seed_tables_bitexact():
+    consts = GI.consts(48, 32, "lookdown")
+    dev, ter = make(consts, seed=424242, rand_kind=1)
+    ter.render_device()
+    r = O.render(O.noise_tables(424242, 1), O.make_frame(consts))
+    assert bits_equal(dev.readback_float(), r["rgba32f"])
+    dev.destroy()
+
+
+def test_reference_error_behaviour():
+    import gpgpuraytrace_amd as G
+    consts = GI.consts(64, 48, "reset")
+    dev, ter = make(consts)
+    cs = dev.create_compute()
+    assert not cs.create("shaders", "nosuch.hlsl", "CSMain", (16, 16, 1))
+    assert not cs.create("shaders", "tracescreen.hlsl", "CSMain", (16, 16, 1), [("AA_SAMPLES", "3")])
+    assert cs.create("shaders", "tracescreen.hlsl", "CSMain", (16, 16, 1))
+    cs.run(1, 1, 1)  # no current shader before swap(): silent no-op (ComputeDirect3D.cpp:532)
+    assert cs.swap() and not cs.swap()
+    assert cs.get_variable("NoSuchVar") is None and cs.get_buffer("CBFrame") is None
+    assert cs.get_array("CellDistance").map() is None       # SRV: map unsupported
+    cam = ter.camera_compute.get_array("CameraResults")
+    assert cam.write(np.zeros((1024, 4), np.float32)) is False  # UAV: write unsupported
+    with pytest.raises(G.NativeError):
+        cs.run(1, 1, 1)  # texture stage 0 not bound
+    G.vfs_add_path("Media/benchmark")
+    assert not cs.create("shaders", "tracescreen.hlsl", "CSMain", (16, 16, 1))  # benchmark does not compile
+    G.vfs_add_path("Media/nomadplains")
+    dev.destroy()
