@@ -5,20 +5,11 @@
 
 #include "rt_types.h"
 
-// Compacted primary hit (split pipeline): 48 bytes.
-struct RtHit {
-    uint32_t sample;  // (py*W + px)*AA + aa
-    float density;    // RayResult.density (> 0)
-    float pad0, pad1;
-    float4 pd;        // RayResult.pd (hit position, dist)
-    float4 fog;       // RayResult.fcolord
-};
-
 // work counters (one 64-byte block, zeroed per launch)
-enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2 };
+enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2, RT_CTR_FINISH = 3 };
 #define RT_CTR_BYTES 64
 
-enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1 };
+enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2 };
 
 struct RtLaunch {
     hipStream_t stream;
@@ -30,8 +21,10 @@ struct RtLaunch {
     uint32_t* queue;          // RT_CTR_BYTES of device work counters
     int num_cus;              // compute units (persistent grid size)
     int pipeline;             // RT_PIPELINE_*
-    float4* samples;          // split pipeline: W*H*AA saturated sample colours
-    RtHit* hits;              // split pipeline: W*H*AA compacted hit records
+    // split pipeline, rt_split_samples() entries each (sample t, see rt_kernels.hip)
+    float4* samples;          // saturated colour of hit samples (written by S, read by R)
+    float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
+    uint32_t* hitlist;        // compacted sample ids of primary hits
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);
@@ -42,6 +35,11 @@ void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out
                            uint32_t off_y, uint32_t ext_x, uint32_t ext_y, uint32_t tile_first, uint32_t tile_stride);
 
 #define RT_TILE 32
+// samples the split pipeline addresses for a w x h frame: whole 32x32 tiles x AA
+inline size_t rt_split_samples(int w, int h, int aa)
+{
+    return (size_t)((w + RT_TILE - 1) / RT_TILE) * ((h + RT_TILE - 1) / RT_TILE) * RT_TILE * RT_TILE * (size_t)aa;
+}
 inline size_t rt_shard_tiles(int w, int h, int rank, int count)
 {
     size_t tx = (size_t)(w + RT_TILE - 1) / RT_TILE, ty = (size_t)(h + RT_TILE - 1) / RT_TILE, total = tx * ty;

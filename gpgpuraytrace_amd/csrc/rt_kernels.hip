@@ -21,19 +21,27 @@ using rtm::f3;
 
 namespace {
 
-// LDS image: lane-private gradients (32 KiB) then the perm2D lattice (64 KiB).
-constexpr int kGradWords = 128 * 16 * 4;
+// LDS image: paired lane-private gradients gxy (32 KiB) + gz (32 KiB), then the
+// perm2D lattice (64 KiB); see rts::NoiseView.
+constexpr int kGxyWords = 128 * 16 * 4;
+constexpr int kGzWords = 128 * 32 * 2;
+constexpr int kGradWords = kGxyWords + kGzWords;
 constexpr int kPermWords = 128 * 128;
 constexpr int kNoiseLdsWords = kGradWords + kPermWords;
 
 __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __restrict__ perm2d,
                                                const float4* __restrict__ grad)
 {
-    float4* g = reinterpret_cast<float4*>(lds);
+    float4* gxy = reinterpret_cast<float4*>(lds);
     for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) {
-        float4 v = grad[i >> 4];
-        v.w = -0.0f; // see rts::gdot
-        g[i] = v;
+        int e = i >> 4;
+        float4 g0 = grad[e], g1 = grad[(e + 1) & 127];
+        gxy[i] = make_float4(g0.x, g1.x, g0.y, g1.y);
+    }
+    float2* gz = reinterpret_cast<float2*>(lds + kGxyWords);
+    for (int i = threadIdx.x; i < 128 * 32; i += blockDim.x) {
+        int e = i >> 5;
+        gz[i] = make_float2(grad[e].z, grad[(e + 1) & 127].z);
     }
     uint4* p = reinterpret_cast<uint4*>(lds + kGradWords);
     const uint4* src = reinterpret_cast<const uint4*>(perm2d);
@@ -44,9 +52,10 @@ __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __
 __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
 {
     Ctx c;
-    c.nz.grad = reinterpret_cast<const float4*>(lds);
+    c.nz.gxy = reinterpret_cast<const float4*>(lds);
+    c.nz.gz = reinterpret_cast<const float2*>(lds + kGxyWords);
     c.nz.perm2d = lds + kGradWords;
-    c.nz.slot = threadIdx.x & 15u;
+    c.nz.slot = threadIdx.x & 63u;
     c.nz.calls = 0;
     c.k = k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
@@ -78,6 +87,51 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
     if constexpr (STATS) {
         atomicAdd(&stats->prepass_steps, (unsigned long long)rr.steps);
         atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+// camerarays.hlsl:12-21 for nomadplains with one 32-lane group per prepass ray:
+// the prepass is 1024 sequential marches of ~350 steps, so it is bound by the
+// latency of one step, and spreading each step's 17 FBM octaves + steep noise over
+// a lane group (rts::density_nomadplains_group) shortens that chain ~4x.
+template <bool STATS>
+__global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __restrict__ k,
+                                                          const uint32_t* __restrict__ perm2d,
+                                                          const float4* __restrict__ grad, float4* __restrict__ out,
+                                                          RtStats* stats)
+{
+    constexpr int L = RT_NOMADPLAINS;
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const int i = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
+    Ctx c = make_ctx(k, lds);
+    const uint32_t j = threadIdx.x & 31u, base = threadIdx.x & 32u;
+    int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
+    const float r31 = rtm::rcp(31.0f);
+    uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
+    uint32_t pys = (uint32_t)(((float)ty * r31) * k->screen[1]);
+    f3 p, dir;
+    get_pixel_ray(c, (float)pxs, (float)pys, &p, &dir);
+    March<L, false> st;
+    march_begin(c, st, p, RT_CAMERA_NEAR, 2.0f, dir);
+    uint32_t noise = 0;
+    while (march_live<L, false, true>(c, st, RT_CAMERA_FAR, 0)) {
+        march_step_with<L, false, true>(c, st, [&](f3 q) {
+            uint32_t used;
+            float d = density_nomadplains_group(c, q, j, base, &used);
+            noise += used + 1u;
+            return d;
+        });
+    }
+    RayResult rr = march_result(st);
+    if (rr.density < 0.0f) rr.pd.w = RT_CAMERA_FAR;
+    if (j == 0) {
+        out[i] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+        if constexpr (STATS) {
+            atomicAdd(&stats->prepass_steps, (unsigned long long)rr.steps);
+            atomicAdd(&stats->noise_calls, (unsigned long long)noise);
+        }
     }
 }
 
@@ -246,10 +300,15 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
 
 // ===========================================================================
 // Split (wavefront) screen pipeline: the same tracescreen.hlsl:16-76 frame in
-// three passes so each kernel body stays small and every shading lane works on a
-// hit.  P: primary march; misses get their sky colour at once, hits are appended
-// to a compacted queue (wave-aggregated atomics).  S: normal + colour + shadow
-// march + sky blend over the compacted hits.  R: in-order AA average + UNORM8.
+// three passes so every kernel body stays small and lanes stay busy.
+//   P k_march  : primary march (tracing.hlsl:47-105) with lane refill -- each lane
+//                owns one ray and takes the next sample the moment its ray leaves
+//                the loop, so a wave's lanes stay full until the sample queue
+//                drains.  Writes the RayResult of every sample; hits are appended
+//                to a compacted list (staged per wave in LDS, one atomic per 64).
+//   S k_shade  : normal + colour + shadow march + sky blend over the hit list.
+//   R k_finish : sky colour of the misses + in-order AA average + UNORM8.
+// Sample t = (u*64 + j)*AA + a: AA sample a of lane-slot j of 8x8 unit u.
 struct UnitMap {
     uint32_t off_x, off_y, ext_x, ext_y, tiles32_x, tile_first, tile_stride, n_units;
 };
@@ -265,85 +324,210 @@ __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_
     return gx < m.ext_x && gy < m.ext_y && *px < W && *py < H;
 }
 
-__device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane)
+__device__ __forceinline__ bool sample_pixel(const UnitMap& m, uint32_t t, uint32_t aa, uint32_t W, uint32_t H,
+                                             uint32_t* px, uint32_t* py, uint32_t* a)
+{
+    uint32_t pix = t / aa;
+    *a = t - pix * aa;
+    return unit_pixel(m, pix >> 6, pix & 63u, W, H, px, py);
+}
+
+__device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane, uint32_t n = 1u)
 {
     uint32_t u = 0;
-    if (lane == 0) u = atomicAdd(counter, 1u);
+    if (lane == 0) u = atomicAdd(counter, n);
     return __builtin_amdgcn_readfirstlane(u);
 }
 
+// Per-sample RayResult of the primary march: 3 float4 (pd, fcolord, density).
+__device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t t, const RayResult& rr)
+{
+    res[3u * t + 0u] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+    res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
+    res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
+}
+
+// Lanes idle before a wave refills them: amortises the refill's divergent
+// prologue against the idle lanes it leaves (k_march).
+constexpr uint32_t kRefillIdle = 8;
+
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                const float4* __restrict__ grad, const float2* __restrict__ cells,
+                                                UnitMap m, float4* __restrict__ res, uint32_t* __restrict__ hitlist,
+                                                uint32_t* __restrict__ counters, RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
+    __shared__ uint32_t s_stage[16][128];
+    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    const uint32_t n_samples = m.n_units * 64u * aa;
+    const int max_steps = k->max_steps;
+    March<L, true> st;
+    st.d = 0.0f;
+    st.iters = 0;
+    bool live = false;
+    uint32_t t = 0;
+    uint32_t pool = 0, pool_left = 0, staged = 0; // wave-uniform
+    bool drained = false;
+    float psteps = 0.0f;
+    uint32_t nhits = 0;
+    for (;;) {
+        // 1. retire rays that left the loop (tracing.hlsl:68 condition false)
+        bool fin = live && !march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
+        bool hit = fin && st.d > 0.0f;
+        if (fin) {
+            store_ray(res, t, march_result(st));
+            live = false;
+            if constexpr (STATS) psteps += (float)st.iters;
+        }
+        uint64_t hb = __ballot(hit);
+        if (hb) {
+            if (hit) s_stage[wv][staged + (uint32_t)__popcll(hb & lt_mask)] = t;
+            staged += (uint32_t)__popcll(hb);
+            if constexpr (STATS) nhits += hit ? 1u : 0u;
+            if (staged >= 64u) {
+                __builtin_amdgcn_wave_barrier();
+                uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, 64u);
+                uint32_t first = s_stage[wv][lane], second = s_stage[wv][64u + lane];
+                hitlist[b + lane] = first;
+                staged -= 64u;
+                if (lane < staged) s_stage[wv][lane] = second;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        // 2. hand idle lanes new samples from the wave's pool (64 ids per queue atomic)
+        if (!drained) {
+            uint64_t idle = __ballot(!live);
+            if ((uint32_t)__popcll(idle) >= kRefillIdle) {
+                while (idle) {
+                    if (pool_left == 0u) {
+                        uint32_t b = wave_fetch(&counters[RT_CTR_PRIMARY], lane, 64u);
+                        if (b >= n_samples) {
+                            drained = true;
+                            break;
+                        }
+                        pool = b;
+                        pool_left = (n_samples - b) < 64u ? (n_samples - b) : 64u;
+                    }
+                    uint32_t nidle = (uint32_t)__popcll(idle);
+                    uint32_t take = nidle < pool_left ? nidle : pool_left;
+                    bool mine = ((idle >> lane) & 1ull) && (uint32_t)__popcll(idle & lt_mask) < take;
+                    if (mine) {
+                        t = pool + (uint32_t)__popcll(idle & lt_mask);
+                        uint32_t px, py, a;
+                        if (sample_pixel(m, t, aa, W, H, &px, &py, &a)) {
+                            // tracescreen.hlsl:53-62 plane + getPixelRay, tracing.hlsl:49-66 prologue
+                            float pxf = (float)px, pyf = (float)py;
+                            float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
+                            uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
+                            f3 p, dir;
+                            get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
+                            march_begin(c, st, p, s_plane[cell], 1.0f, dir);
+                            if (march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps)) live = true;
+                            else store_ray(res, t, march_result(st)); // empty march: a miss at the near plane
+                        }
+                    }
+                    idle &= ~__ballot(mine);
+                    pool += take;
+                    pool_left -= take;
+                }
+            }
+        }
+        // 3. one march step on every live lane
+        if (__ballot(live) == 0ull) {
+            if (drained) break;
+            continue;
+        }
+        if (live) march_step<L, true, false>(c, st);
+    }
+    if (staged) {
+        __builtin_amdgcn_wave_barrier();
+        uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, staged);
+        if (lane < staged) hitlist[b + lane] = s_stage[wv][lane];
+    }
+    if constexpr (STATS) {
+        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
+        atomicAdd(&stats->hits, (unsigned long long)nhits);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+// Tile-ordered primary march: each wave takes one 8x8 unit at a time (neighbouring
+// pixels march to similar distances, so their FBM octave counts agree and few
+// lanes idle inside noise loops).  The march loop is the wave's own; a wave still
+// on its unit after kPrioSteps[i] iterations raises its issue priority so the few
+// grazing, many-hundred-step units (the kernel's critical path) are not starved
+// by the SIMD's short-unit waves (MI355X_MICROARCH.md: VALU issue is arbitrated
+// by priority, then age).
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                   const float4* __restrict__ grad, const float2* __restrict__ cells,
-                                                  UnitMap m, float4* __restrict__ samples, RtHit* __restrict__ hits,
+                                                  UnitMap m, float4* __restrict__ res, uint32_t* __restrict__ hitlist,
                                                   uint32_t* __restrict__ counters, RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
+    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
+    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
-    const int aa = k->aa_samples;
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    const int max_steps = k->max_steps;
     float psteps = 0.0f;
     uint32_t nhits = 0;
     for (;;) {
         uint32_t u = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
         if (u >= m.n_units) break;
         uint32_t px, py;
-        bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
-        float pxf = (float)px, pyf = (float)py;
+        const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
+        const float pxf = (float)px, pyf = (float)py;
         float plane_x = 0.0f;
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-            uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
-            plane_x = cells[cell].x;
+            plane_x = s_plane[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))];
         }
-        for (int a = 0; a < aa; ++a) {
-            bool hit = false;
-            RtHit rec;
-            uint32_t s = (py * W + px) * (uint32_t)aa + (uint32_t)a;
+        for (uint32_t a = 0; a < aa; ++a) {
+            const uint32_t t = (u * 64u + lane) * aa + a;
+            March<L, true> st;
+            st.d = 0.0f;
+            bool lv = false;
             if (valid) {
                 f3 p, dir;
                 get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
-                RayResult rr = trace_ray<L, true, false>(c, p, plane_x, RT_CAMERA_FAR, 1.0f, dir, k->max_steps);
-                psteps += rr.steps;
-                if (rr.density > 0.0f) {
-                    hit = true;
-                    rec.sample = s;
-                    rec.density = rr.density;
-                    rec.pd = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
-                    rec.fog = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
-                } else {
-                    // tracescreen.hlsl:22-27, :36-38 (miss branch)
-                    f3 pdn = rtm::normalize(dir);
-                    float skyAmount = rr.pd.w * 0.0005f;
-                    skyAmount = rtm::sat(skyAmount * skyAmount);
-                    SkyColor scat = get_rayleigh_mie(c, pdn);
-                    float space = get_space_color(c, pdn);
-                    f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
-                                     (scat.mie.z + scat.rayleigh.z) + space);
-                    f3 col = rtm::mk(rtm::lerp(sky.x, rr.fc.x, rr.fc.w), rtm::lerp(sky.y, rr.fc.y, rr.fc.w),
-                                     rtm::lerp(sky.z, rr.fc.z, rr.fc.w));
-                    col = rtm::mk(rtm::lerp(col.x, sky.x, skyAmount), rtm::lerp(col.y, sky.y, skyAmount),
-                                  rtm::lerp(col.z, sky.z, skyAmount));
-                    samples[s] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
-                }
+                march_begin(c, st, p, plane_x, 1.0f, dir);
+                lv = true;
             }
-            // wave-aggregated append of this wave's hits
-            uint64_t bal = __ballot(hit);
-            uint32_t cnt = (uint32_t)__popcll(bal);
-            if (cnt) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&counters[RT_CTR_HITS], cnt);
-                base = __builtin_amdgcn_readfirstlane(base);
-                if (hit) {
-                    uint32_t idx = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                    hits[idx] = rec;
-                }
-                nhits += hit ? 1u : 0u;
+            __builtin_amdgcn_s_setprio(0);
+            for (uint32_t it = 0;; ++it) {
+                lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
+                if (__ballot(lv) == 0ull) break;
+                if (lv) march_step<L, true, false>(c, st);
+                if (it == 96u) __builtin_amdgcn_s_setprio(1);
+                else if (it == 224u) __builtin_amdgcn_s_setprio(2);
+                else if (it == 384u) __builtin_amdgcn_s_setprio(3);
+            }
+            const bool hit = valid && st.d > 0.0f;
+            if (valid) {
+                RayResult rr = march_result(st);
+                store_ray(res, t, rr);
+                if constexpr (STATS) psteps += rr.steps;
+            }
+            const uint64_t hb = __ballot(hit);
+            if (hb) {
+                uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, (uint32_t)__popcll(hb));
+                if (hit) hitlist[b + (uint32_t)__popcll(hb & lt_mask)] = t;
+                if constexpr (STATS) nhits += hit ? 1u : 0u;
             }
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     if constexpr (STATS) {
         atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
         atomicAdd(&stats->hits, (unsigned long long)nhits);
@@ -353,16 +537,16 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
 
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                const float4* __restrict__ grad, float4* __restrict__ samples,
-                                                const RtHit* __restrict__ hits, uint32_t* __restrict__ counters,
+                                                const float4* __restrict__ grad, UnitMap m,
+                                                const float4* __restrict__ res, const uint32_t* __restrict__ hitlist,
+                                                float4* __restrict__ samples, uint32_t* __restrict__ counters,
                                                 RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
     Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width;
-    const uint32_t aa = (uint32_t)k->aa_samples;
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
     const uint32_t n_units = (n_hits + 63u) / 64u;
     float ssteps = 0.0f;
@@ -371,28 +555,28 @@ __global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, 
         if (u >= n_units) break;
         uint32_t i = u * 64u + lane;
         if (i >= n_hits) continue;
-        RtHit rec = hits[i];
-        uint32_t s = rec.sample, pix = s / aa, a = s - pix * aa;
-        uint32_t px = pix % W, py = pix / W;
+        uint32_t t = hitlist[i];
+        float4 pdw = res[3u * t + 0u], fog = res[3u * t + 1u], dn = res[3u * t + 2u];
+        uint32_t px, py, a;
+        sample_pixel(m, t, aa, W, H, &px, &py, &a);
         f3 p, dir;
         get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
         f3 pdn = rtm::normalize(dir);
         // tracescreen.hlsl:22-35 (hit branch)
-        float skyAmount = rec.pd.w * 0.0005f;
+        float skyAmount = pdw.w * 0.0005f;
         skyAmount = rtm::sat(skyAmount * skyAmount);
-        f4 pd = {rec.pd.x, rec.pd.y, rec.pd.z, rec.density};
+        f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
         f3 n = get_normal<L>(c, pd);
-        f3 hp = rtm::mk(rec.pd.x, rec.pd.y, rec.pd.z);
-        ShadePre sp = shade_pre<L>(c, hp, n, pdn, rec.pd.w);
+        f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
+        ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
         RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
         ssteps += sr.steps;
         f3 col = shade_post(c, sp, sr.density, sr.fc.w);
-        col = rtm::mk(rtm::lerp(col.x, rec.fog.x, rec.fog.w), rtm::lerp(col.y, rec.fog.y, rec.fog.w),
-                      rtm::lerp(col.z, rec.fog.z, rec.fog.w));
+        col = rtm::mk(rtm::lerp(col.x, fog.x, fog.w), rtm::lerp(col.y, fog.y, fog.w), rtm::lerp(col.z, fog.z, fog.w));
         SkyColor scat = get_rayleigh_mie(c, pdn);
         col = rtm::mk(rtm::lerp(col.x, scat.rayleigh.x, skyAmount), rtm::lerp(col.y, scat.rayleigh.y, skyAmount),
                       rtm::lerp(col.z, scat.rayleigh.z, skyAmount));
-        samples[s] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+        samples[t] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
     }
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
@@ -400,28 +584,63 @@ __global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, 
     }
 }
 
-// tracescreen.hlsl:67-75: color = sum of saturated samples in AA order, / AA, UNORM8 store
-__global__ void __launch_bounds__(64) k_resolve(const RtConsts* __restrict__ k, UnitMap m,
-                                                const float4* __restrict__ samples, uint32_t* __restrict__ out8,
-                                                float4* __restrict__ out32)
+// tracescreen.hlsl:22-27,36-38 (miss branch) for the misses, then :67-75: the sum of
+// saturated samples in AA order, / AA, UNORM8 store.  Persistent over 8x8 units,
+// strided statically (wave w takes units w, w + n_waves, ...): the per-unit work is
+// so short that a shared queue atomic would serialise the whole pass.
+template <bool STATS>
+__global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                 const float4* __restrict__ grad, UnitMap m,
+                                                 const float4* __restrict__ res, const float4* __restrict__ samples,
+                                                 uint32_t* __restrict__ out8, float4* __restrict__ out32,
+                                                 uint32_t* __restrict__ counters, RtStats* stats)
 {
-    uint32_t px, py;
-    if (!unit_pixel(m, blockIdx.x, threadIdx.x, (uint32_t)k->width, (uint32_t)k->height, &px, &py)) return;
-    const uint32_t aa = (uint32_t)k->aa_samples;
-    size_t o = (size_t)py * (size_t)k->width + px;
-    float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
-    for (uint32_t a = 0; a < aa; ++a) {
-        float4 v = samples[o * aa + a];
-        c0 = c0 + v.x;
-        c1 = c1 + v.y;
-        c2 = c2 + v.z;
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < m.n_units; u += n_waves) {
+        uint32_t px, py;
+        if (!unit_pixel(m, u, lane, W, H, &px, &py)) continue;
+        float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
+        for (uint32_t a = 0; a < aa; ++a) {
+            uint32_t t = (u * 64u + lane) * aa + a;
+            float4 dn = res[3u * t + 2u];
+            float4 v;
+            if (dn.x > 0.0f) {
+                v = samples[t];
+            } else {
+                float4 pdw = res[3u * t + 0u], fog = res[3u * t + 1u];
+                f3 p, dir;
+                get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
+                f3 pdn = rtm::normalize(dir);
+                float skyAmount = pdw.w * 0.0005f;
+                skyAmount = rtm::sat(skyAmount * skyAmount);
+                SkyColor scat = get_rayleigh_mie(c, pdn);
+                float space = get_space_color(c, pdn);
+                f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
+                                 (scat.mie.z + scat.rayleigh.z) + space);
+                f3 col = rtm::mk(rtm::lerp(sky.x, fog.x, fog.w), rtm::lerp(sky.y, fog.y, fog.w),
+                                 rtm::lerp(sky.z, fog.z, fog.w));
+                col = rtm::mk(rtm::lerp(col.x, sky.x, skyAmount), rtm::lerp(col.y, sky.y, skyAmount),
+                              rtm::lerp(col.z, sky.z, skyAmount));
+                v = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+            }
+            c0 = c0 + v.x;
+            c1 = c1 + v.y;
+            c2 = c2 + v.z;
+        }
+        float ia = rtm::rcp((float)aa);
+        c0 = c0 * ia;
+        c1 = c1 * ia;
+        c2 = c2 * ia;
+        size_t o = (size_t)py * (size_t)k->width + px;
+        out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
+        if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
     }
-    float ia = rtm::rcp((float)aa);
-    c0 = c0 * ia;
-    c1 = c1 * ia;
-    c2 = c2 * ia;
-    out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
-    if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
+    if constexpr (STATS) atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
 }
 
 // Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
@@ -444,6 +663,16 @@ __global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, u
 template <int L>
 void launch_camerarays_l(const RtLaunch& a, float4* out)
 {
+    if constexpr (L == RT_NOMADPLAINS) {
+        dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 8), block(256);
+        if (a.stats)
+            hipLaunchKernelGGL((k_camerarays_group<true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out,
+                               a.stats);
+        else
+            hipLaunchKernelGGL((k_camerarays_group<false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out,
+                               a.stats);
+        return;
+    }
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64), block(64);
     if (a.stats)
         hipLaunchKernelGGL((k_camerarays<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats);
@@ -490,19 +719,32 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
     uint32_t need = (m.n_units + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
+    dim3 blk(1024);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
+    const bool refill = a.pipeline == RT_PIPELINE_REFILL;
     if (a.stats) {
-        hipLaunchKernelGGL((k_primary<L, true>), dim3(pblocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
-                           cells, m, a.samples, a.hits, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade<L, true>), dim3(blocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
-                           a.samples, a.hits, a.queue, a.stats);
+        if (refill)
+            hipLaunchKernelGGL((k_march<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
+                               a.res, a.hitlist, a.queue, a.stats);
+        else
+            hipLaunchKernelGGL((k_primary<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
+                               m, a.res, a.hitlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+                           a.hitlist, a.samples, a.queue, a.stats);
+        hipLaunchKernelGGL((k_finish<true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+                           a.samples, out8, out32, a.queue, a.stats);
     } else {
-        hipLaunchKernelGGL((k_primary<L, false>), dim3(pblocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
-                           cells, m, a.samples, a.hits, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade<L, false>), dim3(blocks), dim3(1024), 0, a.stream, a.consts, a.perm2d, a.grad,
-                           a.samples, a.hits, a.queue, a.stats);
+        if (refill)
+            hipLaunchKernelGGL((k_march<L, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
+                               m, a.res, a.hitlist, a.queue, a.stats);
+        else
+            hipLaunchKernelGGL((k_primary<L, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
+                               cells, m, a.res, a.hitlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+                           a.hitlist, a.samples, a.queue, a.stats);
+        hipLaunchKernelGGL((k_finish<false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+                           a.samples, out8, out32, a.queue, a.stats);
     }
-    hipLaunchKernelGGL(k_resolve, dim3(m.n_units), dim3(64), 0, a.stream, a.consts, m, a.samples, out8, out32);
 }
 
 } // namespace

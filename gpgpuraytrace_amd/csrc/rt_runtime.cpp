@@ -106,9 +106,10 @@ struct rt_device_s {
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
-    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" selects the single-kernel path
+    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" = single kernel, "refill" = lane-refill primary
     float4* samples = nullptr;     // split pipeline buffers, sized for samples_cap samples
-    RtHit* hits = nullptr;
+    float4* res = nullptr;
+    uint32_t* hitlist = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
     bool profiling = false;
@@ -390,7 +391,8 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.num_cus = dev->num_cus;
     a.pipeline = dev->pipeline;
     a.samples = dev->samples;
-    a.hits = dev->hits;
+    a.res = dev->res;
+    a.hitlist = dev->hitlist;
     return a;
 }
 
@@ -403,19 +405,23 @@ int check_texture(Shader* s)
     return RT_OK;
 }
 
-// Split-pipeline buffers (one sample colour and one potential hit record per AA sample).
+// Split-pipeline buffers: per AA sample of every whole 32x32 tile, one shaded
+// colour (16 B), one primary RayResult (48 B) and one hit-list slot (4 B).
 int ensure_split_buffers(rt_device dev, int aa)
 {
-    size_t need = (size_t)dev->width * dev->height * (size_t)aa;
+    size_t need = rt_split_samples(dev->width, dev->height, aa);
     if (need <= dev->samples_cap) return RT_OK;
     HIP_TRY(hipStreamSynchronize(dev->stream));
     if (dev->samples) HIP_TRY(hipFree(dev->samples));
-    if (dev->hits) HIP_TRY(hipFree(dev->hits));
+    if (dev->res) HIP_TRY(hipFree(dev->res));
+    if (dev->hitlist) HIP_TRY(hipFree(dev->hitlist));
     dev->samples = nullptr;
-    dev->hits = nullptr;
+    dev->res = nullptr;
+    dev->hitlist = nullptr;
     dev->samples_cap = 0;
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->hits, need * sizeof(RtHit)));
+    HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
     dev->samples_cap = need;
     return RT_OK;
 }
@@ -468,7 +474,10 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
     HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
-    if (const char* p = getenv("RT_PIPELINE")) d->pipeline = strcmp(p, "mega") == 0 ? RT_PIPELINE_MEGA : RT_PIPELINE_SPLIT;
+    if (const char* p = getenv("RT_PIPELINE"))
+        d->pipeline = strcmp(p, "mega") == 0 ? RT_PIPELINE_MEGA
+                      : strcmp(p, "refill") == 0 ? RT_PIPELINE_REFILL
+                                                 : RT_PIPELINE_SPLIT;
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
     return RT_OK;
@@ -491,7 +500,8 @@ void rt_device_destroy(rt_device d)
     if (d->scratch_cam) (void)hipFree(d->scratch_cam);
     if (d->queue) (void)hipFree(d->queue);
     if (d->samples) (void)hipFree(d->samples);
-    if (d->hits) (void)hipFree(d->hits);
+    if (d->res) (void)hipFree(d->res);
+    if (d->hitlist) (void)hipFree(d->hitlist);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);

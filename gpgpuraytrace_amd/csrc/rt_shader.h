@@ -19,30 +19,52 @@ using rtm::fma;
 // ---------------------------------------------------------------------------
 // Noise lattice view (both tables live in LDS for the kernel's lifetime).
 //   perm2d: texPerm2D texels (R8G8B8A8_UINT), texel (x,y) at x + y*128 (64 KiB).
-//   grad:   CBNoise.permGradients as float4, stored lane-private: entry i for
-//           lane slot s (= lane & 15) at grad[i*16 + s] (32 KiB).  A ds_read_b128
-//           wave instruction serves 16-lane groups; giving each lane of a group its
-//           own 16-byte bank slot makes every gradient fetch conflict-free however
-//           random the 8 corner indices are.
+//   gxy/gz: CBNoise.permGradients re-laid as PAIRS.  The z+1 corners of noise3d
+//           (noise.hlsl:166-168, Pu + ONE_PIXEL) index gradient (i+1)&127 where the
+//           z corners index i, so entry i holds gradients i and i+1 side by side:
+//             gxy[i] = (g[i].x, g[i+1].x, g[i].y, g[i+1].y)   16 B
+//             gz[i]  = (g[i].z, g[i+1].z)                      8 B
+//           One pair of loads yields both z-layers of a lattice column in register
+//           pairs that v_pk_fma_f32 consumes as they land (no shuffles), and only
+//           the four z-layer indices need extracting.  Entries are lane-private:
+//           entry i for lane slot s at gxy[i*16 + (s&15)], gz[i*32 + (s&31)], so a
+//           ds_read_b128 (16 lanes per pass) or ds_read_b64 (32 lanes per pass) is
+//           conflict-free however random the indices.  Both are i*256 bytes + slot.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
 struct NoiseView {
     const uint32_t* perm2d;
-    const float4* grad;
-    uint32_t slot;
+    const float4* gxy;
+    const float2* gz;
+    uint32_t slot;  // lane & 63
     mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
 };
 
+__device__ __forceinline__ v2f v2(float a, float b)
+{
+    v2f r = {a, b};
+    return r;
+}
+__device__ __forceinline__ v2f vfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+
+// fade (noise.hlsl:133-136): t*t*t*(t*(t*6-15)+10)
 __device__ __forceinline__ float fade(float t)
 {
     return ((t * t) * t) * fma(t, fma(t, 6.0f, -15.0f), 10.0f);
 }
-
-// gradperm (noise.hlsl:145-150): dot(permGradients[i % 128].xyz, p), HLSL dot (R4).
-// The LDS copy stores w = -0.0, and fma(gx, x, -0.0) == gx*x bit for bit (x + -0 == x
-// for every non-NaN x, signed zeros included), so consuming w costs nothing and keeps
-// the fetch a full ds_read_b128 (4 LDS cycles) instead of the b96 form (8 cycles).
-__device__ __forceinline__ float gdot(const float4& g, float x, float y, float z)
+__device__ __forceinline__ v2f fade2(v2f t)
 {
-    return fma(g.z, z, fma(g.y, y, fma(g.x, x, g.w)));
+    return ((t * t) * t) * vfma(t, vfma(t, v2(6.0f, 6.0f), v2(-15.0f, -15.0f)), v2(10.0f, 10.0f));
+}
+
+// gradperm (noise.hlsl:145-150) for the z and z+1 corners of one lattice column:
+// dot(permGradients[i % 128].xyz, p) as the HLSL dot of rule R4,
+// fma(g.z, p.z, fma(g.y, p.y, g.x * p.x)), evaluated element-wise on the pair.
+__device__ __forceinline__ v2f gdot2(const float4& gxy, const float2& gz, float x, float y, v2f zz)
+{
+    v2f r = v2(gxy.x, gxy.y) * v2(x, x);
+    r = vfma(v2(gxy.z, gxy.w), v2(y, y), r);
+    return vfma(v2(gz.x, gz.y), zz, r);
 }
 
 // noise.hlsl:153-179 (live `#if 1` block)
@@ -51,36 +73,33 @@ __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py
     nz.calls += 1;
     float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
     int32_t Px = (int32_t)fx, Py = (int32_t)fy, Pz = (int32_t)fz;
-    float x = px - fx, y = py - fy, z = pz - fz;
-    float ux = fade(x), uy = fade(y), uz = fade(z);
+    v2f xy = v2(px, py) - v2(fx, fy);
+    float z = pz - fz;
+    v2f uxy = fade2(xy);
+    float uz = fade(z);
     // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
     uint32_t X = (uint32_t)Px & 127u, Y = (uint32_t)Py & 127u, Z = (uint32_t)Pz & 127u;
     uint32_t t = nz.perm2d[X + (Y << 7)];
-    // Pu = texel + Pu.z per channel (bytes <= 127+127+1: no carry), % 128
-    uint32_t zz = Z * 0x01010101u;
-    uint32_t w0 = (t + zz) & 0x7f7f7f7fu;               // Pu.x, Pu.y, Pu.z, Pu.w
-    uint32_t w1 = (t + zz + 0x01010101u) & 0x7f7f7f7fu; // Pu.* + ONE_PIXEL
-    const float4* gb = nz.grad + nz.slot;
-    const float4 ga0 = gb[(w0 & 0xffu) << 4];
-    const float4 ga1 = gb[((w0 >> 8) & 0xffu) << 4];
-    const float4 gb0 = gb[((w0 >> 16) & 0xffu) << 4];
-    const float4 gb1 = gb[(w0 >> 24) << 4];
-    const float4 ha0 = gb[(w1 & 0xffu) << 4];
-    const float4 ha1 = gb[((w1 >> 8) & 0xffu) << 4];
-    const float4 hb0 = gb[((w1 >> 16) & 0xffu) << 4];
-    const float4 hb1 = gb[(w1 >> 24) << 4];
-    float x1 = x + -1.0f, y1 = y + -1.0f, z1 = z + -1.0f;
-    float g000 = gdot(ga0, x, y, z);
-    float g100 = gdot(gb0, x1, y, z);
-    float g010 = gdot(ga1, x, y1, z);
-    float g110 = gdot(gb1, x1, y1, z);
-    float g001 = gdot(ha0, x, y, z1);
-    float g101 = gdot(hb0, x1, y, z1);
-    float g011 = gdot(ha1, x, y1, z1);
-    float g111 = gdot(hb1, x1, y1, z1);
-    float l0 = rtm::lerp(rtm::lerp(g000, g100, ux), rtm::lerp(g010, g110, ux), uy);
-    float l1 = rtm::lerp(rtm::lerp(g001, g101, ux), rtm::lerp(g011, g111, ux), uy);
-    return rtm::lerp(l0, l1, uz);
+    // Pu = texel + Pu.z per channel (bytes <= 127+127: no carry), % 128
+    uint32_t w = (t + Z * 0x01010101u) & 0x7f7f7f7fu; // AA, AB, BA, BB column indices at z
+    const float4* gp = nz.gxy + (nz.slot & 15u);
+    const float2* zp = nz.gz + (nz.slot & 31u);
+    const uint32_t i0 = w & 0xffu, i1 = (w >> 8) & 0xffu, i2 = (w >> 16) & 0xffu, i3 = w >> 24;
+    const float4 a0 = gp[i0 << 4], a1 = gp[i1 << 4], b0 = gp[i2 << 4], b1 = gp[i3 << 4];
+    const float2 za0 = zp[i0 << 5], za1 = zp[i1 << 5], zb0 = zp[i2 << 5], zb1 = zp[i3 << 5];
+    const float x = xy.x, y = xy.y;
+    const float x1 = x + -1.0f, y1 = y + -1.0f;
+    const v2f zz = v2(z, z + -1.0f);
+    v2f g00 = gdot2(a0, za0, x, y, zz);   // (g000, g001)
+    v2f g10 = gdot2(b0, zb0, x1, y, zz);  // (g100, g101)
+    v2f g01 = gdot2(a1, za1, x, y1, zz);  // (g010, g011)
+    v2f g11 = gdot2(b1, zb1, x1, y1, zz); // (g110, g111)
+    // lerp(a, b, t) = fma(t, b - a, a) element-wise: x, then y, then z
+    v2f ux = v2(uxy.x, uxy.x), uy = v2(uxy.y, uxy.y);
+    v2f lx0 = vfma(ux, g10 - g00, g00);
+    v2f lx1 = vfma(ux, g11 - g01, g01);
+    v2f l = vfma(uy, lx1 - lx0, lx0); // (l0, l1)
+    return fma(uz, l.y - l.x, l.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -111,6 +130,60 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     }
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((noise3d(c.nz, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f) - 0.2f) * 6.0f) * 7.5f;
+    float floorsize = steep * 1.8f;
+    float t;
+    t = rtm::sat((p1.y - 13.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((p1.y - 16.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((p1.y - 19.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((p1.y - 22.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    s = fma(rtm::pow_nonneg(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
+    return d + s;
+}
+
+// density_nomadplains with the FBM spread over a 32-lane group that marches ONE ray
+// (latency-bound passes: the camerarays prepass has 1024 rays for 256 CUs).  Lane
+// j < 17 evaluates octave N = j+1, lane 17 the steep noise; the octave sum is then
+// gathered in N order with the same fma chain, so the value is bit-identical to
+// density_nomadplains.  `base` = first lane of the group within the wave.  Every
+// lane of the group must be active (the gathers read all of them).
+__device__ __forceinline__ float density_nomadplains_group(const Ctx& c, f3 p, uint32_t j, uint32_t base,
+                                                           uint32_t* octaves)
+{
+    float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
+    float d = -p.y;
+    f3 p1 = rtm::scale(p, 0.4f);
+    float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
+    f3 q0 = rtm::scale(p1, 0.006f);
+    float nx, ny, nzz;
+    if (j < (uint32_t)RT_NP_OCTAVES) {
+        float S = c.k->np_scale[j + 1];
+        nx = q0.x * S;
+        ny = q0.y * c.k->np_scale_y[j + 1];
+        nzz = q0.z * S;
+    } else {
+        nx = p1.x * 0.007138f;
+        ny = p1.z * 0.007138f;
+        nzz = 0.0f;
+    }
+    const float n = noise3d(c.nz, nx, ny, nzz);
+    float on[RT_NP_OCTAVES + 1];
+#pragma unroll
+    for (int N = 1; N <= RT_NP_OCTAVES + 1; ++N) on[N - 1] = __shfl(n, (int)(base + N - 1), 64);
+    float s = 0.0f;
+    uint32_t used = 0;
+#pragma unroll
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
+        const bool live = (float)N <= detail; // N = 1 .. floor(detail), in order
+        s = live ? fma(on[N - 1], c.k->np_rcp[N], s) : s;
+        used += live ? 1u : 0u;
+    }
+    *octaves = used;
+    s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
+    float steep = rtm::sat((on[RT_NP_OCTAVES] - 0.2f) * 6.0f) * 7.5f;
     float floorsize = steep * 1.8f;
     float t;
     t = rtm::sat((p1.y - 13.0f) * steep);
@@ -161,7 +234,7 @@ __device__ __forceinline__ float density_greenrocks(const Ctx& c, f3 p)
     float nohy = fma(rtm::abs(g), 1.4f, 0.1f);
     f3 pc = rtm::mk(p.x * 0.011f, p.y * 0.0013f, p.z * 0.011f);
     float g32 = g * 0.32f;
-#pragma unroll
+#pragma unroll 1
     for (int N = 1; N <= 7; ++N) {
         float S = (float)(1 << N); // pow(2, N) is exact under R5
         float n = noise3d(c.nz, fma(pc.x, S, g32), fma(pc.y, S, g32), fma(pc.z, S, g32));
@@ -170,7 +243,7 @@ __device__ __forceinline__ float density_greenrocks(const Ctx& c, f3 p)
     d = d - 50.0f;
     f3 p2 = rtm::scale(p, 0.002f);
     f3 p2n = rtm::mk(p2.x * 1.0f, p2.y * nohy, p2.z * 1.0f);
-#pragma unroll
+#pragma unroll 1
     for (int N = 1; N <= 5; ++N) {
         float S = (float)(1 << N);
         float n = noise3d(c.nz, p2n.x * S, p2n.y * S, p2n.z * S);
@@ -232,77 +305,118 @@ struct RayResult {
     float steps;
 };
 
-// Media/common/shaders/tracing.hlsl:47-105 (+ build extension max_steps)
+// Media/common/shaders/tracing.hlsl:47-105 (+ build extension max_steps) as an
+// explicit state machine: march_begin = the prologue (:49-66), march_live = the
+// loop condition (:68, the max_steps cap and SKIPREFINE's break on a hit),
+// march_step = one loop body (:70-103).  trace_ray runs it to completion; the
+// lane-refill kernels advance each lane's ray one step at a time and hand a lane
+// a new ray as soon as its old one leaves the loop.
+template <int L, bool CALCFOG>
+struct March {
+    static constexpr bool FOG = CALCFOG && FogLive<L>::value;
+    f3 p, dir, rayp;
+    float dist, step, lastStep, d;
+    f4 f;
+    int iters;
+};
+
+template <int L, bool CALCFOG>
+__device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, f3 p, float dist, float stepmod, f3 dir)
+{
+    const RtConsts* k = c.k;
+    m.f = {0.0f, 0.0f, 0.0f, 0.0f};
+    m.d = 0.0f;
+    float dirLength = rtm::length(dir);
+    m.step = fma(-dist, k->one_minus_step_factor, (0.03f * stepmod) * dirLength);
+    m.lastStep = m.step;
+    float il = rtm::rcp(dirLength);
+    dir = rtm::scale(dir, il);
+    if constexpr (March<L, CALCFOG>::FOG) {
+        float hd = dist * 0.5f;
+        f3 mp = rtm::mk(fma(dir.x * dist, 0.5f, p.x), fma(dir.y * dist, 0.5f, p.y), fma(dir.z * dist, 0.5f, p.z));
+        f4 mf = get_fog<L>(c, mp, hd);
+        m.f.x = fma(mf.x, dist, m.f.x);
+        m.f.y = fma(mf.y, dist, m.f.y);
+        m.f.z = fma(mf.z, dist, m.f.z);
+        m.f.w = fma(mf.w, dist, m.f.w);
+    }
+    m.p = p;
+    m.dir = dir;
+    m.dist = dist;
+    m.rayp = rtm::mk(0.0f, 0.0f, 0.0f);
+    m.iters = 0;
+}
+
+template <int L, bool CALCFOG, bool SKIPREFINE>
+__device__ __forceinline__ bool march_live(const Ctx& c, const March<L, CALCFOG>& m, float enddist, int max_steps)
+{
+    if (SKIPREFINE && m.d > 0.0f) return false; // tracing.hlsl:84 `break` on a hit
+    return m.dist < enddist && m.step > c.k->min_limit && !(max_steps > 0 && m.iters >= max_steps);
+}
+
+template <int L, bool CALCFOG, bool SKIPREFINE, class Density>
+__device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>& m, Density density)
+{
+    const RtConsts* k = c.k;
+    ++m.iters;
+    m.rayp = rtm::mk(fma(m.dir.x, m.dist, m.p.x), fma(m.dir.y, m.dist, m.p.y), fma(m.dir.z, m.dist, m.p.z));
+    m.d = density(m.rayp);
+    f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (March<L, CALCFOG>::FOG) {
+        f4 g = get_fog<L>(c, m.rayp, m.dist);
+        fs.x = g.x * m.step;
+        fs.y = g.y * m.step;
+        fs.z = g.z * m.step;
+        fs.w = g.w * m.step;
+    }
+    if (m.d > 0.0f) {
+        if constexpr (SKIPREFINE) return;
+        m.dist = m.dist - m.lastStep;
+        m.step = m.step * 0.3f;
+        m.f.x = m.f.x - fs.x;
+        m.f.y = m.f.y - fs.y;
+        m.f.z = m.f.z - fs.z;
+        m.f.w = m.f.w - fs.w;
+    } else {
+        float stepmult = 1.0f + rtm::pow_nonneg(rtm::abs(rtm::min(m.d + 5.0f, 0.0f)), k->density_factor);
+        m.step = m.step * k->step_factor;
+        m.lastStep = m.step * stepmult;
+        m.dist = m.dist + m.lastStep;
+        m.f.x = m.f.x + fs.x;
+        m.f.y = m.f.y + fs.y;
+        m.f.z = m.f.z + fs.z;
+        m.f.w = m.f.w + fs.w;
+    }
+}
+
+template <int L, bool CALCFOG, bool SKIPREFINE>
+__device__ __forceinline__ void march_step(const Ctx& c, March<L, CALCFOG>& m)
+{
+    march_step_with<L, CALCFOG, SKIPREFINE>(c, m, [&](f3 q) { return get_density<L>(c, q); });
+}
+
+template <int L, bool CALCFOG>
+__device__ __forceinline__ RayResult march_result(const March<L, CALCFOG>& m)
+{
+    RayResult rr;
+    rr.pd.x = m.rayp.x;
+    rr.pd.y = m.rayp.y;
+    rr.pd.z = m.rayp.z;
+    rr.pd.w = m.dist;
+    rr.fc = m.f;
+    rr.density = m.d;
+    rr.steps = (float)m.iters; // `total` (:71) counts loop iterations
+    return rr;
+}
+
 template <int L, bool CALCFOG, bool SKIPREFINE>
 __device__ __forceinline__ RayResult trace_ray(const Ctx& c, f3 p, float dist, float enddist, float stepmod, f3 dir,
                                                int max_steps)
 {
-    constexpr bool FOG = CALCFOG && FogLive<L>::value;
-    const RtConsts* k = c.k;
-    RayResult rr;
-    f4 f = {0.0f, 0.0f, 0.0f, 0.0f};
-    float d = 0.0f;
-    float total = 0.0f;
-    float dirLength = rtm::length(dir);
-    float step = fma(-dist, k->one_minus_step_factor, (0.03f * stepmod) * dirLength);
-    float lastStep = step;
-    float il = rtm::rcp(dirLength);
-    dir = rtm::scale(dir, il);
-    if constexpr (FOG) {
-        float hd = dist * 0.5f;
-        f3 mp = rtm::mk(fma(dir.x * dist, 0.5f, p.x), fma(dir.y * dist, 0.5f, p.y), fma(dir.z * dist, 0.5f, p.z));
-        f4 mf = get_fog<L>(c, mp, hd);
-        f.x = fma(mf.x, dist, f.x);
-        f.y = fma(mf.y, dist, f.y);
-        f.z = fma(mf.z, dist, f.z);
-        f.w = fma(mf.w, dist, f.w);
-    }
-    f3 rayp = rtm::mk(0.0f, 0.0f, 0.0f);
-    int iters = 0;
-    const float minl = k->min_limit;
-    const float sf = k->step_factor;
-    const float df = k->density_factor;
-    while (dist < enddist && step > minl) {
-        if (max_steps > 0 && iters >= max_steps) break;
-        ++iters;
-        total = total + 1.0f;
-        rayp = rtm::mk(fma(dir.x, dist, p.x), fma(dir.y, dist, p.y), fma(dir.z, dist, p.z));
-        d = get_density<L>(c, rayp);
-        f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
-        if constexpr (FOG) {
-            f4 g = get_fog<L>(c, rayp, dist);
-            fs.x = g.x * step;
-            fs.y = g.y * step;
-            fs.z = g.z * step;
-            fs.w = g.w * step;
-        }
-        if (d > 0.0f) {
-            if constexpr (SKIPREFINE) break;
-            dist = dist - lastStep;
-            step = step * 0.3f;
-            f.x = f.x - fs.x;
-            f.y = f.y - fs.y;
-            f.z = f.z - fs.z;
-            f.w = f.w - fs.w;
-        } else {
-            float stepmult = 1.0f + rtm::pow_nonneg(rtm::abs(rtm::min(d + 5.0f, 0.0f)), df);
-            step = step * sf;
-            lastStep = step * stepmult;
-            dist = dist + lastStep;
-            f.x = f.x + fs.x;
-            f.y = f.y + fs.y;
-            f.z = f.z + fs.z;
-            f.w = f.w + fs.w;
-        }
-    }
-    rr.pd.x = rayp.x;
-    rr.pd.y = rayp.y;
-    rr.pd.z = rayp.z;
-    rr.pd.w = dist;
-    rr.fc = f;
-    rr.density = d;
-    rr.steps = total;
-    return rr;
+    March<L, CALCFOG> m;
+    march_begin(c, m, p, dist, stepmod, dir);
+    while (march_live<L, CALCFOG, SKIPREFINE>(c, m, enddist, max_steps)) march_step<L, CALCFOG, SKIPREFINE>(c, m);
+    return march_result(m);
 }
 
 // tracing.hlsl:107-116

@@ -21,7 +21,7 @@ def load(paths):
 
 
 def short(k):
-    for tag in ("k_tracescreen", "k_camerarays", "k_cell_depths", "k_shard_copy"):
+    for tag in ("k_tracescreen", "k_camerarays", "k_cell_depths", "k_shard_copy", "k_march", "k_shade", "k_finish", "k_primary"):
         if tag in k:
             return tag + ("<stats>" if "true" in k else "")
     return k[:40]
