@@ -27,6 +27,10 @@ METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
 PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, = FP32 MFMA dense)
 PEAK_HBM_GBS = 8000.0
+# what one tracescreen launch (the HIP-event-timed region) runs, per RT_PIPELINE
+TRACESCREEN_KERNELS = {"split": "tracescreen = k_primary + k_shade + k_finish",
+                       "refill": "tracescreen = k_march + k_shade + k_finish",
+                       "mega": "tracescreen = k_tracescreen"}
 
 
 def parse():
@@ -42,7 +46,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                     help="PMC-derived HBM bytes per tracescreen launch (from rocprofv3 --pmc), if present")
     return ap.parse_args()
 
@@ -204,7 +208,8 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_VECTOR_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_VECTOR_TFLOPS, 4), "traffic": traffic,
-                "kernel": "k_tracescreen", "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn.value,
+                "kernel": TRACESCREEN_KERNELS.get(os.environ.get("RT_PIPELINE", "split"), TRACESCREEN_KERNELS["split"]),
+                "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn.value,
                 "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per launch",
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "
                         "= FP32 dense matrix peak = 157.3 TFLOP/s",

@@ -1,0 +1,82 @@
+"""Summarise a scripts/profile_round.sh run into profiles/<round>/:
+kernel_stats.csv (rocprofv3 --stats, verbatim), kernels.md (per-kernel table),
+pmc.md (per-kernel counter means over the non-instrumented dispatches) and
+traffic.json (HBM bytes per tracescreen launch for bench.py's roofline.traffic).
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) doubled for gfx950's
+half-counted wide streaming reads, WRITE_SIZE (KiB) as reported; TCC_EA0_* request
+counts are kept alongside as the raw cross-check."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+TRACESCREEN = ("k_primary", "k_shade", "k_finish", "k_march")
+
+
+def short(name):
+    n = name.replace("void ", "").replace("(anonymous namespace)::", "")
+    return n.split("(")[0]
+
+
+def pmc_means(d):
+    per = defaultdict(lambda: defaultdict(float))
+    for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(p)):
+            per[(r["Kernel_Name"], r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    agg = defaultdict(lambda: defaultdict(list))
+    for (k, _), cs in per.items():
+        for c, v in cs.items():
+            agg[short(k)][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    ks = glob.glob(os.path.join(src, "kt", "**", "*kernel_stats.csv"), recursive=True)
+    rows = list(csv.DictReader(open(ks[0])))
+    shutil.copy(ks[0], os.path.join(dst, "kernel_stats.csv"))
+    bench = open(os.path.join(src, "kt_bench.json")).read().strip().splitlines()[-1]
+    with open(os.path.join(dst, "kernels.md"), "w") as f:
+        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`\n\n")
+        f.write("| kernel | calls | avg ms | total ms |\n|---|---:|---:|---:|\n")
+        for r in rows:
+            f.write(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
+                    f"{float(r['TotalDurationNs']) / 1e6:.3f} |\n")
+        plain = {short(r["Name"]): float(r["AverageNs"]) / 1e6 for r in rows}
+        ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k)
+        f.write(f"\ntracescreen (uninstrumented k_primary + k_shade + k_finish) avg sum: {ts:.4f} ms\n")
+        f.write(f"\nbench line of the same run:\n\n```\n{bench}\n```\n")
+    m = pmc_means(src)
+    with open(os.path.join(dst, "pmc.md"), "w") as f:
+        f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group)\n\n")
+        for k in sorted(m):
+            f.write(f"## {k}\n\n")
+            for c in sorted(m[k]):
+                f.write(f"- {c}: {m[k][c]:.6g}\n")
+            f.write("\n")
+    tr = {}
+    fetch = write = rd = wr = 0.0
+    for k, cs in m.items():
+        if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k:
+            fetch += cs.get("FETCH_SIZE", 0.0)
+            write += cs.get("WRITE_SIZE", 0.0)
+            rd += cs.get("TCC_EA0_RDREQ_sum", 0.0)
+            wr += cs.get("TCC_EA0_WRREQ_sum", 0.0)
+    b = json.loads(bench)
+    key = f"{b['config']['width']}x{b['config']['height']}_{b['config']['landscape']}_{b['config']['pose']}"
+    tr[key] = {"hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
+               "fetch_size_kib": fetch, "write_size_kib": write,
+               "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
+               "kernels": "k_primary + k_shade + k_finish (uninstrumented)",
+               "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"}
+    json.dump(tr, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    print(open(os.path.join(dst, "kernels.md")).read())
+    print(json.dumps(tr, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])

@@ -129,6 +129,19 @@ def test_shard_bytes_match_library():
     assert G.lib().rt_shard_bytes(None, 0, 1) == 0  # null device -> 0, no crash
 
 
+REF_SRC = "/root/reference/gpuraytrace"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_SRC), reason="reference headers not present (GPU box)")
+def test_cpp_adapter_compiles_against_reference_headers():
+    """integration/hip_adapter.cpp implements the reference's IDevice/ICompute/IShaderVariable/
+    IShaderArray/ITexture over include/frosttrace.h; compile it against the reference's own headers."""
+    import subprocess
+    r = subprocess.run(["g++", "-std=c++11", "-fsyntax-only", "-I", REF_SRC, "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "integration", "hip_adapter.cpp")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+
+
 def test_capi_errors_are_reported_not_crashes():
     import gpgpuraytrace_amd as G
     L = G.lib()
