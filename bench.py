@@ -28,8 +28,8 @@ FLOPS_PER_NOISE3D = 88          # algorithmic work unit
 PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, = FP32 MFMA dense)
 PEAK_HBM_GBS = 8000.0
 # what one tracescreen launch (the HIP-event-timed region) runs, per RT_PIPELINE
-TRACESCREEN_KERNELS = {"split": "tracescreen = k_primary + k_shade + k_finish",
-                       "refill": "tracescreen = k_march + k_shade + k_finish",
+TRACESCREEN_KERNELS = {"split": "tracescreen = k_order + k_primary + k_shade_pre + k_shadow + k_finish",
+                       "refill": "tracescreen = k_march + k_shade_pre + k_shadow + k_finish",
                        "mega": "tracescreen = k_tracescreen"}
 
 

@@ -306,7 +306,8 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
 //                the loop, so a wave's lanes stay full until the sample queue
 //                drains.  Writes the RayResult of every sample; hits are appended
 //                to a compacted list (staged per wave in LDS, one atomic per 64).
-//   S k_shade  : normal + colour + shadow march + sky blend over the hit list.
+//   S k_shade_pre + k_shadow: normal, colour, sky and the first shadow step over
+//                the hit list, then the long shadow rays with lane refill.
 //   R k_finish : sky colour of the misses + in-order AA average + UNORM8.
 // Sample t = (u*64 + j)*AA + a: AA sample a of lane-slot j of 8x8 unit u.
 struct UnitMap {
@@ -458,6 +459,60 @@ __global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, 
     }
 }
 
+// Longest-first tile order for k_primary.  A frame's critical path is its few
+// grazing units (hundreds of march steps near the horizon); in screen order they
+// start half-way through the queue and finish long after the rest.  The prepass
+// cells already say where they are: a tile whose cells' depth bracket
+// log2(far/near) is wide starts its rays far in front of the surface they hit (or
+// graze).  One workgroup buckets the shard's 32x32 tiles by that key (64 buckets,
+// descending); the order only decides which wave takes a unit when, never what
+// it computes.
+__global__ void __launch_bounds__(1024) k_order(const RtConsts* __restrict__ k, const float2* __restrict__ cells,
+                                                UnitMap m, uint32_t* __restrict__ order)
+{
+    __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
+    __shared__ uint32_t s_hist[64];
+    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) {
+        float2 cd = cells[i];
+        s_key[i] = __log2f(cd.y / cd.x);
+    }
+    if (threadIdx.x < 64) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
+    const uint32_t n_tiles = m.n_units >> 4;
+    auto bucket = [&](uint32_t tile) -> uint32_t {
+        float key = 0.0f;
+        // corner pixels of the tile: unit 0 lane 0, unit 3 lane 7, unit 12 lane 56, unit 15 lane 63
+        for (uint32_t corner = 0; corner < 4; ++corner) {
+            uint32_t px, py;
+            uint32_t u = tile * 16u + (corner & 1u) * 3u + (corner >> 1) * 12u;
+            uint32_t lane = (corner & 1u) * 7u + (corner >> 1) * 56u;
+            if (!unit_pixel(m, u, lane, W, H, &px, &py)) {
+                if (!unit_pixel(m, tile * 16u, 0u, W, H, &px, &py)) continue;
+                px = px + (corner & 1u) * 31u < W ? px + (corner & 1u) * 31u : W - 1u;
+                py = py + (corner >> 1) * 31u < H ? py + (corner >> 1) * 31u : H - 1u;
+            }
+            float spx = (float)px * k->rcp_w, spy = (float)py * k->rcp_h;
+            uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
+            key = fmaxf(key, s_key[cell]);
+        }
+        int b = (int)(key * 3.3f);
+        return (uint32_t)(b < 0 ? 0 : (b > 63 ? 63 : b));
+    };
+    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) atomicAdd(&s_hist[bucket(t)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int b = 63; b >= 0; --b) {
+            uint32_t c = s_hist[b];
+            s_hist[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) order[atomicAdd(&s_hist[bucket(t)], 1u)] = t;
+}
+
 // Tile-ordered primary march: each wave takes one 8x8 unit at a time (neighbouring
 // pixels march to similar distances, so their FBM octave counts agree and few
 // lanes idle inside noise loops).  The march loop is the wave's own; a wave still
@@ -468,7 +523,8 @@ __global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, 
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                   const float4* __restrict__ grad, const float2* __restrict__ cells,
-                                                  UnitMap m, float4* __restrict__ res, uint32_t* __restrict__ hitlist,
+                                                  UnitMap m, const uint32_t* __restrict__ order,
+                                                  float4* __restrict__ res, uint32_t* __restrict__ hitlist,
                                                   uint32_t* __restrict__ counters, RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
@@ -483,8 +539,9 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
     float psteps = 0.0f;
     uint32_t nhits = 0;
     for (;;) {
-        uint32_t u = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
-        if (u >= m.n_units) break;
+        const uint32_t q = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+        if (q >= m.n_units) break;
+        const uint32_t u = __builtin_amdgcn_readfirstlane(order[q >> 4]) * 16u + (q & 15u);
         uint32_t px, py;
         const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
         const float pxf = (float)px, pyf = (float)py;
@@ -535,16 +592,51 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
     }
 }
 
+// Shading in two passes so the divergent part runs on full waves.
+//   S1 k_shade_pre: per hit, the uniform work -- getNormal (3 densities), getColor up
+//      to the shadow ray (20-octave albedo FBM), the Rayleigh/Mie sky -- and the
+//      FIRST shadow-march step (nomadplains/color.hlsl:51).  About 70% of shadow rays
+//      end there (the surface faces away from the low sun or the first sample is
+//      already inside the terrain); those samples are finished on the spot.  The
+//      rest are appended, with their march state and shading record, to a
+//      compacted long-shadow list.
+//   S2 k_shadow: the long shadow rays (2..~120 steps) with lane refill: each lane
+//      takes the next ray as soon as its own ends; all march toward the same sun
+//      and neighbours in the list come from neighbouring pixels, so FBM octave
+//      counts stay close.  A retiring lane finishes its sample.
+// Long-shadow record j (6 float4): (albedo+specular rgb, brightness), fcolord,
+// (rayleigh rgb, skyAmount), (p, dist), (step, lastStep, d, iters), shadow fog.
+constexpr uint32_t kShadowRec = 6;
+
+// color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
+__device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, float4 fog, float4 ray,
+                                               float shadow_density, float shadow_fog_w)
+{
+    float b = cb.w;
+    if (shadow_density > 0.0f) b = b * 0.1f;
+    else b = rtm::sat(b - shadow_fog_w);
+    f3 col = rtm::mk(cb.x * fma(b, k->one_minus_shadow[0], k->shadow_color[0]),
+                     cb.y * fma(b, k->one_minus_shadow[1], k->shadow_color[1]),
+                     cb.z * fma(b, k->one_minus_shadow[2], k->shadow_color[2]));
+    col = rtm::mk(rtm::lerp(col.x, fog.x, fog.w), rtm::lerp(col.y, fog.y, fog.w), rtm::lerp(col.z, fog.z, fog.w));
+    col = rtm::mk(rtm::lerp(col.x, ray.x, ray.w), rtm::lerp(col.y, ray.y, ray.w), rtm::lerp(col.z, ray.z, ray.w));
+    return make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+}
+
 template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                const float4* __restrict__ grad, UnitMap m,
-                                                const float4* __restrict__ res, const uint32_t* __restrict__ hitlist,
-                                                float4* __restrict__ samples, uint32_t* __restrict__ counters,
-                                                RtStats* stats)
+__global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__ k,
+                                                    const uint32_t* __restrict__ perm2d,
+                                                    const float4* __restrict__ grad, UnitMap m,
+                                                    const float4* __restrict__ res,
+                                                    const uint32_t* __restrict__ hitlist,
+                                                    float4* __restrict__ samples, float4* __restrict__ shrec,
+                                                    uint32_t* __restrict__ longlist, uint32_t* __restrict__ counters,
+                                                    RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
@@ -553,30 +645,137 @@ __global__ void __launch_bounds__(1024) k_shade(const RtConsts* __restrict__ k, 
     for (;;) {
         uint32_t u = wave_fetch(&counters[RT_CTR_SHADE], lane);
         if (u >= n_units) break;
-        uint32_t i = u * 64u + lane;
-        if (i >= n_hits) continue;
-        uint32_t t = hitlist[i];
-        float4 pdw = res[3u * t + 0u], fog = res[3u * t + 1u], dn = res[3u * t + 2u];
-        uint32_t px, py, a;
-        sample_pixel(m, t, aa, W, H, &px, &py, &a);
-        f3 p, dir;
-        get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
-        f3 pdn = rtm::normalize(dir);
-        // tracescreen.hlsl:22-35 (hit branch)
-        float skyAmount = pdw.w * 0.0005f;
-        skyAmount = rtm::sat(skyAmount * skyAmount);
-        f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
-        f3 n = get_normal<L>(c, pd);
-        f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
-        ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
-        RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
-        ssteps += sr.steps;
-        f3 col = shade_post(c, sp, sr.density, sr.fc.w);
-        col = rtm::mk(rtm::lerp(col.x, fog.x, fog.w), rtm::lerp(col.y, fog.y, fog.w), rtm::lerp(col.z, fog.z, fog.w));
-        SkyColor scat = get_rayleigh_mie(c, pdn);
-        col = rtm::mk(rtm::lerp(col.x, scat.rayleigh.x, skyAmount), rtm::lerp(col.y, scat.rayleigh.y, skyAmount),
-                      rtm::lerp(col.z, scat.rayleigh.z, skyAmount));
-        samples[t] = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+        const uint32_t i = u * 64u + lane;
+        bool more = false;
+        uint32_t t = 0;
+        float4 cb, fog, ray;
+        March<L, true> st;
+        if (i < n_hits) {
+            t = hitlist[i];
+            float4 pdw = res[3u * t + 0u], dn = res[3u * t + 2u];
+            fog = res[3u * t + 1u];
+            uint32_t px, py, a;
+            sample_pixel(m, t, aa, W, H, &px, &py, &a);
+            f3 p, dir;
+            get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
+            f3 pdn = rtm::normalize(dir);
+            // tracescreen.hlsl:22-35 (hit branch)
+            float skyAmount = pdw.w * 0.0005f;
+            skyAmount = rtm::sat(skyAmount * skyAmount);
+            f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
+            f3 n = get_normal<L>(c, pd);
+            f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
+            ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
+            // color.hlsl:63-66: the specular term does not depend on the shadow
+            float specular = rtm::sat(rtm::pow_nonneg(rtm::max(sp.spec_dot, 0.0f), 40.0f)) * sp.spec_k;
+            SkyColor scat = get_rayleigh_mie(c, pdn);
+            cb = make_float4(sp.col[0] + specular, sp.col[1] + specular, sp.col[2] + specular, sp.brightness);
+            ray = make_float4(scat.rayleigh.x, scat.rayleigh.y, scat.rayleigh.z, skyAmount);
+            // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): first step
+            march_begin(c, st, hp, 0.4f, sp.precision, c.sun);
+            if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
+            more = march_live<L, true, true>(c, st, 100.0f, 0);
+            if (!more) {
+                samples[t] = shade_finish(k, cb, fog, ray, st.d, st.f.w);
+                if constexpr (STATS) ssteps += (float)st.iters;
+            }
+        }
+        const uint64_t lb = __ballot(more);
+        if (lb) {
+            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
+            if (more) {
+                const uint32_t j = b + (uint32_t)__popcll(lb & lt_mask);
+                longlist[j] = t;
+                float4* r = shrec + (size_t)kShadowRec * j;
+                r[0] = cb;
+                r[1] = fog;
+                r[2] = ray;
+                r[3] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
+                r[4] = make_float4(st.step, st.lastStep, st.d, __int_as_float(st.iters));
+                r[5] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
+            }
+        }
+    }
+    if constexpr (STATS) {
+        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                 const float4* __restrict__ grad,
+                                                 const float4* __restrict__ shrec,
+                                                 const uint32_t* __restrict__ longlist, float4* __restrict__ samples,
+                                                 uint32_t* __restrict__ counters, RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t n_long = __builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]);
+    // tracing.hlsl:60-61: the march direction is dir / length(dir) of SunDirection
+    const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
+    March<L, true> st;
+    st.d = 0.0f;
+    st.iters = 0;
+    bool live = false;
+    uint32_t j = 0;
+    uint32_t pool = 0, pool_left = 0; // wave-uniform
+    bool drained = false;
+    float ssteps = 0.0f;
+    for (;;) {
+        // 1. retire rays that left the loop: finish their samples
+        if (live && !march_live<L, true, true>(c, st, 100.0f, 0)) {
+            const float4* r = shrec + (size_t)kShadowRec * j;
+            samples[longlist[j]] = shade_finish(k, r[0], r[1], r[2], st.d, st.f.w);
+            live = false;
+            if constexpr (STATS) ssteps += (float)st.iters;
+        }
+        // 2. refill idle lanes from the wave's pool of long-list indices
+        if (!drained) {
+            uint64_t idle = __ballot(!live);
+            if ((uint32_t)__popcll(idle) >= kRefillIdle) {
+                while (idle) {
+                    if (pool_left == 0u) {
+                        uint32_t b = wave_fetch(&counters[RT_CTR_SHADOW], lane, 64u);
+                        if (b >= n_long) {
+                            drained = true;
+                            break;
+                        }
+                        pool = b;
+                        pool_left = (n_long - b) < 64u ? (n_long - b) : 64u;
+                    }
+                    const uint32_t take = (uint32_t)__popcll(idle) < pool_left ? (uint32_t)__popcll(idle) : pool_left;
+                    const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                    const bool mine = ((idle >> lane) & 1ull) && rank < take;
+                    if (mine) {
+                        j = pool + rank;
+                        const float4* r = shrec + (size_t)kShadowRec * j;
+                        const float4 pd = r[3], sv = r[4], f = r[5];
+                        st.p = rtm::mk(pd.x, pd.y, pd.z);
+                        st.dist = pd.w;
+                        st.dir = sun_dir;
+                        st.step = sv.x;
+                        st.lastStep = sv.y;
+                        st.d = sv.z;
+                        st.iters = __float_as_int(sv.w);
+                        st.f = {f.x, f.y, f.z, f.w};
+                        live = true; // it was live when k_shade_pre stored it
+                    }
+                    idle &= ~__ballot(mine);
+                    pool += take;
+                    pool_left -= take;
+                }
+            }
+        }
+        // 3. one shadow-march step on every live lane
+        if (__ballot(live) == 0ull) {
+            if (drained) break;
+            continue;
+        }
+        if (live) march_step<L, true, true>(c, st);
     }
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
@@ -722,15 +921,18 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     dim3 blk(1024);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     const bool refill = a.pipeline == RT_PIPELINE_REFILL;
+    if (!refill) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
     if (a.stats) {
         if (refill)
             hipLaunchKernelGGL((k_march<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
                                a.res, a.hitlist, a.queue, a.stats);
         else
             hipLaunchKernelGGL((k_primary<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
-                               m, a.res, a.hitlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.hitlist, a.samples, a.queue, a.stats);
+                               m, a.order, a.res, a.hitlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade_pre<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
+                           a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shadow<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+                           a.longlist, a.samples, a.queue, a.stats);
         hipLaunchKernelGGL((k_finish<true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.samples, out8, out32, a.queue, a.stats);
     } else {
@@ -739,9 +941,11 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
                                m, a.res, a.hitlist, a.queue, a.stats);
         else
             hipLaunchKernelGGL((k_primary<L, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               cells, m, a.res, a.hitlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.hitlist, a.samples, a.queue, a.stats);
+                               cells, m, a.order, a.res, a.hitlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade_pre<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
+                           a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shadow<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+                           a.longlist, a.samples, a.queue, a.stats);
         hipLaunchKernelGGL((k_finish<false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.samples, out8, out32, a.queue, a.stats);
     }

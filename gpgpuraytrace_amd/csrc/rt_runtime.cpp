@@ -110,6 +110,9 @@ struct rt_device_s {
     float4* samples = nullptr;     // split pipeline buffers, sized for samples_cap samples
     float4* res = nullptr;
     uint32_t* hitlist = nullptr;
+    uint32_t* order = nullptr;
+    float4* shrec = nullptr;
+    uint32_t* longlist = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
     bool profiling = false;
@@ -393,6 +396,9 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.samples = dev->samples;
     a.res = dev->res;
     a.hitlist = dev->hitlist;
+    a.order = dev->order;
+    a.shrec = dev->shrec;
+    a.longlist = dev->longlist;
     return a;
 }
 
@@ -415,13 +421,22 @@ int ensure_split_buffers(rt_device dev, int aa)
     if (dev->samples) HIP_TRY(hipFree(dev->samples));
     if (dev->res) HIP_TRY(hipFree(dev->res));
     if (dev->hitlist) HIP_TRY(hipFree(dev->hitlist));
+    if (dev->order) HIP_TRY(hipFree(dev->order));
+    if (dev->shrec) HIP_TRY(hipFree(dev->shrec));
+    if (dev->longlist) HIP_TRY(hipFree(dev->longlist));
+    dev->shrec = nullptr;
+    dev->longlist = nullptr;
     dev->samples = nullptr;
     dev->res = nullptr;
     dev->hitlist = nullptr;
+    dev->order = nullptr;
     dev->samples_cap = 0;
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->shrec, need * 6 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->longlist, need * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * sizeof(uint32_t)));
     dev->samples_cap = need;
     return RT_OK;
 }
@@ -502,6 +517,9 @@ void rt_device_destroy(rt_device d)
     if (d->samples) (void)hipFree(d->samples);
     if (d->res) (void)hipFree(d->res);
     if (d->hitlist) (void)hipFree(d->hitlist);
+    if (d->order) (void)hipFree(d->order);
+    if (d->shrec) (void)hipFree(d->shrec);
+    if (d->longlist) (void)hipFree(d->longlist);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);

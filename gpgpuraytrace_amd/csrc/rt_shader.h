@@ -564,6 +564,7 @@ __device__ __forceinline__ ShadePre shade_pre(const Ctx& c, f3 p, f3 n, f3 d, fl
         } else {
             float detail = rtm::max(16.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
             f3 q = rtm::mk(p.y * 0.5f, p.x * 0.01f, p.z * 0.1f);
+            #pragma unroll 1
             for (int N = 1; N <= RT_COL_OCTAVES; ++N) {
                 if (!((float)N <= detail)) break;
                 float S = c.k->col_scale[N];

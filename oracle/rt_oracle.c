@@ -760,6 +760,12 @@ static f3 trace_sample(ctx* c, const sky_consts* k, f3 pp, f3 pdir, f3 pdn, floa
 /* camerarays.hlsl:12-21 */
 void ro_camerarays(const ro_noise* nz, const ro_frame* fr, float* camera_results, ro_stats* st)
 {
+    ro_camerarays_steps(nz, fr, camera_results, NULL, st);
+}
+
+void ro_camerarays_steps(const ro_noise* nz, const ro_frame* fr, float* camera_results, float* steps_out,
+                         ro_stats* st)
+{
     uint64_t noise = 0, steps = 0, dens = 0;
     int nt = fr->threads > 0 ? fr->threads : 0;
 #pragma omp parallel for schedule(dynamic, 4) reduction(+ : noise, steps, dens) num_threads(nt ? nt : omp_get_max_threads())
@@ -778,6 +784,7 @@ void ro_camerarays(const ro_noise* nz, const ro_frame* fr, float* camera_results
         camera_results[4 * i + 1] = rr.pd.y;
         camera_results[4 * i + 2] = rr.pd.z;
         camera_results[4 * i + 3] = rr.pd.w;
+        if (steps_out) steps_out[i] = rr.steps;
         noise += c.noise_calls;
         dens += c.density_calls;
         steps += (uint64_t)rr.steps;

@@ -85,6 +85,9 @@ void ro_get_density_batch(const ro_noise* nz, const ro_frame* fr, const float* x
 
 /* camerarays.hlsl:12-21 -> CameraResults float4[1024] */
 void ro_camerarays(const ro_noise* nz, const ro_frame* fr, float* camera_results, ro_stats* st);
+/* same, plus the per-cell traceRay iteration count (steps_out may be NULL) */
+void ro_camerarays_steps(const ro_noise* nz, const ro_frame* fr, float* camera_results, float* steps_out,
+                         ro_stats* st);
 /* Terrain.cpp:356-439 -> CellDistance float2[1024] */
 void ro_set_target_depths(const float* camera_results, float* cell_distance);
 /* tracescreen.hlsl:50-76 for rows [row_begin,row_end) step row_step.  Outputs

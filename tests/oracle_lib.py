@@ -67,6 +67,7 @@ def lib():
         L.ro_noise3d_batch.argtypes = [C.POINTER(Noise), fp, fp, C.c_int64]
         L.ro_get_density_batch.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.c_int64]
         L.ro_camerarays.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, C.POINTER(Stats)]
+        L.ro_camerarays_steps.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.POINTER(Stats)]
         L.ro_set_target_depths.argtypes = [fp, fp]
         L.ro_tracescreen.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.POINTER(C.c_uint8), fp,
                                      C.POINTER(Stats)]
