@@ -13,6 +13,8 @@
 // until the slowest wave of its workgroup retires.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "rt_kernels.h"
 #include "rt_shader.h"
 
@@ -55,7 +57,8 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     c.nz.gxy = reinterpret_cast<const float4*>(lds);
     c.nz.gz = reinterpret_cast<const float2*>(lds + kGxyWords);
     c.nz.perm2d = lds + kGradWords;
-    c.nz.slot = threadIdx.x & 63u;
+    c.nz.so16 = (threadIdx.x & 15u) * 16u;
+    c.nz.so32 = (threadIdx.x & 31u) * 8u;
     c.nz.calls = 0;
     c.k = k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
@@ -919,6 +922,12 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     uint32_t need = (m.n_units + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
+    static const int shadow_threads = [] {
+        const char* e = getenv("RT_SHADOW_THREADS");
+        int v = e ? atoi(e) : 1024;
+        return (v == 256 || v == 512 || v == 1024) ? v : 1024;
+    }();
+    dim3 sblk(shadow_threads);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     const bool refill = a.pipeline == RT_PIPELINE_REFILL;
     if (!refill) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
@@ -931,7 +940,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
                                m, a.order, a.res, a.hitlist, a.queue, a.stats);
         hipLaunchKernelGGL((k_shade_pre<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
                            a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+        hipLaunchKernelGGL((k_shadow<L, true>), dim3(blocks), sblk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
                            a.longlist, a.samples, a.queue, a.stats);
         hipLaunchKernelGGL((k_finish<true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.samples, out8, out32, a.queue, a.stats);
@@ -944,7 +953,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
                                cells, m, a.order, a.res, a.hitlist, a.queue, a.stats);
         hipLaunchKernelGGL((k_shade_pre<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
                            a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+        hipLaunchKernelGGL((k_shadow<L, false>), dim3(blocks), sblk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
                            a.longlist, a.samples, a.queue, a.stats);
         hipLaunchKernelGGL((k_finish<false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.samples, out8, out32, a.queue, a.stats);

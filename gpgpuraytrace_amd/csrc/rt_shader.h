@@ -36,7 +36,8 @@ struct NoiseView {
     const uint32_t* perm2d;
     const float4* gxy;
     const float2* gz;
-    uint32_t slot;  // lane & 63
+    uint32_t so16;  // (lane & 15) * 16: this lane's byte slot in a gxy entry row
+    uint32_t so32;  // (lane & 31) * 8:  this lane's byte slot in a gz entry row
     mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
 };
 
@@ -67,10 +68,9 @@ __device__ __forceinline__ v2f gdot2(const float4& gxy, const float2& gz, float 
     return vfma(v2(gz.x, gz.y), zz, r);
 }
 
-// noise.hlsl:153-179 (live `#if 1` block)
-__device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py, float pz)
+// noise.hlsl:153-179 (live `#if 1` block); noise3d_raw does not count the call
+__device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, float py, float pz)
 {
-    nz.calls += 1;
     float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
     int32_t Px = (int32_t)fx, Py = (int32_t)fy, Pz = (int32_t)fz;
     v2f xy = v2(px, py) - v2(fx, fy);
@@ -82,11 +82,18 @@ __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py
     uint32_t t = nz.perm2d[X + (Y << 7)];
     // Pu = texel + Pu.z per channel (bytes <= 127+127: no carry), % 128
     uint32_t w = (t + Z * 0x01010101u) & 0x7f7f7f7fu; // AA, AB, BA, BB column indices at z
-    const float4* gp = nz.gxy + (nz.slot & 15u);
-    const float2* zp = nz.gz + (nz.slot & 31u);
-    const uint32_t i0 = w & 0xffu, i1 = (w >> 8) & 0xffu, i2 = (w >> 16) & 0xffu, i3 = w >> 24;
-    const float4 a0 = gp[i0 << 4], a1 = gp[i1 << 4], b0 = gp[i2 << 4], b1 = gp[i3 << 4];
-    const float2 za0 = zp[i0 << 5], za1 = zp[i1 << 5], zb0 = zp[i2 << 5], zb1 = zp[i3 << 5];
+    // entry i of either plane starts at byte i*256: one v_perm_b32 per corner builds
+    // (index byte << 8) | lane slot ({w, slot} byte pick: 4+k = byte k of w, 0 = slot, 12 = 0)
+    const char* gb = reinterpret_cast<const char*>(nz.gxy);
+    const char* zb = reinterpret_cast<const char*>(nz.gz);
+    auto gxy_at = [&](uint32_t sel) {
+        return *reinterpret_cast<const float4*>(gb + __builtin_amdgcn_perm(w, nz.so16, sel));
+    };
+    auto gz_at = [&](uint32_t sel) {
+        return *reinterpret_cast<const float2*>(zb + __builtin_amdgcn_perm(w, nz.so32, sel));
+    };
+    const float4 a0 = gxy_at(0x0c0c0400u), a1 = gxy_at(0x0c0c0500u), b0 = gxy_at(0x0c0c0600u), b1 = gxy_at(0x0c0c0700u);
+    const float2 za0 = gz_at(0x0c0c0400u), za1 = gz_at(0x0c0c0500u), zb0 = gz_at(0x0c0c0600u), zb1 = gz_at(0x0c0c0700u);
     const float x = xy.x, y = xy.y;
     const float x1 = x + -1.0f, y1 = y + -1.0f;
     const v2f zz = v2(z, z + -1.0f);
@@ -100,6 +107,12 @@ __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py
     v2f lx1 = vfma(ux, g11 - g01, g01);
     v2f l = vfma(uy, lx1 - lx0, lx0); // (l0, l1)
     return fma(uz, l.y - l.x, l.x);
+}
+
+__device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py, float pz)
+{
+    nz.calls += 1;
+    return noise3d_raw(nz, px, py, pz);
 }
 
 // ---------------------------------------------------------------------------
@@ -120,10 +133,12 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     float s = 0.0f;
     float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
-    // N = 1 .. floor(detail); detail <= 17.79 so N <= 17 (RT_NP_OCTAVES)
+    // N = 1 .. floor(detail); detail in [2, 17.79] so N <= 17 (RT_NP_OCTAVES) and
+    // (float)N <= detail <=> N <= (int)detail
+    const int n_oct = (int)detail;
     #pragma unroll 1
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
-        if (!((float)N <= detail)) break;
+        if (N > n_oct) break;
         float S = c.k->np_scale[N];
         float n = noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S);
         s = fma(n, c.k->np_rcp[N], s);
