@@ -9,7 +9,7 @@
 enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2, RT_CTR_FINISH = 3, RT_CTR_SHADOW = 4, RT_CTR_LONG = 5 };
 #define RT_CTR_BYTES 64
 
-enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2 };
+enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2, RT_PIPELINE_STAGED = 3 };
 
 struct RtLaunch {
     hipStream_t stream;
@@ -25,8 +25,8 @@ struct RtLaunch {
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
     float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
     uint32_t* hitlist;        // compacted sample ids of primary hits
-    float4* shrec;            // 6 float4 per long shadow ray: shading record + march state (k_shade_pre -> k_shadow)
-    uint32_t* longlist;       // sample ids of the long shadow rays
+    float4* shrec;            // 4 float4 per long shadow ray on the global list: march state + sample id
+    float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     uint32_t* order;          // k_primary tile order (rt_split_samples/1024 entries)
 };
 

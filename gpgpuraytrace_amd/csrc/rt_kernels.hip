@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "rt_kernels.h"
 #include "rt_shader.h"
@@ -595,21 +596,16 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
     }
 }
 
-// Shading in two passes so the divergent part runs on full waves.
-//   S1 k_shade_pre: per hit, the uniform work -- getNormal (3 densities), getColor up
-//      to the shadow ray (20-octave albedo FBM), the Rayleigh/Mie sky -- and the
-//      FIRST shadow-march step (nomadplains/color.hlsl:51).  About 70% of shadow rays
-//      end there (the surface faces away from the low sun or the first sample is
-//      already inside the terrain); those samples are finished on the spot.  The
-//      rest are appended, with their march state and shading record, to a
-//      compacted long-shadow list.
-//   S2 k_shadow: the long shadow rays (2..~120 steps) with lane refill: each lane
-//      takes the next ray as soon as its own ends; all march toward the same sun
-//      and neighbours in the list come from neighbouring pixels, so FBM octave
-//      counts stay close.  A retiring lane finishes its sample.
-// Long-shadow record j (6 float4): (albedo+specular rgb, brightness), fcolord,
-// (rayleigh rgb, skyAmount), (p, dist), (step, lastStep, d, iters), shadow fog.
-constexpr uint32_t kShadowRec = 6;
+// Shading (tracescreen.hlsl:28-35, nomadplains/color.hlsl:8-72).  Per hit, the
+// uniform work -- getNormal (3 densities), getColor up to the shadow ray (20-octave
+// albedo FBM), the Rayleigh/Mie sky -- and the FIRST shadow-march step
+// (color.hlsl:51).  About 70% of shadow rays end there (the surface faces away from
+// the low sun, or the first sample is already inside the terrain) and those samples
+// are finished on the spot; the rest become long shadow rays (2..~120 steps).
+// A long ray's finishing inputs go to fin[t] (3 float4: albedo+specular rgb and
+// brightness, fcolord, rayleigh rgb and skyAmount) and its march state to a
+// 4-float4 record: (p, dist), (step, lastStep, d, iters), shadow fog, (t, -, -, -).
+constexpr uint32_t kShadowRec = 4;
 
 // color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
 __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, float4 fog, float4 ray,
@@ -626,23 +622,98 @@ __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, flo
     return make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
 }
 
+// Loads of data another wave of this kernel wrote: bypass the CU's L1 (a line cached
+// there earlier would be stale), served by the XCD's L2 the producer wrote through.
+__device__ __forceinline__ float4 ld_fresh(const float4* p)
+{
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
+struct ShadeHit {
+    float4 cb, fog, ray;
+    bool more; // the shadow ray is still marching after its first step
+};
+
+// tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.
+template <int L, bool FRESH>
+__device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, const float4* __restrict__ res,
+                                              uint32_t t, March<L, true>& st)
+{
+    const RtConsts* k = c.k;
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    ShadeHit h;
+    const float4 pdw = FRESH ? ld_fresh(res + 3u * t) : res[3u * t];
+    const float4 dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
+    h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
+    uint32_t px, py, a;
+    sample_pixel(m, t, aa, W, H, &px, &py, &a);
+    f3 p, dir;
+    get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
+    f3 pdn = rtm::normalize(dir);
+    float skyAmount = pdw.w * 0.0005f;
+    skyAmount = rtm::sat(skyAmount * skyAmount);
+    f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
+    f3 n = get_normal<L>(c, pd);
+    f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
+    ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
+    // color.hlsl:63-66: the specular term does not depend on the shadow
+    float specular = rtm::sat(rtm::pow_nonneg(rtm::max(sp.spec_dot, 0.0f), 40.0f)) * sp.spec_k;
+    SkyColor scat = get_rayleigh_mie(c, pdn);
+    h.cb = make_float4(sp.col[0] + specular, sp.col[1] + specular, sp.col[2] + specular, sp.brightness);
+    h.ray = make_float4(scat.rayleigh.x, scat.rayleigh.y, scat.rayleigh.z, skyAmount);
+    // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): first step
+    march_begin(c, st, hp, 0.4f, sp.precision, c.sun);
+    if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
+    h.more = march_live<L, true, true>(c, st, 100.0f, 0);
+    return h;
+}
+
+template <int L>
+__device__ __forceinline__ void shadow_pack(const March<L, true>& st, uint32_t t, float4* r)
+{
+    r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
+    r[1] = make_float4(st.step, st.lastStep, st.d, __int_as_float(st.iters));
+    r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
+    r[3] = make_float4(__uint_as_float(t), 0.0f, 0.0f, 0.0f);
+}
+
+// tracing.hlsl:60-61: the march direction is SunDirection / length(SunDirection)
+template <int L>
+__device__ __forceinline__ uint32_t shadow_unpack(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
+                                                  f3 sun_dir, March<L, true>& st)
+{
+    st.p = rtm::mk(r0.x, r0.y, r0.z);
+    st.dist = r0.w;
+    st.dir = sun_dir;
+    st.step = r1.x;
+    st.lastStep = r1.y;
+    st.d = r1.z;
+    st.iters = __float_as_int(r1.w);
+    st.f = {r2.x, r2.y, r2.z, r2.w};
+    return __float_as_uint(r3.x);
+}
+
+// Shading of the hits a fused k_trace could not keep on its CU (hitlist, counter
+// RT_CTR_HITS): finish the short shadows, append the long ones to the global list.
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__ k,
                                                     const uint32_t* __restrict__ perm2d,
                                                     const float4* __restrict__ grad, UnitMap m,
                                                     const float4* __restrict__ res,
                                                     const uint32_t* __restrict__ hitlist,
-                                                    float4* __restrict__ samples, float4* __restrict__ shrec,
-                                                    uint32_t* __restrict__ longlist, uint32_t* __restrict__ counters,
+                                                    float4* __restrict__ samples, float4* __restrict__ fin,
+                                                    float4* __restrict__ shrec, uint32_t* __restrict__ counters,
                                                     RtStats* stats)
 {
+    const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
+    if (n_hits == 0u) return; // everything was shaded inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
-    const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
     const uint32_t n_units = (n_hits + 63u) / 64u;
     float ssteps = 0.0f;
     for (;;) {
@@ -651,52 +722,24 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
         const uint32_t i = u * 64u + lane;
         bool more = false;
         uint32_t t = 0;
-        float4 cb, fog, ray;
         March<L, true> st;
         if (i < n_hits) {
             t = hitlist[i];
-            float4 pdw = res[3u * t + 0u], dn = res[3u * t + 2u];
-            fog = res[3u * t + 1u];
-            uint32_t px, py, a;
-            sample_pixel(m, t, aa, W, H, &px, &py, &a);
-            f3 p, dir;
-            get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
-            f3 pdn = rtm::normalize(dir);
-            // tracescreen.hlsl:22-35 (hit branch)
-            float skyAmount = pdw.w * 0.0005f;
-            skyAmount = rtm::sat(skyAmount * skyAmount);
-            f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
-            f3 n = get_normal<L>(c, pd);
-            f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
-            ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
-            // color.hlsl:63-66: the specular term does not depend on the shadow
-            float specular = rtm::sat(rtm::pow_nonneg(rtm::max(sp.spec_dot, 0.0f), 40.0f)) * sp.spec_k;
-            SkyColor scat = get_rayleigh_mie(c, pdn);
-            cb = make_float4(sp.col[0] + specular, sp.col[1] + specular, sp.col[2] + specular, sp.brightness);
-            ray = make_float4(scat.rayleigh.x, scat.rayleigh.y, scat.rayleigh.z, skyAmount);
-            // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): first step
-            march_begin(c, st, hp, 0.4f, sp.precision, c.sun);
-            if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
-            more = march_live<L, true, true>(c, st, 100.0f, 0);
+            ShadeHit h = shade_hit<L, false>(c, m, res, t, st);
+            more = h.more;
             if (!more) {
-                samples[t] = shade_finish(k, cb, fog, ray, st.d, st.f.w);
+                samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
                 if constexpr (STATS) ssteps += (float)st.iters;
+            } else {
+                fin[3u * t + 0u] = h.cb;
+                fin[3u * t + 1u] = h.fog;
+                fin[3u * t + 2u] = h.ray;
             }
         }
         const uint64_t lb = __ballot(more);
         if (lb) {
             const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
-            if (more) {
-                const uint32_t j = b + (uint32_t)__popcll(lb & lt_mask);
-                longlist[j] = t;
-                float4* r = shrec + (size_t)kShadowRec * j;
-                r[0] = cb;
-                r[1] = fog;
-                r[2] = ray;
-                r[3] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
-                r[4] = make_float4(st.step, st.lastStep, st.d, __int_as_float(st.iters));
-                r[5] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
-            }
+            if (more) shadow_pack(st, t, shrec + (size_t)kShadowRec * (b + (uint32_t)__popcll(lb & lt_mask)));
         }
     }
     if constexpr (STATS) {
@@ -705,34 +748,35 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
     }
 }
 
+// The long shadow rays on the global list (counter RT_CTR_LONG) with lane refill:
+// each lane takes the next ray as soon as its own ends.  A retiring lane finishes
+// its sample from fin[t].
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                 const float4* __restrict__ grad,
-                                                 const float4* __restrict__ shrec,
-                                                 const uint32_t* __restrict__ longlist, float4* __restrict__ samples,
+                                                 const float4* __restrict__ grad, const float4* __restrict__ shrec,
+                                                 const float4* __restrict__ fin, float4* __restrict__ samples,
                                                  uint32_t* __restrict__ counters, RtStats* stats)
 {
+    const uint32_t n_long = __builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]);
+    if (n_long == 0u) return; // every long shadow ray was marched inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
-    const uint32_t n_long = __builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]);
-    // tracing.hlsl:60-61: the march direction is dir / length(dir) of SunDirection
     const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
     March<L, true> st;
     st.d = 0.0f;
     st.iters = 0;
     bool live = false;
-    uint32_t j = 0;
+    uint32_t t = 0;
     uint32_t pool = 0, pool_left = 0; // wave-uniform
     bool drained = false;
     float ssteps = 0.0f;
     for (;;) {
         // 1. retire rays that left the loop: finish their samples
         if (live && !march_live<L, true, true>(c, st, 100.0f, 0)) {
-            const float4* r = shrec + (size_t)kShadowRec * j;
-            samples[longlist[j]] = shade_finish(k, r[0], r[1], r[2], st.d, st.f.w);
+            samples[t] = shade_finish(k, fin[3u * t], fin[3u * t + 1u], fin[3u * t + 2u], st.d, st.f.w);
             live = false;
             if constexpr (STATS) ssteps += (float)st.iters;
         }
@@ -754,18 +798,9 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
                     const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                     const bool mine = ((idle >> lane) & 1ull) && rank < take;
                     if (mine) {
-                        j = pool + rank;
-                        const float4* r = shrec + (size_t)kShadowRec * j;
-                        const float4 pd = r[3], sv = r[4], f = r[5];
-                        st.p = rtm::mk(pd.x, pd.y, pd.z);
-                        st.dist = pd.w;
-                        st.dir = sun_dir;
-                        st.step = sv.x;
-                        st.lastStep = sv.y;
-                        st.d = sv.z;
-                        st.iters = __float_as_int(sv.w);
-                        st.f = {f.x, f.y, f.z, f.w};
-                        live = true; // it was live when k_shade_pre stored it
+                        const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
+                        t = shadow_unpack(r[0], r[1], r[2], r[3], sun_dir, st);
+                        live = true; // it was live when it was stored
                     }
                     idle &= ~__ballot(mine);
                     pool += take;
@@ -782,6 +817,256 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     }
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    }
+}
+
+// ===========================================================================
+// Fused trace (default pipeline): the primary march, the hit shading and the long
+// shadow rays in ONE persistent kernel, so the latency-bound shading phases run in
+// the shadow of the VALU-bound primary march instead of after it.  Each CU keeps
+// two block-local rings in LDS, fed and drained by its own 16 waves:
+//   hits  : sample ids of primary hits (pushed by a wave when it finishes a unit);
+//   longs : march state of shadow rays still live after their first step (pushed
+//           by a wave when it finishes a shading batch).
+// A wave's next job, in priority order: march long shadows (lane refill from the
+// ring) when enough are queued; shade a batch of 64 queued hits; march the next
+// primary unit from the global longest-first queue.  Ring operations hold a
+// per-block LDS lock for a few instructions.  Every hand-off stays on one CU: the
+// producer's global stores (res / fin) complete (s_waitcnt) before the ring push,
+// and the consumer reads them with L1-bypassing loads from the XCD's L2.  A full
+// ring spills to the global lists, which k_shade_pre / k_shadow drain afterwards.
+constexpr uint32_t kHitRing = 1024;
+constexpr uint32_t kLongRing = 256;
+constexpr uint32_t kLongBatch = 48; // queued long shadows that make a wave switch to them
+
+struct TraceQueues {
+    uint32_t lock;
+    uint32_t h_head, h_tail;
+    uint32_t l_head, l_tail;
+    uint32_t active;  // waves inside a primary unit or a shading batch (they may still push)
+    uint32_t drained; // the global unit queue is exhausted
+    uint32_t pad;
+    uint32_t hits[kHitRing];
+    float4 longs[kLongRing * kShadowRec];
+};
+
+template <class T>
+__device__ __forceinline__ T vload(const T& x)
+{
+    return *const_cast<const volatile T*>(&x);
+}
+
+__device__ __forceinline__ void q_lock(uint32_t* lock, uint32_t lane)
+{
+    if (lane == 0) {
+        while (atomicCAS(lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) atomicExch(lock, 0u);
+}
+
+template <int L, bool STATS>
+__global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                const float4* __restrict__ grad, const float2* __restrict__ cells,
+                                                UnitMap m, const uint32_t* __restrict__ order,
+                                                float4* __restrict__ res, float4* __restrict__ samples,
+                                                float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
+                                                float4* __restrict__ shrec, uint32_t* __restrict__ counters,
+                                                RtStats* stats)
+{
+    __shared__ uint32_t lds[kNoiseLdsWords];
+    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
+    __shared__ TraceQueues q;
+    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
+    if (threadIdx.x == 0) {
+        q.lock = 0;
+        q.h_head = q.h_tail = 0;
+        q.l_head = q.l_tail = 0;
+        q.active = 0;
+        q.drained = 0;
+    }
+    load_noise_lds(lds, perm2d, grad);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    Ctx c = make_ctx(k, lds);
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    const int max_steps = k->max_steps;
+    const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
+    float psteps = 0.0f, ssteps = 0.0f;
+    uint32_t nhits = 0;
+
+    // ---- a batch of long shadow rays, lane refill from the ring ----
+    auto do_shadow = [&]() {
+        March<L, true> st;
+        st.d = 0.0f;
+        st.iters = 0;
+        bool live = false;
+        uint32_t t = 0;
+        for (;;) {
+            if (live && !march_live<L, true, true>(c, st, 100.0f, 0)) {
+                samples[t] = shade_finish(k, ld_fresh(fin + 3u * t), ld_fresh(fin + 3u * t + 1u),
+                                          ld_fresh(fin + 3u * t + 2u), st.d, st.f.w);
+                live = false;
+                if constexpr (STATS) ssteps += (float)st.iters;
+            }
+            const uint64_t idle = __ballot(!live);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= kRefillIdle && vload(q.l_tail) != vload(q.l_head)) {
+                q_lock(&q.lock, lane);
+                const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
+                const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
+                const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                if (((idle >> lane) & 1ull) && rank < take) {
+                    const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
+                    t = shadow_unpack(r[0], r[1], r[2], r[3], sun_dir, st);
+                    live = true;
+                }
+                if (lane == 0) q.l_head = head + take;
+                q_unlock(&q.lock, lane);
+            }
+            if (__ballot(live) == 0ull) return;
+            if (live) march_step<L, true, true>(c, st);
+        }
+    };
+
+    // ---- a batch of up to 64 queued hits: shading + first shadow step ----
+    auto do_shade = [&]() {
+        q_lock(&q.lock, lane);
+        const uint32_t head = vload(q.h_head), tail = vload(q.h_tail);
+        const uint32_t take = (tail - head) < 64u ? (tail - head) : 64u;
+        uint32_t t = 0;
+        if (lane < take) t = q.hits[(head + lane) % kHitRing];
+        if (lane == 0) q.h_head = head + take;
+        q_unlock(&q.lock, lane);
+        March<L, true> st;
+        bool more = false;
+        if (lane < take) {
+            ShadeHit h = shade_hit<L, true>(c, m, res, t, st);
+            more = h.more;
+            if (!more) {
+                samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
+                if constexpr (STATS) ssteps += (float)st.iters;
+            } else {
+                fin[3u * t + 0u] = h.cb;
+                fin[3u * t + 1u] = h.fog;
+                fin[3u * t + 2u] = h.ray;
+            }
+        }
+        const uint64_t lb = __ballot(more);
+        if (lb) {
+            const uint32_t n = (uint32_t)__popcll(lb), rank = (uint32_t)__popcll(lb & lt_mask);
+            __builtin_amdgcn_s_waitcnt(0); // fin[t] is in L2 before the ray is visible
+            q_lock(&q.lock, lane);
+            const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
+            const bool fits = lt - lh + n <= kLongRing;
+            if (fits) {
+                if (more) shadow_pack(st, t, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
+                if (lane == 0) q.l_tail = lt + n;
+            }
+            q_unlock(&q.lock, lane);
+            if (!fits) {
+                const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, n);
+                if (more) shadow_pack(st, t, shrec + (size_t)kShadowRec * (b + rank));
+            }
+        }
+    };
+
+    // ---- one 8x8 primary unit (as k_primary) ----
+    auto do_unit = [&](uint32_t u) {
+        uint32_t px, py;
+        const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
+        const float pxf = (float)px, pyf = (float)py;
+        float plane_x = 0.0f;
+        if (valid) {
+            float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
+            plane_x = s_plane[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))];
+        }
+        for (uint32_t a = 0; a < aa; ++a) {
+            const uint32_t t = (u * 64u + lane) * aa + a;
+            March<L, true> st;
+            st.d = 0.0f;
+            bool lv = false;
+            if (valid) {
+                f3 p, dir;
+                get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
+                march_begin(c, st, p, plane_x, 1.0f, dir);
+                lv = true;
+            }
+            __builtin_amdgcn_s_setprio(0);
+            for (uint32_t it = 0;; ++it) {
+                lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
+                if (__ballot(lv) == 0ull) break;
+                if (lv) march_step<L, true, false>(c, st);
+                if (it == 96u) __builtin_amdgcn_s_setprio(1);
+                else if (it == 224u) __builtin_amdgcn_s_setprio(2);
+                else if (it == 384u) __builtin_amdgcn_s_setprio(3);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            const bool hit = valid && st.d > 0.0f;
+            if (valid) {
+                RayResult rr = march_result(st);
+                store_ray(res, t, rr);
+                if constexpr (STATS) psteps += rr.steps;
+            }
+            const uint64_t hb = __ballot(hit);
+            if (hb) {
+                const uint32_t n = (uint32_t)__popcll(hb), rank = (uint32_t)__popcll(hb & lt_mask);
+                if constexpr (STATS) nhits += hit ? 1u : 0u;
+                __builtin_amdgcn_s_waitcnt(0); // res[t] is in L2 before the hit is visible
+                q_lock(&q.lock, lane);
+                const uint32_t hh = vload(q.h_head), ht = vload(q.h_tail);
+                const bool fits = ht - hh + n <= kHitRing;
+                if (fits) {
+                    if (hit) q.hits[(ht + rank) % kHitRing] = t;
+                    if (lane == 0) q.h_tail = ht + n;
+                }
+                q_unlock(&q.lock, lane);
+                if (!fits) {
+                    const uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, n);
+                    if (hit) hitlist[b + rank] = t;
+                }
+            }
+        }
+    };
+
+    for (;;) {
+        const uint32_t lp = vload(q.l_tail) - vload(q.l_head);
+        const uint32_t hp = vload(q.h_tail) - vload(q.h_head);
+        const bool drained = vload(q.drained) != 0u;
+        if (lp >= kLongBatch || (drained && lp > 0u)) {
+            do_shadow();
+            continue;
+        }
+        if (hp >= 64u || (drained && hp > 0u)) {
+            if (lane == 0) atomicAdd(&q.active, 1u);
+            do_shade();
+            if (lane == 0) atomicSub(&q.active, 1u);
+            continue;
+        }
+        if (!drained) {
+            if (lane == 0) atomicAdd(&q.active, 1u);
+            const uint32_t qi = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+            if (qi < m.n_units) do_unit(__builtin_amdgcn_readfirstlane(order[qi >> 4]) * 16u + (qi & 15u));
+            else if (lane == 0) q.drained = 1u;
+            if (lane == 0) atomicSub(&q.active, 1u);
+            continue;
+        }
+        // drained and nothing queued: leave once no wave of the block can still push
+        if (vload(q.active) == 0u && vload(q.l_tail) == vload(q.l_head) && vload(q.h_tail) == vload(q.h_head)) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if constexpr (STATS) {
+        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
+        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->hits, (unsigned long long)nhits);
         atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
     }
 }
@@ -922,42 +1207,30 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     uint32_t need = (m.n_units + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
-    static const int shadow_threads = [] {
-        const char* e = getenv("RT_SHADOW_THREADS");
-        int v = e ? atoi(e) : 1024;
-        return (v == 256 || v == 512 || v == 1024) ? v : 1024;
-    }();
-    dim3 sblk(shadow_threads);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
-    const bool refill = a.pipeline == RT_PIPELINE_REFILL;
-    if (!refill) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
-    if (a.stats) {
-        if (refill)
-            hipLaunchKernelGGL((k_march<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
+    const int pipe = a.pipeline;
+    if (pipe != RT_PIPELINE_REFILL) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
+    // primary (+ shading in the fused kernel); hits it did not shade go to the global list
+    auto primary = [&](auto stats_tag) {
+        constexpr bool S = decltype(stats_tag)::value;
+        if (pipe == RT_PIPELINE_REFILL)
+            hipLaunchKernelGGL((k_march<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
                                a.res, a.hitlist, a.queue, a.stats);
-        else
-            hipLaunchKernelGGL((k_primary<L, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
+        else if (pipe == RT_PIPELINE_STAGED)
+            hipLaunchKernelGGL((k_primary<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
                                m, a.order, a.res, a.hitlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade_pre<L, true>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
-                           a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, true>), dim3(blocks), sblk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
-                           a.longlist, a.samples, a.queue, a.stats);
-        hipLaunchKernelGGL((k_finish<true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.samples, out8, out32, a.queue, a.stats);
-    } else {
-        if (refill)
-            hipLaunchKernelGGL((k_march<L, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
-                               m, a.res, a.hitlist, a.queue, a.stats);
         else
-            hipLaunchKernelGGL((k_primary<L, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               cells, m, a.order, a.res, a.hitlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shade_pre<L, false>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m,
-                           a.res, a.hitlist, a.samples, a.shrec, a.longlist, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, false>), dim3(blocks), sblk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
-                           a.longlist, a.samples, a.queue, a.stats);
-        hipLaunchKernelGGL((k_finish<false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+            hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
+                               a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+                           a.hitlist, a.samples, a.fin, a.shrec, a.queue, a.stats);
+        hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+                           a.fin, a.samples, a.queue, a.stats);
+        hipLaunchKernelGGL((k_finish<S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.samples, out8, out32, a.queue, a.stats);
-    }
+    };
+    if (a.stats) primary(std::true_type{});
+    else primary(std::false_type{});
 }
 
 } // namespace

@@ -106,13 +106,13 @@ struct rt_device_s {
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
-    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" = single kernel, "refill" = lane-refill primary
+    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" = single kernel, "refill" / "staged" = unfused primary
     float4* samples = nullptr;     // split pipeline buffers, sized for samples_cap samples
     float4* res = nullptr;
     uint32_t* hitlist = nullptr;
     uint32_t* order = nullptr;
     float4* shrec = nullptr;
-    uint32_t* longlist = nullptr;
+    float4* fin = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
     bool profiling = false;
@@ -398,7 +398,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.hitlist = dev->hitlist;
     a.order = dev->order;
     a.shrec = dev->shrec;
-    a.longlist = dev->longlist;
+    a.fin = dev->fin;
     return a;
 }
 
@@ -423,9 +423,9 @@ int ensure_split_buffers(rt_device dev, int aa)
     if (dev->hitlist) HIP_TRY(hipFree(dev->hitlist));
     if (dev->order) HIP_TRY(hipFree(dev->order));
     if (dev->shrec) HIP_TRY(hipFree(dev->shrec));
-    if (dev->longlist) HIP_TRY(hipFree(dev->longlist));
+    if (dev->fin) HIP_TRY(hipFree(dev->fin));
     dev->shrec = nullptr;
-    dev->longlist = nullptr;
+    dev->fin = nullptr;
     dev->samples = nullptr;
     dev->res = nullptr;
     dev->hitlist = nullptr;
@@ -434,8 +434,8 @@ int ensure_split_buffers(rt_device dev, int aa)
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dev->shrec, need * 6 * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->longlist, need * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->shrec, need * 4 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * sizeof(uint32_t)));
     dev->samples_cap = need;
     return RT_OK;
@@ -490,8 +490,9 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
     HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
     if (const char* p = getenv("RT_PIPELINE"))
-        d->pipeline = strcmp(p, "mega") == 0 ? RT_PIPELINE_MEGA
+        d->pipeline = strcmp(p, "mega") == 0     ? RT_PIPELINE_MEGA
                       : strcmp(p, "refill") == 0 ? RT_PIPELINE_REFILL
+                      : strcmp(p, "staged") == 0 ? RT_PIPELINE_STAGED
                                                  : RT_PIPELINE_SPLIT;
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
@@ -519,7 +520,7 @@ void rt_device_destroy(rt_device d)
     if (d->hitlist) (void)hipFree(d->hitlist);
     if (d->order) (void)hipFree(d->order);
     if (d->shrec) (void)hipFree(d->shrec);
-    if (d->longlist) (void)hipFree(d->longlist);
+    if (d->fin) (void)hipFree(d->fin);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);

@@ -5,7 +5,7 @@ import gpgpuraytrace_amd as G
 import oracle_lib as O
 W, H = 96, 64
 nz = O.noise_tables()
-for pipe in ("split", "mega", "refill"):
+for pipe in ("split", "staged", "mega", "refill"):
     os.environ["RT_PIPELINE"] = pipe
     for land in ("nomadplains", "testing"):
         for name, eul in (("reset", G.camera.INITIAL_ROTATION_EULER), ("down", G.camera.LOOKDOWN_ROTATION_EULER)):

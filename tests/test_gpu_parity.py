@@ -124,7 +124,7 @@ def test_density_bitexact(land):
 
 
 # --- whole frames vs the golden oracle frames ----------------------------------------------
-@pytest.mark.parametrize("pipeline", ["split", "mega", "refill"])
+@pytest.mark.parametrize("pipeline", ["split", "staged", "mega", "refill"])
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_frame_bitexact_device_path(spec, pipeline):
     gold = GI.load()
