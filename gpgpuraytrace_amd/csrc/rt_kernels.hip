@@ -111,6 +111,7 @@ __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __rest
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
     Ctx c = make_ctx(k, lds);
     const uint32_t j = threadIdx.x & 31u, base = threadIdx.x & 32u;
+    const GroupOctaves g = group_octaves(c, j);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
     const float r31 = rtm::rcp(31.0f);
     uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
@@ -123,7 +124,7 @@ __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __rest
     while (march_live<L, false, true>(c, st, RT_CAMERA_FAR, 0)) {
         march_step_with<L, false, true>(c, st, [&](f3 q) {
             uint32_t used;
-            float d = density_nomadplains_group(c, q, j, base, &used);
+            float d = density_nomadplains_group(c, g, q, base, &used);
             noise += used + 1u;
             return d;
         });

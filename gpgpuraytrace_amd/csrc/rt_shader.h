@@ -165,7 +165,28 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 // gathered in N order with the same fma chain, so the value is bit-identical to
 // density_nomadplains.  `base` = first lane of the group within the wave.  Every
 // lane of the group must be active (the gathers read all of them).
-__device__ __forceinline__ float density_nomadplains_group(const Ctx& c, f3 p, uint32_t j, uint32_t base,
+// Per-lane constants of the group form, loaded once per kernel: this lane's octave
+// scales (lane j < 17: octave j+1; the steep-noise lane takes its own constants) and
+// the octave weights 1/S (uniform).
+struct GroupOctaves {
+    float sx, sy;  // noise-input scales of this lane's octave
+    bool steep;    // this lane evaluates the steep noise
+    float rcp[RT_NP_OCTAVES + 1];
+};
+
+__device__ __forceinline__ GroupOctaves group_octaves(const Ctx& c, uint32_t j)
+{
+    GroupOctaves g;
+    g.steep = j >= (uint32_t)RT_NP_OCTAVES;
+    const uint32_t o = g.steep ? 1u : j + 1u;
+    g.sx = c.k->np_scale[o];
+    g.sy = c.k->np_scale_y[o];
+#pragma unroll
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) g.rcp[N] = c.k->np_rcp[N];
+    return g;
+}
+
+__device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const GroupOctaves& g, f3 p, uint32_t base,
                                                            uint32_t* octaves)
 {
     float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
@@ -173,13 +194,8 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, f3 p, u
     f3 p1 = rtm::scale(p, 0.4f);
     float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
-    float nx, ny, nzz;
-    if (j < (uint32_t)RT_NP_OCTAVES) {
-        float S = c.k->np_scale[j + 1];
-        nx = q0.x * S;
-        ny = q0.y * c.k->np_scale_y[j + 1];
-        nzz = q0.z * S;
-    } else {
+    float nx = q0.x * g.sx, ny = q0.y * g.sy, nzz = q0.z * g.sx;
+    if (g.steep) {
         nx = p1.x * 0.007138f;
         ny = p1.z * 0.007138f;
         nzz = 0.0f;
@@ -188,15 +204,14 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, f3 p, u
     float on[RT_NP_OCTAVES + 1];
 #pragma unroll
     for (int N = 1; N <= RT_NP_OCTAVES + 1; ++N) on[N - 1] = __shfl(n, (int)(base + N - 1), 64);
+    // N = 1 .. floor(detail) in order.  A dead octave adds n*0 = +-0 instead of being
+    // skipped: s + (+-0) == s bit for bit because s is never -0 (it starts at +0 and
+    // an exact cancellation rounds to +0), so the chain needs no branches.
+    const int n_oct = (int)detail;
     float s = 0.0f;
-    uint32_t used = 0;
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
-        const bool live = (float)N <= detail; // N = 1 .. floor(detail), in order
-        s = live ? fma(on[N - 1], c.k->np_rcp[N], s) : s;
-        used += live ? 1u : 0u;
-    }
-    *octaves = used;
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N - 1], N <= n_oct ? g.rcp[N] : 0.0f, s);
+    *octaves = (uint32_t)n_oct;
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((on[RT_NP_OCTAVES] - 0.2f) * 6.0f) * 7.5f;
     float floorsize = steep * 1.8f;
