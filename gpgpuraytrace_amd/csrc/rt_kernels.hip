@@ -122,12 +122,13 @@ __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __rest
     march_begin(c, st, p, RT_CAMERA_NEAR, 2.0f, dir);
     uint32_t noise = 0;
     while (march_live<L, false, true>(c, st, RT_CAMERA_FAR, 0)) {
-        march_step_with<L, false, true>(c, st, [&](f3 q) {
+        auto dens = [&](f3 q) {
             uint32_t used;
             float d = density_nomadplains_group(c, g, q, base, &used);
             noise += used + 1u;
             return d;
-        });
+        };
+        march_step_with<L, false, true, decltype(dens), true>(c, st, dens);
     }
     RayResult rr = march_result(st);
     if (rr.density < 0.0f) rr.pd.w = RT_CAMERA_FAR;

@@ -195,6 +195,52 @@ RT_HD float exp2_fin(float x)
     return __builtin_ldexpf(p, (int)n);
 }
 
+// pow_nonneg without control flow, for latency-bound code where a single wave's
+// dependency chain is the critical path: every lane runs both polynomials and the
+// special cases are selected afterwards, so it is bit-identical to pow_nonneg for
+// x >= 0 finite and finite y > 0 (x == 0 -> log2 -inf -> exp2 0; the clamped
+// exp2 argument only ever replaces results that are then selected away).
+RT_HD float pow_nonneg_flat(float x, float y)
+{
+#if !defined(__HIP_DEVICE_COMPILE__)
+    return exp2_fin(y * log2_nonneg(x));
+#else
+    int e;
+    float m = __builtin_frexpf(x, &e);
+    uint32_t mb = bits(m) + 0x00800000u;
+    e -= 1;
+    const bool hi = mb > 0x3fb504f3u;
+    mb = hi ? mb - 0x00800000u : mb;
+    e = hi ? e + 1 : e;
+    float f = fbits(mb) - 1.0f;
+    float p = -0x1.c362c0p-4f;
+    p = fma(p, f, 0x1.7d9132p-3f);
+    p = fma(p, f, -0x1.87381ap-3f);
+    p = fma(p, f, 0x1.a2f85ep-3f);
+    p = fma(p, f, -0x1.eabd64p-3f);
+    p = fma(p, f, 0x1.277e9ap-2f);
+    p = fma(p, f, -0x1.715a76p-2f);
+    p = fma(p, f, 0x1.ec7094p-2f);
+    p = fma(p, f, -0x1.715470p-1f);
+    p = fma(p, f, 0x1.715476p+0f);
+    const float lg = x == 0.0f ? -__builtin_inff() : fma(f, p, (float)e);
+    const float a = y * lg;
+    const float ac = min(max(a, -150.0f), 128.0f);
+    const float n = rint(ac);
+    const float g = ac - n;
+    float q = 0x1.41a6fep-13f;
+    q = fma(q, g, 0x1.5f44f0p-10f);
+    q = fma(q, g, 0x1.3b2dfep-7f);
+    q = fma(q, g, 0x1.c6aed6p-5f);
+    q = fma(q, g, 0x1.ebfbdap-3f);
+    q = fma(q, g, 0x1.62e430p-1f);
+    q = fma(q, g, 1.0f);
+    float r = __builtin_ldexpf(q, (int)n);
+    r = a >= 128.0f ? __builtin_inff() : r;
+    return a < -150.0f ? 0.0f : r;
+#endif
+}
+
 RT_HD float pow(float x, float y) { return exp2(y * log2(x)); }
 // pow for x >= 0 (abs/saturate/length bases) and finite y > 0.
 RT_HD float pow_nonneg(float x, float y) { return exp2_fin(y * log2_nonneg(x)); }

@@ -192,7 +192,7 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const G
     float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
     float d = -p.y;
     f3 p1 = rtm::scale(p, 0.4f);
-    float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
+    float detail = rtm::max(18.0f - rtm::pow_nonneg_flat(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
     float nx = q0.x * g.sx, ny = q0.y * g.sy, nzz = q0.z * g.sx;
     if (g.steep) {
@@ -212,7 +212,7 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const G
 #pragma unroll
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N - 1], N <= n_oct ? g.rcp[N] : 0.0f, s);
     *octaves = (uint32_t)n_oct;
-    s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
+    s = rtm::pow_nonneg_flat(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((on[RT_NP_OCTAVES] - 0.2f) * 6.0f) * 7.5f;
     float floorsize = steep * 1.8f;
     float t;
@@ -224,7 +224,7 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const G
     s = fma(-(t * t), floorsize, s);
     t = rtm::sat((p1.y - 22.0f) * steep);
     s = fma(-(t * t), floorsize, s);
-    s = fma(rtm::pow_nonneg(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
+    s = fma(rtm::pow_nonneg_flat(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
     return d + s;
 }
 
@@ -384,7 +384,7 @@ __device__ __forceinline__ bool march_live(const Ctx& c, const March<L, CALCFOG>
     return m.dist < enddist && m.step > c.k->min_limit && !(max_steps > 0 && m.iters >= max_steps);
 }
 
-template <int L, bool CALCFOG, bool SKIPREFINE, class Density>
+template <int L, bool CALCFOG, bool SKIPREFINE, class Density, bool FLAT = false>
 __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>& m, Density density)
 {
     const RtConsts* k = c.k;
@@ -408,7 +408,10 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
         m.f.z = m.f.z - fs.z;
         m.f.w = m.f.w - fs.w;
     } else {
-        float stepmult = 1.0f + rtm::pow_nonneg(rtm::abs(rtm::min(m.d + 5.0f, 0.0f)), k->density_factor);
+        const float sx = rtm::abs(rtm::min(m.d + 5.0f, 0.0f));
+        float stepmult;
+        if constexpr (FLAT) stepmult = 1.0f + rtm::pow_nonneg_flat(sx, k->density_factor);
+        else stepmult = 1.0f + rtm::pow_nonneg(sx, k->density_factor);
         m.step = m.step * k->step_factor;
         m.lastStep = m.step * stepmult;
         m.dist = m.dist + m.lastStep;
