@@ -201,8 +201,10 @@ __global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__
 // tracescreen.hlsl:16-48 traceSample
 template <int L>
 __device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn, float plane_x, float plane_y,
-                                           float* psteps, float* ssteps, int* hit)
+                                           float* psteps, float* ssteps, int* hit, uint32_t px, uint32_t py,
+                                           uint32_t a, float* ao_out, float* aosteps)
 {
+    *ao_out = 1.0f;
     RayResult rr = trace_ray<L, true, false>(c, pp, plane_x, plane_y, 1.0f, pdir, c.k->max_steps);
     *psteps += rr.steps;
     float skyAmount = rr.pd.w * 0.0005f;
@@ -217,6 +219,16 @@ __device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn,
         ShadePre sp = shade_pre<L>(c, hp, n, pdn, rr.pd.w);
         RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
         *ssteps += sr.steps;
+        if (c.k->ao_samples > 0) { // AO extension (rt_shader.h ao_dir)
+            uint32_t occ = 0;
+            for (int kk = 0; kk < c.k->ao_samples; ++kk) {
+                RayResult ar = trace_ray<L, false, true>(c, hp, 0.4f, RT_AO_END, sp.precision,
+                                                         ao_dir(n, px, py, a, (uint32_t)kk), 0);
+                *aosteps += ar.steps;
+                occ += ar.density > 0.0f ? 1u : 0u;
+            }
+            *ao_out = ao_factor(occ, c.k->ao_samples);
+        }
         color = shade_post(c, sp, sr.density, sr.fc.w);
         color = rtm::mk(rtm::lerp(color.x, rr.fc.x, rr.fc.w), rtm::lerp(color.y, rr.fc.y, rr.fc.w),
                         rtm::lerp(color.z, rr.fc.z, rr.fc.w));
@@ -238,7 +250,7 @@ __device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn,
 template <int L>
 __device__ __forceinline__ void shade_pixel(const Ctx& c, uint32_t px, uint32_t py, const float2* __restrict__ cells,
                                             uint32_t* __restrict__ out8, float4* __restrict__ out32, float* psteps,
-                                            float* ssteps, int* hits)
+                                            float* ssteps, int* hits, float* aosteps)
 {
     const RtConsts* k = c.k;
     float pxf = (float)px, pyf = (float)py;
@@ -251,10 +263,18 @@ __device__ __forceinline__ void shade_pixel(const Ctx& c, uint32_t px, uint32_t 
         f3 p, dir;
         get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
         f3 pdn = rtm::normalize(dir);
-        f3 s = trace_sample<L>(c, p, dir, pdn, plane_x, plane_y, psteps, ssteps, hits);
-        col0 = col0 + rtm::sat(s.x);
-        col1 = col1 + rtm::sat(s.y);
-        col2 = col2 + rtm::sat(s.z);
+        float ao;
+        f3 s = trace_sample<L>(c, p, dir, pdn, plane_x, plane_y, psteps, ssteps, hits, px, py, (uint32_t)a, &ao,
+                               aosteps);
+        if (k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
+            col0 = col0 + rtm::sat(s.x) * ao;
+            col1 = col1 + rtm::sat(s.y) * ao;
+            col2 = col2 + rtm::sat(s.z) * ao;
+        } else {
+            col0 = col0 + rtm::sat(s.x);
+            col1 = col1 + rtm::sat(s.y);
+            col2 = col2 + rtm::sat(s.z);
+        }
     }
     float ia = rtm::rcp((float)aa);
     col0 = col0 * ia;
@@ -281,7 +301,7 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
     const uint32_t lane = threadIdx.x & 63u;
     Ctx c = make_ctx(k, lds);
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
-    float psteps = 0.0f, ssteps = 0.0f;
+    float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
     int hits = 0;
     for (;;) {
         uint32_t u = 0;
@@ -293,12 +313,13 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
         uint32_t gy = (T / tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
         if (gx < ext_x && gy < ext_y) {
             uint32_t px = gx + off_x, py = gy + off_y;
-            if (px < W && py < H) shade_pixel<L>(c, px, py, cells, out8, out32, &psteps, &ssteps, &hits);
+            if (px < W && py < H) shade_pixel<L>(c, px, py, cells, out8, out32, &psteps, &ssteps, &hits, &aosteps);
         }
     }
     if constexpr (STATS) {
         atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
         atomicAdd(&stats->hits, (unsigned long long)hits);
         atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
     }
@@ -636,7 +657,12 @@ __device__ __forceinline__ float4 ld_fresh(const float4* p)
 struct ShadeHit {
     float4 cb, fog, ray;
     bool more; // the shadow ray is still marching after its first step
+    f3 hp, n;  // hit position and normal (AO rays start here)
+    float prec; // shadow-ray stepmod (AO rays reuse it)
+    uint32_t px, py, a;
 };
+
+enum { RT_LONG_SHADOW = 0, RT_LONG_AO = 1 };
 
 // tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.
 template <int L, bool FRESH>
@@ -651,6 +677,9 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
     uint32_t px, py, a;
     sample_pixel(m, t, aa, W, H, &px, &py, &a);
+    h.px = px;
+    h.py = py;
+    h.a = a;
     f3 p, dir;
     get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
     f3 pdn = rtm::normalize(dir);
@@ -659,12 +688,15 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
     f3 n = get_normal<L>(c, pd);
     f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
+    h.hp = hp;
+    h.n = n;
     ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
     // color.hlsl:63-66: the specular term does not depend on the shadow
     float specular = rtm::sat(rtm::pow_nonneg(rtm::max(sp.spec_dot, 0.0f), 40.0f)) * sp.spec_k;
     SkyColor scat = get_rayleigh_mie(c, pdn);
     h.cb = make_float4(sp.col[0] + specular, sp.col[1] + specular, sp.col[2] + specular, sp.brightness);
     h.ray = make_float4(scat.rayleigh.x, scat.rayleigh.y, scat.rayleigh.z, skyAmount);
+    h.prec = sp.precision;
     // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): first step
     march_begin(c, st, hp, 0.4f, sp.precision, c.sun);
     if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
@@ -672,29 +704,64 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     return h;
 }
 
+// Long-ray record: (p, dist), (step, lastStep, d, iters), (shadow fog | AO dir, -), (t, type, -, -).
+// A shadow ray's direction is SunDirection / length(SunDirection) (tracing.hlsl:60-61) for
+// every ray; an AO ray carries its own (normalised) direction in the fog slot, since AO
+// rays march without fog.
 template <int L>
-__device__ __forceinline__ void shadow_pack(const March<L, true>& st, uint32_t t, float4* r)
+__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t type, float4* r)
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
     r[1] = make_float4(st.step, st.lastStep, st.d, __int_as_float(st.iters));
-    r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
-    r[3] = make_float4(__uint_as_float(t), 0.0f, 0.0f, 0.0f);
+    if (type == RT_LONG_AO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
+    else r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
+    r[3] = make_float4(__uint_as_float(t), __uint_as_float(type), 0.0f, 0.0f);
 }
 
-// tracing.hlsl:60-61: the march direction is SunDirection / length(SunDirection)
 template <int L>
-__device__ __forceinline__ uint32_t shadow_unpack(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
-                                                  f3 sun_dir, March<L, true>& st)
+__device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
+                                                f3 sun_dir, March<L, true>& st, uint32_t* type)
 {
+    *type = __float_as_uint(r3.y);
     st.p = rtm::mk(r0.x, r0.y, r0.z);
     st.dist = r0.w;
-    st.dir = sun_dir;
     st.step = r1.x;
     st.lastStep = r1.y;
     st.d = r1.z;
     st.iters = __float_as_int(r1.w);
-    st.f = {r2.x, r2.y, r2.z, r2.w};
+    if (*type == RT_LONG_AO) {
+        st.dir = rtm::mk(r2.x, r2.y, r2.z);
+        st.f = {0.0f, 0.0f, 0.0f, 0.0f};
+        st.fog = false;
+    } else {
+        st.dir = sun_dir;
+        st.f = {r2.x, r2.y, r2.z, r2.w};
+        st.fog = true;
+    }
     return __float_as_uint(r3.x);
+}
+
+// AO ray k of a shaded hit, at its start (AO extension, rt_shader.h ao_dir)
+template <int L>
+__device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32_t kk, March<L, true>& st)
+{
+    march_begin(c, st, h.hp, 0.4f, h.prec, ao_dir(h.n, h.px, h.py, h.a, kk), false);
+}
+
+// A long ray left its loop: a shadow ray finishes its sample from fin[t]; an AO ray
+// counts its occlusion for k_finish.
+template <int L, bool FRESH>
+__device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __restrict__ fin,
+                                            float4* __restrict__ samples, uint32_t* __restrict__ aocc, uint32_t t,
+                                            uint32_t type, const March<L, true>& st)
+{
+    if (type == RT_LONG_AO) {
+        if (st.d > 0.0f) atomicAdd(&aocc[t], 1u);
+    } else {
+        const float4* f = fin + 3u * t;
+        samples[t] = FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
+                           : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w);
+    }
 }
 
 // Shading of the hits a fused k_trace could not keep on its CU (hitlist, counter
@@ -706,9 +773,10 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
                                                     const float4* __restrict__ res,
                                                     const uint32_t* __restrict__ hitlist,
                                                     float4* __restrict__ samples, float4* __restrict__ fin,
-                                                    float4* __restrict__ shrec, uint32_t* __restrict__ counters,
-                                                    RtStats* stats)
+                                                    float4* __restrict__ shrec, uint32_t long_cap,
+                                                    uint32_t* __restrict__ counters, RtStats* stats)
 {
+    // hits the primary pass did not shade itself (all of them for k_primary / k_march)
     const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
     if (n_hits == 0u) return; // everything was shaded inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
@@ -722,12 +790,14 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
         uint32_t u = wave_fetch(&counters[RT_CTR_SHADE], lane);
         if (u >= n_units) break;
         const uint32_t i = u * 64u + lane;
+        const bool valid = i < n_hits;
         bool more = false;
         uint32_t t = 0;
         March<L, true> st;
-        if (i < n_hits) {
+        ShadeHit h;
+        if (valid) {
             t = hitlist[i];
-            ShadeHit h = shade_hit<L, false>(c, m, res, t, st);
+            h = shade_hit<L, false>(c, m, res, t, st);
             more = h.more;
             if (!more) {
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
@@ -741,7 +811,19 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
         const uint64_t lb = __ballot(more);
         if (lb) {
             const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
-            if (more) shadow_pack(st, t, shrec + (size_t)kShadowRec * (b + (uint32_t)__popcll(lb & lt_mask)));
+            const uint32_t j = b + (uint32_t)__popcll(lb & lt_mask);
+            if (more && j < long_cap) long_pack(st, t, RT_LONG_SHADOW, shrec + (size_t)kShadowRec * j);
+        }
+        // AO extension: every AO ray of every hit goes to the long list
+        const uint64_t vb = __ballot(valid);
+        for (int kk = 0; kk < k->ao_samples; ++kk) {
+            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(vb));
+            const uint32_t j = b + (uint32_t)__popcll(vb & lt_mask);
+            if (valid && j < long_cap) {
+                March<L, true> ao;
+                ao_begin(c, h, (uint32_t)kk, ao);
+                long_pack(ao, t, RT_LONG_AO, shrec + (size_t)kShadowRec * j);
+            }
         }
     }
     if constexpr (STATS) {
@@ -757,9 +839,10 @@ template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                  const float4* __restrict__ grad, const float4* __restrict__ shrec,
                                                  const float4* __restrict__ fin, float4* __restrict__ samples,
+                                                 uint32_t* __restrict__ aocc, uint32_t long_cap,
                                                  uint32_t* __restrict__ counters, RtStats* stats)
 {
-    const uint32_t n_long = __builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]);
+    const uint32_t n_long = min(__builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]), long_cap);
     if (n_long == 0u) return; // every long shadow ray was marched inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
@@ -771,16 +854,19 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     st.d = 0.0f;
     st.iters = 0;
     bool live = false;
-    uint32_t t = 0;
+    uint32_t t = 0, type = RT_LONG_SHADOW;
     uint32_t pool = 0, pool_left = 0; // wave-uniform
     bool drained = false;
-    float ssteps = 0.0f;
+    float ssteps = 0.0f, aosteps = 0.0f;
     for (;;) {
         // 1. retire rays that left the loop: finish their samples
-        if (live && !march_live<L, true, true>(c, st, 100.0f, 0)) {
-            samples[t] = shade_finish(k, fin[3u * t], fin[3u * t + 1u], fin[3u * t + 2u], st.d, st.f.w);
+        if (live && !march_live<L, true, true>(c, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
+            long_finish<L, false>(k, fin, samples, aocc, t, type, st);
             live = false;
-            if constexpr (STATS) ssteps += (float)st.iters;
+            if constexpr (STATS) {
+                if (type == RT_LONG_AO) aosteps += (float)st.iters;
+                else ssteps += (float)st.iters;
+            }
         }
         // 2. refill idle lanes from the wave's pool of long-list indices
         if (!drained) {
@@ -801,8 +887,8 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
                     const bool mine = ((idle >> lane) & 1ull) && rank < take;
                     if (mine) {
                         const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
-                        t = shadow_unpack(r[0], r[1], r[2], r[3], sun_dir, st);
-                        live = true; // it was live when it was stored
+                        t = long_unpack(r[0], r[1], r[2], r[3], sun_dir, st, &type);
+                        live = true; // AO rays start live; shadow rays were live when stored
                     }
                     idle &= ~__ballot(mine);
                     pool += take;
@@ -819,6 +905,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     }
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
         atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
     }
 }
@@ -881,7 +968,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 UnitMap m, const uint32_t* __restrict__ order,
                                                 float4* __restrict__ res, float4* __restrict__ samples,
                                                 float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
-                                                float4* __restrict__ shrec, uint32_t* __restrict__ counters,
+                                                float4* __restrict__ shrec, uint32_t long_cap,
+                                                uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
@@ -902,22 +990,44 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
     const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
-    float psteps = 0.0f, ssteps = 0.0f;
+    float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
     uint32_t nhits = 0;
 
-    // ---- a batch of long shadow rays, lane refill from the ring ----
+    // push the lanes' long rays (shadow continuations or AO starts) to the ring, or
+    // to the global list when the ring is full
+    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t type) {
+        const uint64_t lb = __ballot(want);
+        if (!lb) return;
+        const uint32_t n = (uint32_t)__popcll(lb), rank = (uint32_t)__popcll(lb & lt_mask);
+        q_lock(&q.lock, lane);
+        const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
+        const bool fits = lt - lh + n <= kLongRing;
+        if (fits) {
+            if (want) long_pack(st, t, type, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
+            if (lane == 0) q.l_tail = lt + n;
+        }
+        q_unlock(&q.lock, lane);
+        if (!fits) {
+            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, n);
+            if (want && b + rank < long_cap) long_pack(st, t, type, shrec + (size_t)kShadowRec * (b + rank));
+        }
+    };
+
+    // ---- a batch of long rays, lane refill from the ring ----
     auto do_shadow = [&]() {
         March<L, true> st;
         st.d = 0.0f;
         st.iters = 0;
         bool live = false;
-        uint32_t t = 0;
+        uint32_t t = 0, type = RT_LONG_SHADOW;
         for (;;) {
-            if (live && !march_live<L, true, true>(c, st, 100.0f, 0)) {
-                samples[t] = shade_finish(k, ld_fresh(fin + 3u * t), ld_fresh(fin + 3u * t + 1u),
-                                          ld_fresh(fin + 3u * t + 2u), st.d, st.f.w);
+            if (live && !march_live<L, true, true>(c, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
+                long_finish<L, true>(k, fin, samples, aocc, t, type, st);
                 live = false;
-                if constexpr (STATS) ssteps += (float)st.iters;
+                if constexpr (STATS) {
+                    if (type == RT_LONG_AO) aosteps += (float)st.iters;
+                    else ssteps += (float)st.iters;
+                }
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -928,7 +1038,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                 if (((idle >> lane) & 1ull) && rank < take) {
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
-                    t = shadow_unpack(r[0], r[1], r[2], r[3], sun_dir, st);
+                    t = long_unpack(r[0], r[1], r[2], r[3], sun_dir, st, &type);
                     live = true;
                 }
                 if (lane == 0) q.l_head = head + take;
@@ -950,8 +1060,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         q_unlock(&q.lock, lane);
         March<L, true> st;
         bool more = false;
-        if (lane < take) {
-            ShadeHit h = shade_hit<L, true>(c, m, res, t, st);
+        const bool valid = lane < take;
+        ShadeHit h;
+        if (valid) {
+            h = shade_hit<L, true>(c, m, res, t, st);
             more = h.more;
             if (!more) {
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
@@ -962,22 +1074,15 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 fin[3u * t + 2u] = h.ray;
             }
         }
-        const uint64_t lb = __ballot(more);
-        if (lb) {
-            const uint32_t n = (uint32_t)__popcll(lb), rank = (uint32_t)__popcll(lb & lt_mask);
+        if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // fin[t] is in L2 before the ray is visible
-            q_lock(&q.lock, lane);
-            const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
-            const bool fits = lt - lh + n <= kLongRing;
-            if (fits) {
-                if (more) shadow_pack(st, t, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
-                if (lane == 0) q.l_tail = lt + n;
-            }
-            q_unlock(&q.lock, lane);
-            if (!fits) {
-                const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, n);
-                if (more) shadow_pack(st, t, shrec + (size_t)kShadowRec * (b + rank));
-            }
+            push_long(more, st, t, RT_LONG_SHADOW);
+        }
+        // AO extension: the hit's AO rays start as long rays
+        for (int kk = 0; kk < k->ao_samples; ++kk) {
+            March<L, true> ao;
+            if (valid) ao_begin(c, h, (uint32_t)kk, ao);
+            push_long(valid, ao, t, RT_LONG_AO);
         }
     };
 
@@ -1068,6 +1173,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     if constexpr (STATS) {
         atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
+        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
         atomicAdd(&stats->hits, (unsigned long long)nhits);
         atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
     }
@@ -1081,8 +1187,9 @@ template <bool STATS>
 __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                  const float4* __restrict__ grad, UnitMap m,
                                                  const float4* __restrict__ res, const float4* __restrict__ samples,
-                                                 uint32_t* __restrict__ out8, float4* __restrict__ out32,
-                                                 uint32_t* __restrict__ counters, RtStats* stats)
+                                                 const uint32_t* __restrict__ aocc, uint32_t* __restrict__ out8,
+                                                 float4* __restrict__ out32, uint32_t* __restrict__ counters,
+                                                 RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
@@ -1100,6 +1207,10 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
             float4 v;
             if (dn.x > 0.0f) {
                 v = samples[t];
+                if (k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
+                    const float ao = ao_factor(aocc[t], k->ao_samples);
+                    v = make_float4(v.x * ao, v.y * ao, v.z * ao, v.w);
+                }
             } else {
                 float4 pdw = res[3u * t + 0u], fog = res[3u * t + 1u];
                 f3 p, dir;
@@ -1210,6 +1321,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
+    if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
     if (pipe != RT_PIPELINE_REFILL) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
     // primary (+ shading in the fused kernel); hits it did not shade go to the global list
@@ -1223,13 +1335,14 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
                                m, a.order, a.res, a.hitlist, a.queue, a.stats);
         else
             hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
-                               a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.queue, a.stats);
+                               a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
+                               a.stats);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.hitlist, a.samples, a.fin, a.shrec, a.queue, a.stats);
+                           a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
-                           a.fin, a.samples, a.queue, a.stats);
+                           a.fin, a.samples, a.aocc, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_finish<S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.samples, out8, out32, a.queue, a.stats);
+                           a.samples, a.aocc, out8, out32, a.queue, a.stats);
     };
     if (a.stats) primary(std::true_type{});
     else primary(std::false_type{});

@@ -113,7 +113,9 @@ struct rt_device_s {
     uint32_t* order = nullptr;
     float4* shrec = nullptr;
     float4* fin = nullptr;
+    uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
+    size_t long_cap = 0; // entries of the global long-ray list (shrec)
     // dominant-kernel timing (rt_device_set_profiling)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -180,7 +182,7 @@ static const int kCbSize[CB_COUNT] = {12, 84, 80, 2048, 8};
 struct Shader {
     int kind = KIND_TRACESCREEN;
     int landscape = RT_NOMADPLAINS;
-    int aa = 1, recording = 0, max_steps = 0;
+    int aa = 1, recording = 0, max_steps = 0, ao = 0;
     int tx = 16, ty = 16, tz = 1;
     bool has_cb[CB_COUNT] = {};
     std::vector<uint8_t> cb[CB_COUNT];
@@ -361,6 +363,7 @@ void build_consts(const Shader& s, const rt_device_s& dev, RtConsts& k)
     k.aa_samples = s.aa;
     k.landscape = s.landscape;
     k.max_steps = s.max_steps;
+    k.ao_samples = s.kind == KIND_TRACESCREEN ? s.ao : 0;
     k.width = dev.width;
     k.height = dev.height;
 }
@@ -398,7 +401,11 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.hitlist = dev->hitlist;
     a.order = dev->order;
     a.shrec = dev->shrec;
+    a.long_cap = (uint32_t)std::min<size_t>(dev->long_cap, 0xffffffffu);
     a.fin = dev->fin;
+    a.aocc = dev->aocc;
+    a.ao_samples = s->ao;
+    a.aa = s->aa;
     return a;
 }
 
@@ -412,11 +419,17 @@ int check_texture(Shader* s)
 }
 
 // Split-pipeline buffers: per AA sample of every whole 32x32 tile, one shaded
-// colour (16 B), one primary RayResult (48 B) and one hit-list slot (4 B).
-int ensure_split_buffers(rt_device dev, int aa)
+// colour (16 B), one primary RayResult (48 B), one hit-list slot (4 B), the
+// shading inputs of a long shadow ray (48 B) and an AO occlusion count (4 B); the
+// global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
+// (64 B each).
+int ensure_split_buffers(rt_device dev, int aa, int ao)
 {
     size_t need = rt_split_samples(dev->width, dev->height, aa);
-    if (need <= dev->samples_cap) return RT_OK;
+    size_t long_need = need * (size_t)(1 + ao);
+    if (need <= dev->samples_cap && long_need <= dev->long_cap) return RT_OK;
+    need = std::max(need, dev->samples_cap);
+    long_need = std::max(long_need, dev->long_cap);
     HIP_TRY(hipStreamSynchronize(dev->stream));
     if (dev->samples) HIP_TRY(hipFree(dev->samples));
     if (dev->res) HIP_TRY(hipFree(dev->res));
@@ -424,8 +437,10 @@ int ensure_split_buffers(rt_device dev, int aa)
     if (dev->order) HIP_TRY(hipFree(dev->order));
     if (dev->shrec) HIP_TRY(hipFree(dev->shrec));
     if (dev->fin) HIP_TRY(hipFree(dev->fin));
+    if (dev->aocc) HIP_TRY(hipFree(dev->aocc));
     dev->shrec = nullptr;
     dev->fin = nullptr;
+    dev->aocc = nullptr;
     dev->samples = nullptr;
     dev->res = nullptr;
     dev->hitlist = nullptr;
@@ -434,10 +449,12 @@ int ensure_split_buffers(rt_device dev, int aa)
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dev->shrec, need * 4 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->shrec, long_need * 4 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->aocc, need * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * sizeof(uint32_t)));
     dev->samples_cap = need;
+    dev->long_cap = long_need;
     return RT_OK;
 }
 
@@ -521,6 +538,7 @@ void rt_device_destroy(rt_device d)
     if (d->order) (void)hipFree(d->order);
     if (d->shrec) (void)hipFree(d->shrec);
     if (d->fin) (void)hipFree(d->fin);
+    if (d->aocc) (void)hipFree(d->aocc);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -600,6 +618,7 @@ int rt_device_stats(rt_device d, rt_stats* out, int reset)
     out->prepass_steps = h.prepass_steps;
     out->hits = h.hits;
     out->noise_calls = h.noise_calls;
+    out->ao_steps = h.ao_steps;
     if (reset) HIP_TRY(hipMemsetAsync(d->stats, 0, sizeof(RtStats), d->stream));
     return RT_OK;
 }
@@ -716,6 +735,11 @@ int rt_compute_load(rt_compute c, const char* directory, const char* file, const
                 return fail(RT_ERR_INVALID, "Unsupported AA sample count (antialiasing.hlsl:47)");
             s->aa = aa;
         } else if (k == "RT_MAX_STEPS") s->max_steps = std::max(0, atoi(v.c_str()));
+        else if (k == "RT_AO_SAMPLES") {
+            int ao = atoi(v.c_str());
+            if (ao < 0 || ao > 16) return fail(RT_ERR_INVALID, "RT_AO_SAMPLES must be 0..16");
+            s->ao = ao;
+        }
     }
     // Reflection (what fxc reports for these shaders; tracing.hlsl:6-22, noise.hlsl:130-133,
     // tracescreen.hlsl:8-14, camerarays.hlsl:3).
@@ -804,7 +828,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     if (rc) return rc;
     rc = sync_shader(dev, s);
     if (rc) return rc;
-    if (s->kind == KIND_TRACESCREEN && (rc = ensure_split_buffers(dev, s->aa))) return rc;
+    if (s->kind == KIND_TRACESCREEN && (rc = ensure_split_buffers(dev, s->aa, s->ao))) return rc;
     RtLaunch a = make_launch(dev, s);
     if (dz == 0) return RT_OK;
     if (s->kind == KIND_CAMERARAYS) {
@@ -914,7 +938,7 @@ int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_
     int rc;
     if ((rc = check_texture(cam->shader)) || (rc = check_texture(scr->shader))) return rc;
     if ((rc = sync_shader(dev, cam->shader)) || (rc = sync_shader(dev, scr->shader))) return rc;
-    if ((rc = ensure_split_buffers(dev, scr->shader->aa))) return rc;
+    if ((rc = ensure_split_buffers(dev, scr->shader->aa, scr->shader->ao))) return rc;
     rt_array_s* cr = cam->shader->array("CameraResults");
     rt_array_s* cd = scr->shader->array("CellDistance");
     if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");

@@ -241,12 +241,16 @@ __device__ __forceinline__ float density_simple(const Ctx& c, f3 p)
     float d = -p.y;
     f3 q = rtm::scale(p, 0.006f);
     float n = noise3d(c.nz, q.x * 1.0f, q.y * 0.0f, q.z * 1.0f) * 150.0f;
+    // serialise the four independent lattice evaluations (register pressure)
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z) : "v"(n));
     f3 q2 = rtm::scale(p, 0.002f);
     float w2 = rtm::min(rtm::max(fma(-p.y, 1.5f, 50.0f), 0.0f), 36.0f);
     n = fma(-fma(noise3d(c.nz, q2.x, q2.y, q2.z), 0.5f, 0.5f), w2, n);
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z) : "v"(n));
     f3 q3 = rtm::scale(p, 0.003f);
     float w3 = rtm::min(rtm::max(fma(-p.y, 1.5f, 10.0f), 0.0f), 36.0f);
     n = fma(-fma(noise3d(c.nz, q3.x, q3.y, q3.z), 0.5f, 0.5f), w3, n);
+    asm volatile("" : "+v"(p.x), "+v"(p.y), "+v"(p.z) : "v"(n));
     f3 q4 = rtm::scale(p, 0.06f);
     float S = c.k->np_scale[1];
     n = fma(noise3d(c.nz, q4.x * S, q4.y * c.k->np_scale_y[1], q4.z * S), c.k->np_rcp[1], n);
@@ -348,11 +352,14 @@ struct March {
     float dist, step, lastStep, d;
     f4 f;
     int iters;
+    bool fog; // calcfog at run time (AO rays share the shadow lanes but march without fog)
 };
 
 template <int L, bool CALCFOG>
-__device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, f3 p, float dist, float stepmod, f3 dir)
+__device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, f3 p, float dist, float stepmod, f3 dir,
+                                            bool fog = true)
 {
+    m.fog = fog;
     const RtConsts* k = c.k;
     m.f = {0.0f, 0.0f, 0.0f, 0.0f};
     m.d = 0.0f;
@@ -361,7 +368,7 @@ __device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, 
     m.lastStep = m.step;
     float il = rtm::rcp(dirLength);
     dir = rtm::scale(dir, il);
-    if constexpr (March<L, CALCFOG>::FOG) {
+    if constexpr (March<L, CALCFOG>::FOG) if (fog) {
         float hd = dist * 0.5f;
         f3 mp = rtm::mk(fma(dir.x * dist, 0.5f, p.x), fma(dir.y * dist, 0.5f, p.y), fma(dir.z * dist, 0.5f, p.z));
         f4 mf = get_fog<L>(c, mp, hd);
@@ -392,7 +399,7 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
     m.rayp = rtm::mk(fma(m.dir.x, m.dist, m.p.x), fma(m.dir.y, m.dist, m.p.y), fma(m.dir.z, m.dist, m.p.z));
     m.d = density(m.rayp);
     f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
-    if constexpr (March<L, CALCFOG>::FOG) {
+    if constexpr (March<L, CALCFOG>::FOG) if (m.fog) {
         f4 g = get_fog<L>(c, m.rayp, m.dist);
         fs.x = g.x * m.step;
         fs.y = g.y * m.step;
@@ -642,6 +649,49 @@ __device__ __forceinline__ f3 shade_post(const Ctx& c, const ShadePre& s, float 
     return rtm::mk(c0 * fma(b, k->one_minus_shadow[0], k->shadow_color[0]),
                    c1 * fma(b, k->one_minus_shadow[1], k->shadow_color[1]),
                    c2 * fma(b, k->one_minus_shadow[2], k->shadow_color[2]));
+}
+
+// ---------------------------------------------------------------------------
+// Build extension, BASELINE.json configs C3/C5 ("1-bounce AO"; the reference has no
+// ambient occlusion, so the definition is the build's own, restated identically in
+// oracle/rt_oracle.c ao_dir / ambient_occlusion): per primary hit, AO_SAMPLES
+// cosine-weighted hemisphere rays about the normal, direction from a PCG hash of
+// (pixel, AA sample, k), marched as traceRay(p, 0.4, 25, shadow stepmod, dir,
+// no fog, skiprefine); ao = 1 - 0.6 * occluded / AO multiplies the saturated sample.
+#define RT_AO_END 25.0f
+#define RT_AO_STRENGTH 0.6f
+
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t x)
+{
+    uint32_t st = x * 747796405u + 2891336453u;
+    uint32_t w = ((st >> ((st >> 28u) + 4u)) ^ st) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+
+__device__ __forceinline__ f3 cross3(f3 a, f3 b)
+{
+    return rtm::mk(fma(a.y, b.z, -(a.z * b.y)), fma(a.z, b.x, -(a.x * b.z)), fma(a.x, b.y, -(a.y * b.x)));
+}
+
+__device__ __forceinline__ f3 ao_dir(f3 n, uint32_t px, uint32_t py, uint32_t a, uint32_t k)
+{
+    uint32_t h = pcg_hash((px * 0x9E3779B1u) ^ (py * 0x85EBCA77u) ^ ((a * 16u + k) * 0xC2B2AE3Du));
+    uint32_t h2 = pcg_hash(h);
+    float u1 = (float)(h >> 8) * 0x1p-24f, u2 = (float)(h2 >> 8) * 0x1p-24f;
+    float r = rtm::sqrt(u1);
+    float sn, cs;
+    rtm::sincos(u2 * 6.2831855f, &sn, &cs);
+    float sx = r * cs, sy = r * sn, sz = rtm::sqrt(rtm::max(1.0f - u1, 0.0f));
+    f3 up = rtm::abs(n.x) > 0.9f ? rtm::mk(0.0f, 1.0f, 0.0f) : rtm::mk(1.0f, 0.0f, 0.0f);
+    f3 tx = rtm::normalize(cross3(up, n));
+    f3 ty = cross3(n, tx);
+    return rtm::mk(fma(tx.x, sx, fma(ty.x, sy, n.x * sz)), fma(tx.y, sx, fma(ty.y, sy, n.y * sz)),
+                   fma(tx.z, sx, fma(ty.z, sy, n.z * sz)));
+}
+
+__device__ __forceinline__ float ao_factor(uint32_t occluded, int ao)
+{
+    return fma(-RT_AO_STRENGTH, (float)occluded * rtm::rcp((float)ao), 1.0f);
 }
 
 __device__ __forceinline__ uint32_t unorm8(float v) { return (uint32_t)rtm::rint(rtm::sat(v) * 255.0f); }

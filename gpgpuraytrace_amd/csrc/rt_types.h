@@ -44,6 +44,7 @@ struct RtConsts {
     int32_t aa_samples;
     int32_t landscape;
     int32_t max_steps; // build extension (0 = unbounded, reference semantics)
+    int32_t ao_samples; // build extension: AO rays per primary hit (0 = off, reference semantics)
     int32_t width, height;
     int32_t pad[3];
 };
@@ -55,4 +56,5 @@ struct RtStats {
     unsigned long long prepass_steps;
     unsigned long long hits;
     unsigned long long noise_calls;
+    unsigned long long ao_steps;
 };

@@ -258,10 +258,11 @@ class Terrain:
     render_device() is the same frame with the round trip kept on the GPU."""
 
     def __init__(self, device, theme="nomadplains", record_mode=False, aa_samples=1, max_steps=0,
-                 noise_seed=300, rand_kind=Noise.RAND_MSVC):
+                 noise_seed=300, rand_kind=Noise.RAND_MSVC, ao_samples=0):
         vfs_add_path("Media/" + theme)  # Terrain.cpp:23
         self.device, self.theme, self.record_mode = device, theme, record_mode
-        self.aa_samples, self.max_steps = aa_samples, max_steps
+        # max_steps / ao_samples: build extensions (BASELINE configs), 0 = reference semantics
+        self.aa_samples, self.max_steps, self.ao_samples = aa_samples, max_steps, ao_samples
         self.noise_seed, self.rand_kind = noise_seed, rand_kind
         self.compute = self.camera_compute = None
         self.camera = None
@@ -286,7 +287,9 @@ class Terrain:
             macros.append(("AA_SAMPLES", str(self.aa_samples)))
         if self.max_steps:
             macros.append(("RT_MAX_STEPS", str(self.max_steps)))
-        ok1 = self.compute.create("shaders", "tracescreen.hlsl", "CSMain", (self.thread_x, self.thread_y, 1), macros)
+        screen_macros = macros + ([("RT_AO_SAMPLES", str(self.ao_samples))] if self.ao_samples else [])
+        ok1 = self.compute.create("shaders", "tracescreen.hlsl", "CSMain", (self.thread_x, self.thread_y, 1),
+                                  screen_macros)
         ok2 = self.camera_compute.create("shaders", "camerarays.hlsl", "CSMain",
                                          (CAMERA_THREAD_RES, CAMERA_THREAD_RES, 1), macros)
         return ok1 and ok2

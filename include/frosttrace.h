@@ -59,6 +59,7 @@ typedef struct {
     unsigned long long prepass_steps; /* traceRay iterations, camerarays */
     unsigned long long hits;          /* primary hits == shadow rays */
     unsigned long long noise_calls;   /* noise3d evaluations (BASELINE.md algorithmic work unit) */
+    unsigned long long ao_steps;      /* traceRay iterations, AO rays (build extension RT_AO_SAMPLES) */
 } rt_stats;
 
 /* ---- diagnostics ---- */

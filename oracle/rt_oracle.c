@@ -726,10 +726,73 @@ static const float (*aa_table(int n))[2]
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/* Build extension, BASELINE.json configs C3/C5 ("1-bounce AO"); the reference has
+ * no ambient occlusion, so this definition is the build's own and
+ * the GPU implements it identically:
+ *   for each primary hit and k = 0..AO-1, one cosine-weighted hemisphere ray about
+ *   the surface normal, direction from a PCG hash of (pixel, AA sample, k), marched
+ *   like a shadow ray (traceRay(p, 0.4, 25, shadow stepmod, dir, no fog, skiprefine));
+ *   ao = 1 - 0.6 * occluded / AO multiplies the saturated sample colour. */
+#define RO_AO_END 25.0f
+#define RO_AO_STRENGTH 0.6f
+
+static uint32_t pcg_hash(uint32_t x)
+{
+    uint32_t st = x * 747796405u + 2891336453u;
+    uint32_t w = ((st >> ((st >> 28u) + 4u)) ^ st) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+
+static f3 cross3(f3 a, f3 b)
+{
+    return v3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+
+static f3 ao_dir(f3 n, uint32_t px, uint32_t py, uint32_t a, uint32_t k)
+{
+    uint32_t h = pcg_hash((px * 0x9E3779B1u) ^ (py * 0x85EBCA77u) ^ ((a * 16u + k) * 0xC2B2AE3Du));
+    uint32_t h2 = pcg_hash(h);
+    float u1 = (float)(h >> 8) * 0x1p-24f, u2 = (float)(h2 >> 8) * 0x1p-24f;
+    float r = sqrtf(u1);
+    float sn, cs;
+    sincos_red(u2 * 6.2831855f, &sn, &cs);
+    float sx = r * cs, sy = r * sn, sz = sqrtf(ro_max(1.0f - u1, 0.0f));
+    f3 up = fabsf(n.x) > 0.9f ? v3(0.0f, 1.0f, 0.0f) : v3(1.0f, 0.0f, 0.0f);
+    f3 tx = norm3(cross3(up, n));
+    f3 ty = cross3(n, tx);
+    return v3(fmaf(tx.x, sx, fmaf(ty.x, sy, n.x * sz)), fmaf(tx.y, sx, fmaf(ty.y, sy, n.y * sz)),
+              fmaf(tx.z, sx, fmaf(ty.z, sy, n.z * sz)));
+}
+
+/* color.hlsl:47-50: the shadow ray's stepmod, reused by the AO rays */
+static float shadow_precision(float dist)
+{
+    float mipf = ro_max(0.5f * ro_log2(dist), 0.0f);
+    return ro_max((mipf - 3.2f) * 3.0f, 1.0f) * 8.0f;
+}
+
+static float ambient_occlusion(ctx* c, f3 p, f3 n, float dist, uint32_t px, uint32_t py, uint32_t a,
+                               uint64_t* ao_steps, uint64_t* ao_rays)
+{
+    int ao = c->fr->ao_samples;
+    float prec = shadow_precision(dist);
+    int occ = 0;
+    for (int k = 0; k < ao; ++k) {
+        ray_result rr = trace_ray(c, p, 0.4f, RO_AO_END, prec, ao_dir(n, px, py, a, (uint32_t)k), 0, 1, 0);
+        *ao_steps += (uint64_t)rr.steps;
+        *ao_rays += 1;
+        if (rr.density > 0.0f) occ += 1;
+    }
+    return fmaf(-RO_AO_STRENGTH, (float)occ * rcp((float)ao), 1.0f);
+}
+
 /* tracescreen.hlsl:16-48 */
 static f3 trace_sample(ctx* c, const sky_consts* k, f3 pp, f3 pdir, f3 pdn, float plane_x, float plane_y,
-                       float* steps_out, uint64_t* prim_steps, uint64_t* hits, uint64_t* shadow_steps)
+                       float* steps_out, uint64_t* prim_steps, uint64_t* hits, uint64_t* shadow_steps,
+                       uint32_t px, uint32_t py, uint32_t a, float* ao_out, uint64_t* ao_steps, uint64_t* ao_rays)
 {
+    *ao_out = 1.0f;
     ray_result rr = trace_ray(c, pp, plane_x, plane_y, 1.0f, pdir, 1, 0, c->fr->max_steps);
     *steps_out += rr.steps;
     *prim_steps += (uint64_t)rr.steps;
@@ -742,6 +805,8 @@ static f3 trace_sample(ctx* c, const sky_consts* k, f3 pp, f3 pdir, f3 pdn, floa
         f4 npd = {rr.pd.x, rr.pd.y, rr.pd.z, rr.density}; /* getNormal(float4(rr.pd.xyz, rr.density)) :31 */
         f3 n = get_normal(c, npd);
         color = get_color(c, v3(rr.pd.x, rr.pd.y, rr.pd.z), n, pdn, rr.pd.w, shadow_steps);
+        if (c->fr->ao_samples > 0)
+            *ao_out = ambient_occlusion(c, v3(rr.pd.x, rr.pd.y, rr.pd.z), n, rr.pd.w, px, py, a, ao_steps, ao_rays);
         color = v3(lerp(color.x, rr.fcolord.x, rr.fcolord.w), lerp(color.y, rr.fcolord.y, rr.fcolord.w),
                    lerp(color.z, rr.fcolord.z, rr.fcolord.w));
         color = v3(lerp(color.x, scat.rayleigh.x, skyAmount), lerp(color.y, scat.rayleigh.y, skyAmount),
@@ -851,9 +916,9 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
     int aa = fr->aa_samples;
     if (aa != 2 && aa != 4 && aa != 8 && aa != 16) aa = 1;
     const float (*offs)[2] = aa_table(aa);
-    uint64_t noise = 0, pst = 0, sst = 0, hits = 0, rays = 0, dens = 0;
+    uint64_t noise = 0, pst = 0, sst = 0, hits = 0, rays = 0, dens = 0, aost = 0, aor = 0;
     int nt = fr->threads > 0 ? fr->threads : 0;
-#pragma omp parallel for schedule(dynamic, 1) reduction(+ : noise, pst, sst, hits, rays, dens) num_threads(nt ? nt : omp_get_max_threads())
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : noise, pst, sst, hits, rays, dens, aost, aor) num_threads(nt ? nt : omp_get_max_threads())
     for (int ri = 0; ri < nrows; ++ri) {
         int y = r0 + ri * rs;
         ctx c;
@@ -869,10 +934,19 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
                 f3 p, dir;
                 get_pixel_ray(&c, pxf + offs[a][0] * (1.0f / 16.0f), pyf + offs[a][1] * (1.0f / 16.0f), &p, &dir);
                 f3 pdn = norm3(dir);
-                f3 s = trace_sample(&c, &k, p, dir, pdn, plane_x, plane_y, &steps, &pst, &hits, &sst);
-                col[0] = col[0] + sat(s.x);
-                col[1] = col[1] + sat(s.y);
-                col[2] = col[2] + sat(s.z);
+                float ao;
+                f3 s = trace_sample(&c, &k, p, dir, pdn, plane_x, plane_y, &steps, &pst, &hits, &sst, (uint32_t)x,
+                                    (uint32_t)y, (uint32_t)a, &ao, &aost, &aor);
+                if (fr->ao_samples > 0) {
+                    /* AO extension: ao multiplies the saturated sample (1.0 for misses) */
+                    col[0] = col[0] + sat(s.x) * ao;
+                    col[1] = col[1] + sat(s.y) * ao;
+                    col[2] = col[2] + sat(s.z) * ao;
+                } else {
+                    col[0] = col[0] + sat(s.x);
+                    col[1] = col[1] + sat(s.y);
+                    col[2] = col[2] + sat(s.z);
+                }
                 rays += 1;
             }
             float ia = rcp((float)aa);
@@ -898,6 +972,8 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
         st->primary_hits += hits;
         st->primary_rays += rays;
         st->density_calls += dens;
+        st->ao_steps += aost;
+        st->ao_rays += aor;
     }
 }
 

@@ -50,6 +50,7 @@ typedef struct {
     float sun[3];                 /* XTweakable.SunDirection */
     int32_t row_begin, row_end, row_step; /* tracescreen rows to evaluate (CPU-baseline subsample) */
     int32_t threads;              /* OpenMP threads, <=0 = all */
+    int32_t ao_samples;           /* build extension (BASELINE configs C3/C5): AO rays per primary hit, 0 = off */
 } ro_frame;
 
 typedef struct {
@@ -60,6 +61,8 @@ typedef struct {
     uint64_t primary_rays;
     uint64_t primary_hits;    /* = shadow rays */
     uint64_t density_calls;
+    uint64_t ao_steps;        /* traceRay iterations of AO rays (build extension) */
+    uint64_t ao_rays;
 } ro_stats;
 
 /* ---- tables ---- */

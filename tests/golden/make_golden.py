@@ -25,7 +25,7 @@ import oracle_lib as O  # noqa: E402
 from gpgpuraytrace_amd import camera as cam  # noqa: E402
 
 POSES = {"reset": cam.INITIAL_ROTATION_EULER, "lookdown": cam.LOOKDOWN_ROTATION_EULER}
-FRAMES = [  # (landscape, pose, W, H, aa, max_steps)
+FRAMES = [  # (landscape, pose, W, H, aa, max_steps[, ao_samples])
     ("nomadplains", "reset", 64, 48, 1, 0),
     ("nomadplains", "lookdown", 64, 48, 1, 0),
     ("nomadplains", "reset", 48, 32, 4, 0),
@@ -34,11 +34,20 @@ FRAMES = [  # (landscape, pose, W, H, aa, max_steps)
     ("testing", "lookdown", 64, 48, 1, 0),
     ("simple", "reset", 48, 32, 1, 0),
     ("greenrocks", "reset", 48, 32, 1, 0),
+    # AO build extension (BASELINE configs C3/C5): (..., ao_samples)
+    ("nomadplains", "reset", 64, 48, 1, 0, 1),
+    ("nomadplains", "lookdown", 48, 32, 1, 512, 4),
+    ("greenrocks", "reset", 48, 32, 2, 0, 2),
 ]
 
 
-def frame_key(land, pose, w, h, aa, ms):
-    return f"{land}_{pose}_{w}x{h}_aa{aa}_ms{ms}"
+def frame_key(land, pose, w, h, aa, ms, ao=0):
+    return f"{land}_{pose}_{w}x{h}_aa{aa}_ms{ms}" + (f"_ao{ao}" if ao else "")
+
+
+def unpack(spec):
+    """(landscape, pose, W, H, aa, max_steps[, ao_samples]) -> 7-tuple"""
+    return tuple(spec) + (0,) * (7 - len(spec))
 
 
 def consts_for(w, h, pose):
@@ -63,10 +72,11 @@ def main():
 
     nz = O.noise_tables()
     out = {}
-    for land, pose, w, h, aa, ms in FRAMES:
-        fr = O.make_frame(consts_for(w, h, pose), landscape=O.LANDSCAPES[land], aa=aa, max_steps=ms)
+    for spec in FRAMES:
+        land, pose, w, h, aa, ms, ao = unpack(spec)
+        fr = O.make_frame(consts_for(w, h, pose), landscape=O.LANDSCAPES[land], aa=aa, max_steps=ms, ao=ao)
         r = O.render(nz, fr)
-        key = frame_key(land, pose, w, h, aa, ms)
+        key = frame_key(land, pose, w, h, aa, ms, ao)
         out[key + "_rgba32f"] = r["rgba32f"]
         out[key + "_rgba8"] = r["rgba8"]
         out[key + "_steps"] = r["primary_steps"]
@@ -74,7 +84,8 @@ def main():
         out[key + "_cell_distance"] = r["cell_distance"]
         s = r["stats"]
         out[key + "_stats"] = np.array([s["noise3d_calls"], s["prepass_steps"], s["primary_steps"],
-                                        s["shadow_steps"], s["primary_rays"], s["primary_hits"]], np.uint64)
+                                        s["shadow_steps"], s["primary_rays"], s["primary_hits"], s["ao_steps"]],
+                                       np.uint64)
         print(key, s)
     np.savez_compressed(os.path.join(HERE, "oracle_frames.npz"), **out)
 

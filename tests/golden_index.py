@@ -7,7 +7,7 @@ import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
-FRAMES = [  # (landscape, pose, W, H, aa, max_steps) -- keep in sync with make_golden.py
+FRAMES = [  # (landscape, pose, W, H, aa, max_steps[, ao_samples]) -- keep in sync with make_golden.py
     ("nomadplains", "reset", 64, 48, 1, 0),
     ("nomadplains", "lookdown", 64, 48, 1, 0),
     ("nomadplains", "reset", 48, 32, 4, 0),
@@ -16,13 +16,22 @@ FRAMES = [  # (landscape, pose, W, H, aa, max_steps) -- keep in sync with make_g
     ("testing", "lookdown", 64, 48, 1, 0),
     ("simple", "reset", 48, 32, 1, 0),
     ("greenrocks", "reset", 48, 32, 1, 0),
+    # AO build extension (BASELINE configs C3/C5): (..., ao_samples)
+    ("nomadplains", "reset", 64, 48, 1, 0, 1),
+    ("nomadplains", "lookdown", 48, 32, 1, 512, 4),
+    ("greenrocks", "reset", 48, 32, 2, 0, 2),
 ]
 
 _cache = {}
 
 
-def frame_key(land, pose, w, h, aa, ms):
-    return f"{land}_{pose}_{w}x{h}_aa{aa}_ms{ms}"
+def frame_key(land, pose, w, h, aa, ms, ao=0):
+    return f"{land}_{pose}_{w}x{h}_aa{aa}_ms{ms}" + (f"_ao{ao}" if ao else "")
+
+
+def unpack(spec):
+    """(landscape, pose, W, H, aa, max_steps[, ao_samples]) -> 7-tuple"""
+    return tuple(spec) + (0,) * (7 - len(spec))
 
 
 def load():

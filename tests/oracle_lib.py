@@ -28,12 +28,13 @@ class Frame(C.Structure):
         ("recording", C.c_int32), ("max_steps", C.c_int32), ("eye", C.c_float * 4),
         ("view_inverse", C.c_float * 16), ("projection", C.c_float * 16), ("sun", C.c_float * 3),
         ("row_begin", C.c_int32), ("row_end", C.c_int32), ("row_step", C.c_int32), ("threads", C.c_int32),
+        ("ao_samples", C.c_int32),
     ]
 
 
 class Stats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("noise3d_calls", "prepass_steps", "primary_steps", "shadow_steps",
-                                          "primary_rays", "primary_hits", "density_calls")]
+                                          "primary_rays", "primary_hits", "density_calls", "ao_steps", "ao_rays")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -109,7 +110,7 @@ def noise3d(nz, xyz):
     return out
 
 
-def make_frame(consts, landscape=NOMADPLAINS, aa=1, recording=0, max_steps=0, rows=None, threads=0):
+def make_frame(consts, landscape=NOMADPLAINS, aa=1, recording=0, max_steps=0, rows=None, threads=0, ao=0):
     """consts: dict with width, height, eye(4), view_inverse(16), projection(16), sun(3) (HLSL matrices)."""
     fr = Frame()
     fr.width, fr.height = int(consts["width"]), int(consts["height"])
@@ -122,6 +123,7 @@ def make_frame(consts, landscape=NOMADPLAINS, aa=1, recording=0, max_steps=0, ro
         rows = (0, fr.height, 1)
     fr.row_begin, fr.row_end, fr.row_step = rows
     fr.threads = threads
+    fr.ao_samples = ao
     return fr
 
 

@@ -31,14 +31,14 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         pipeline="split"):
+         pipeline="split", ao=0):
     import gpgpuraytrace_amd as G
     os.environ["RT_PIPELINE"] = pipeline
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
                                     stats=stats)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
-                    rand_kind=rand_kind)
+                    rand_kind=rand_kind, ao_samples=ao)
     ter.create()
     assert ter.reload(), G.lib().rt_last_error()
     ter.set_camera(FixedCamera(consts))
@@ -128,18 +128,18 @@ def test_density_bitexact(land):
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_frame_bitexact_device_path(spec, pipeline):
     gold = GI.load()
-    land, pose, w, h, aa, ms = spec
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True, pipeline=pipeline)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True, pipeline=pipeline, ao=ao)
     ter.render_device()
     dev.present()
     img, img8 = dev.readback_float(), dev.readback()
     st = dev.stats()
     assert bits_equal(img, gold[key + "_rgba32f"])
     assert np.array_equal(img8, gold[key + "_rgba8"])
-    ref = gold[key + "_stats"]  # noise3d, prepass, primary, shadow, rays, hits
-    assert (st["noise_calls"], st["prepass_steps"], st["primary_steps"], st["shadow_steps"], st["hits"]) == \
-        (ref[0], ref[1], ref[2], ref[3], ref[5])
+    ref = gold[key + "_stats"]  # noise3d, prepass, primary, shadow, rays, hits, ao
+    assert (st["noise_calls"], st["prepass_steps"], st["primary_steps"], st["shadow_steps"], st["hits"],
+            st["ao_steps"]) == (ref[0], ref[1], ref[2], ref[3], ref[5], ref[6])
     assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
     dev.destroy()
 
@@ -161,9 +161,9 @@ def test_frame_bitexact_reference_call_sequence(spec):
     """Terrain::render's own sequence: run(2,2,1) -> CameraResults map/unmap -> host
     setTargetDepths -> CellDistance write -> per-tile ThreadOffset write + run + flush."""
     gold = GI.load()
-    land, pose, w, h, aa, ms = spec
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, ao=ao)
     ter.render()
     dev.present()
     assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])

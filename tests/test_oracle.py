@@ -208,9 +208,9 @@ def test_testing_landscape_prepass_hits_surface():
 def test_oracle_frames_regression(spec):
     import golden_index as GI
     gold = GI.load()
-    land, pose, w, h, aa, ms = spec
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    fr = O.make_frame(GI.consts(w, h, pose), landscape=O.LANDSCAPES[land], aa=aa, max_steps=ms)
+    fr = O.make_frame(GI.consts(w, h, pose), landscape=O.LANDSCAPES[land], aa=aa, max_steps=ms, ao=ao)
     r = O.render(O.noise_tables(), fr)
     assert np.array_equal(r["rgba32f"].view(np.uint32), gold[key + "_rgba32f"].view(np.uint32))
     assert np.array_equal(r["rgba8"], gold[key + "_rgba8"])
