@@ -2,9 +2,15 @@
 """bench.py -- Mray/s + ms/frame at 1920x1080 on 1..8 MI355X (BASELINE.json metric).
 
 A "step" is one frame of the hot path: camerarays prepass -> setTargetDepths
-(on the GPU) -> tracescreen (primary march + normal + colour + shadow march + sky)
-over the whole 1920x1080 frame, nomadplains landscape, noise seed 300 (MSVC rand),
-camera reset pose, time of day 0.3, AA 1, reference (uncapped) march.
+(on the GPU) -> tracescreen (primary march + normal + colour + shadow march + sky
+[+ AO]) over the whole frame, nomadplains landscape, noise seed 300 (MSVC rand),
+camera reset pose, time of day 0.3, AA 1.
+
+Default workload = BASELINE.json configs[2] ("C3", the config the 1920x1080 metric
+is quoted on): 1920x1080, 512-step primary cap + one shadow ray per hit + one
+"1-bounce AO" ray per hit (both build extensions; the AO
+definition is rt_shader.h ao_dir / oracle ambient_occlusion).  --config ref runs the
+reference semantics (uncapped march, no AO); c2 / c5 are the other GPU configs.
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
 scaling: the frame is fixed), each rank packs its tiles and one RCCL gather to rank 0
@@ -27,8 +33,21 @@ METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
 PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, = FP32 MFMA dense)
 PEAK_HBM_GBS = 8000.0
+# BASELINE.json configs (GPU ones): resolution, primary step cap, AO rays per hit
+CONFIGS = {
+    "c2": {"width": 1280, "height": 720, "max_steps": 256, "ao": 0,
+           "name": "C2: 1280x720, 256-step primary + 1 shadow ray"},
+    "c3": {"width": 1920, "height": 1080, "max_steps": 512, "ao": 1,
+           "name": "C3: 1920x1080, 512-step primary + shadow + 1-bounce AO"},
+    "c5": {"width": 3840, "height": 2160, "max_steps": 1024, "ao": 4,
+           "name": "C5: 3840x2160, 1024-step primary + shadow + 4 AO samples"},
+    "ref": {"width": 1920, "height": 1080, "max_steps": 0, "ao": 0,
+            "name": "1920x1080, reference semantics (uncapped march, shadow, no AO)"},
+}
+
 # what one tracescreen launch (the HIP-event-timed region) runs, per RT_PIPELINE
-TRACESCREEN_KERNELS = {"split": "tracescreen = k_order + k_primary + k_shade_pre + k_shadow + k_finish",
+TRACESCREEN_KERNELS = {"split": "tracescreen = k_order + k_trace + k_shade_pre + k_shadow + k_finish",
+                       "staged": "tracescreen = k_order + k_primary + k_shade_pre + k_shadow + k_finish",
                        "refill": "tracescreen = k_march + k_shade_pre + k_shadow + k_finish",
                        "mega": "tracescreen = k_tracescreen"}
 
@@ -38,27 +57,35 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--landscape", default="nomadplains")
     ap.add_argument("--pose", choices=["reset", "lookdown"], default="reset")
-    ap.add_argument("--max-steps", type=int, default=0, help="primary-march cap (build extension); 0 = reference")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="c3",
+                    help="BASELINE.json config preset (resolution, step cap, AO rays); explicit flags override")
+    ap.add_argument("--max-steps", type=int, default=None, help="primary-march cap (build extension); 0 = reference")
+    ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
                     help="PMC-derived HBM bytes per tracescreen launch (from rocprofv3 --pmc), if present")
-    return ap.parse_args()
+    a = ap.parse_args()
+    preset = CONFIGS[a.config]
+    for key in ("width", "height", "max_steps", "ao"):
+        if getattr(a, key) is None:
+            setattr(a, key, preset[key])
+    return a
 
 
-def cpu_baseline(consts, landscape, max_steps, row_step, threads):
+def cpu_baseline(consts, landscape, max_steps, ao, row_step, threads):
     """Oracle (scalar C restatement, OpenMP over rows) on a bounded row sample of the same frame."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
     nz = O.noise_tables()
     fr = O.make_frame(consts, landscape=O.LANDSCAPES[landscape], max_steps=max_steps,
-                      rows=(0, consts["height"], row_step), threads=threads)
+                      rows=(0, consts["height"], row_step), threads=threads, ao=ao)
     import ctypes as C
     cr = np.zeros(1024 * 4, np.float32)
     cd = np.zeros(1024 * 2, np.float32)
@@ -69,12 +96,12 @@ def cpu_baseline(consts, landscape, max_steps, row_step, threads):
     O.lib().ro_tracescreen(C.byref(nz), C.byref(fr), O._fp(cd), None, None, None, C.byref(st))
     dt = time.perf_counter() - t0
     s = st.as_dict()
-    rays = s["primary_rays"] + s["primary_hits"] + 1024
+    rays = s["primary_rays"] + s["primary_hits"] + s["ao_rays"] + 1024
     return {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads,
             "kind": "port",
             "sample": f"oracle/rt_oracle.c, prepass + rows 0::{row_step} of the {consts['width']}x{consts['height']} "
-                      f"frame ({s['primary_rays']} primary + {s['primary_hits']} shadow + 1024 prepass rays, "
-                      f"{dt:.1f} s, {threads} OpenMP threads)"}
+                      f"frame ({s['primary_rays']} primary + {s['primary_hits']} shadow + {s['ao_rays']} AO + "
+                      f"1024 prepass rays, {dt:.1f} s, {threads} OpenMP threads)"}
 
 
 def main():
@@ -100,7 +127,7 @@ def main():
         dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=local, stats=stats)
         if dev is None:
             raise RuntimeError("device create failed: " + G.lib().rt_last_error().decode())
-        ter = G.Terrain(dev, a.landscape, max_steps=a.max_steps)
+        ter = G.Terrain(dev, a.landscape, max_steps=a.max_steps, ao_samples=a.ao)
         ter.create()
         if not ter.reload():
             raise RuntimeError("shader load failed: " + G.lib().rt_last_error().decode())
@@ -124,7 +151,7 @@ def main():
     else:
         whole = full
     hits = whole["hits"]
-    rays_per_frame = W * H + hits + 1024
+    rays_per_frame = W * H + hits + hits * a.ao + 1024
     sdev.destroy()
 
     # --- timed device ---
@@ -184,7 +211,7 @@ def main():
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            key = f"{W}x{H}_{a.landscape}_{a.pose}"
+            key = f"{W}x{H}_{a.landscape}_{a.pose}_ms{a.max_steps}_ao{a.ao}"
             traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -196,12 +223,15 @@ def main():
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: procedural nomadplains terrain, noise seed 300 (MSVC rand), fixed camera",
             "config": {
-                "workload": f"{W}x{H} {a.landscape} frame ({a.pose} pose), camerarays prepass + device "
-                            f"setTargetDepths + tracescreen (primary + normal + colour + shadow + sky), "
+                "workload": f"{CONFIGS[a.config]['name'] if (W, H, a.max_steps, a.ao) == tuple(CONFIGS[a.config][k] for k in ('width', 'height', 'max_steps', 'ao')) else 'custom'}; "
+                            f"{W}x{H} {a.landscape} frame ({a.pose} pose), camerarays prepass + device "
+                            f"setTargetDepths + tracescreen (primary + normal + colour + shadow + sky"
+                            f"{f' + {a.ao} AO ray(s) per hit' if a.ao else ''}), "
                             f"{'uncapped march (reference semantics)' if a.max_steps == 0 else f'{a.max_steps}-step primary cap'}",
                 "width": W, "height": H, "landscape": a.landscape, "pose": a.pose, "aa_samples": 1,
-                "max_steps": a.max_steps, "rays_per_frame": rays_per_frame, "primary_rays": W * H,
-                "shadow_rays": hits, "prepass_rays": 1024, "hit_fraction": round(hits / (W * H), 4),
+                "max_steps": a.max_steps, "ao_samples": a.ao, "rays_per_frame": rays_per_frame, "primary_rays": W * H,
+                "shadow_rays": hits, "ao_rays": hits * a.ao, "prepass_rays": 1024,
+                "hit_fraction": round(hits / (W * H), 4),
                 "noise3d_per_frame_tracescreen": shard_noise if world == 1 else None,
                 "parallelism": "single GPU" if world == 1 else f"tile-cyclic 32x32 shards x{world} + RCCL gather",
             },
@@ -218,7 +248,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             consts = G.frame_constants(W, H, euler=euler)
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(consts, a.landscape, a.max_steps, a.cpu_row_step, threads)
+            out["cpu_baseline"] = cpu_baseline(consts, a.landscape, a.max_steps, a.ao, a.cpu_row_step, threads)
         print(json.dumps(out), flush=True)
     dev.destroy()
     if world > 1:

@@ -14,7 +14,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-TRACESCREEN = ("k_order", "k_primary", "k_shade", "k_shadow", "k_finish", "k_march")
+TRACESCREEN = ("k_order", "k_trace", "k_primary", "k_shade", "k_shadow", "k_finish", "k_march")
 
 
 def short(name):
@@ -48,7 +48,7 @@ def main(src, dst):
                     f"{float(r['TotalDurationNs']) / 1e6:.3f} |\n")
         plain = {short(r["Name"]): float(r["AverageNs"]) / 1e6 for r in rows}
         ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k)
-        f.write(f"\ntracescreen (uninstrumented k_order + k_primary + k_shade_pre + k_shadow + k_finish) avg sum: {ts:.4f} ms\n")
+        f.write(f"\ntracescreen (uninstrumented k_order + k_trace + k_shade_pre + k_shadow + k_finish) avg sum: {ts:.4f} ms\n")
         f.write(f"\nbench line of the same run:\n\n```\n{bench}\n```\n")
     m = pmc_means(src)
     with open(os.path.join(dst, "pmc.md"), "w") as f:
@@ -67,11 +67,12 @@ def main(src, dst):
             rd += cs.get("TCC_EA0_RDREQ_sum", 0.0)
             wr += cs.get("TCC_EA0_WRREQ_sum", 0.0)
     b = json.loads(bench)
-    key = f"{b['config']['width']}x{b['config']['height']}_{b['config']['landscape']}_{b['config']['pose']}"
+    cf = b["config"]
+    key = f"{cf['width']}x{cf['height']}_{cf['landscape']}_{cf['pose']}_ms{cf['max_steps']}_ao{cf.get('ao_samples', 0)}"
     tr[key] = {"hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
                "fetch_size_kib": fetch, "write_size_kib": write,
                "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
-               "kernels": "k_order + k_primary + k_shade_pre + k_shadow + k_finish (uninstrumented)",
+               "kernels": "tracescreen launch: k_order + k_trace + k_shade_pre + k_shadow + k_finish (uninstrumented)",
                "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"}
     json.dump(tr, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
     print(open(os.path.join(dst, "kernels.md")).read())
