@@ -925,8 +925,8 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 // producer's global stores (res / fin) complete (s_waitcnt) before the ring push,
 // and the consumer reads them with L1-bypassing loads from the XCD's L2.  A full
 // ring spills to the global lists, which k_shade_pre / k_shadow drain afterwards.
-constexpr uint32_t kHitRing = 1024;
-constexpr uint32_t kLongRing = 256;
+constexpr uint32_t kHitRing = 512;
+constexpr uint32_t kLongRing = 400; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
 constexpr uint32_t kLongBatch = 48; // queued long shadows that make a wave switch to them
 
 struct TraceQueues {
