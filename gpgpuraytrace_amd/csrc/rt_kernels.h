@@ -25,7 +25,7 @@ struct RtLaunch {
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
     float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
     uint32_t* hitlist;        // compacted sample ids of primary hits
-    float4* shrec;            // 4 float4 per long ray on the global list: march state + sample id + type
+    float4* shrec;            // 3 float4 per long ray on the global list: march state + sample id + type
     uint32_t long_cap;        // entries shrec holds
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension)

@@ -627,8 +627,8 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
 // are finished on the spot; the rest become long shadow rays (2..~120 steps).
 // A long ray's finishing inputs go to fin[t] (3 float4: albedo+specular rgb and
 // brightness, fcolord, rayleigh rgb and skyAmount) and its march state to a
-// 4-float4 record: (p, dist), (step, lastStep, d, iters), shadow fog, (t, -, -, -).
-constexpr uint32_t kShadowRec = 4;
+// 3-float4 record (long_pack).
+constexpr uint32_t kShadowRec = 3;
 
 // color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
 __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, float4 fog, float4 ray,
@@ -704,31 +704,33 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     return h;
 }
 
-// Long-ray record: (p, dist), (step, lastStep, d, iters), (shadow fog | AO dir, -), (t, type, -, -).
-// A shadow ray's direction is SunDirection / length(SunDirection) (tracing.hlsl:60-61) for
-// every ray; an AO ray carries its own (normalised) direction in the fog slot, since AO
-// rays march without fog.
+// Long-ray record (48 B): (p, dist), (step, lastStep, iters | type << 31, t),
+// (shadow fog | AO dir).  A shadow ray's direction is SunDirection /
+// length(SunDirection) (tracing.hlsl:60-61) for every ray; an AO ray carries its own
+// (normalised) direction in the fog slot, since AO rays march without fog.  The
+// density d is not kept: a stored ray is live, so its next step overwrites d before
+// anything reads it.
 template <int L>
 __device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t type, float4* r)
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
-    r[1] = make_float4(st.step, st.lastStep, st.d, __int_as_float(st.iters));
+    r[1] = make_float4(st.step, st.lastStep, __uint_as_float((uint32_t)st.iters | (type << 31)), __uint_as_float(t));
     if (type == RT_LONG_AO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
     else r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
-    r[3] = make_float4(__uint_as_float(t), __uint_as_float(type), 0.0f, 0.0f);
 }
 
 template <int L>
-__device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1, const float4 r2, const float4 r3,
-                                                f3 sun_dir, March<L, true>& st, uint32_t* type)
+__device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1, const float4 r2, f3 sun_dir,
+                                                March<L, true>& st, uint32_t* type)
 {
-    *type = __float_as_uint(r3.y);
+    const uint32_t it = __float_as_uint(r1.z);
+    *type = it >> 31;
     st.p = rtm::mk(r0.x, r0.y, r0.z);
     st.dist = r0.w;
     st.step = r1.x;
     st.lastStep = r1.y;
-    st.d = r1.z;
-    st.iters = __float_as_int(r1.w);
+    st.d = 0.0f;
+    st.iters = (int)(it & 0x7fffffffu);
     if (*type == RT_LONG_AO) {
         st.dir = rtm::mk(r2.x, r2.y, r2.z);
         st.f = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -738,7 +740,7 @@ __device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1
         st.f = {r2.x, r2.y, r2.z, r2.w};
         st.fog = true;
     }
-    return __float_as_uint(r3.x);
+    return __float_as_uint(r1.w);
 }
 
 // AO ray k of a shaded hit, at its start (AO extension, rt_shader.h ao_dir)
@@ -887,7 +889,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
                     const bool mine = ((idle >> lane) & 1ull) && rank < take;
                     if (mine) {
                         const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
-                        t = long_unpack(r[0], r[1], r[2], r[3], sun_dir, st, &type);
+                        t = long_unpack(r[0], r[1], r[2], sun_dir, st, &type);
                         live = true; // AO rays start live; shadow rays were live when stored
                     }
                     idle &= ~__ballot(mine);
@@ -926,8 +928,8 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 // and the consumer reads them with L1-bypassing loads from the XCD's L2.  A full
 // ring spills to the global lists, which k_shade_pre / k_shadow drain afterwards.
 constexpr uint32_t kHitRing = 512;
-constexpr uint32_t kLongRing = 400; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
-constexpr uint32_t kLongBatch = 48; // queued long shadows that make a wave switch to them
+constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
+constexpr uint32_t kLongBatch = 128; // queued long rays that make a wave switch to them
 
 struct TraceQueues {
     uint32_t lock;
@@ -970,7 +972,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
                                                 float4* __restrict__ shrec, uint32_t long_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
-                                                RtStats* stats)
+                                                RtStats* stats, uint32_t long_batch, uint32_t refill_idle)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
@@ -1031,14 +1033,14 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= kRefillIdle && vload(q.l_tail) != vload(q.l_head)) {
+            if (nidle >= refill_idle && vload(q.l_tail) != vload(q.l_head)) {
                 q_lock(&q.lock, lane);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                 if (((idle >> lane) & 1ull) && rank < take) {
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
-                    t = long_unpack(r[0], r[1], r[2], r[3], sun_dir, st, &type);
+                    t = long_unpack(r[0], r[1], r[2], sun_dir, st, &type);
                     live = true;
                 }
                 if (lane == 0) q.l_head = head + take;
@@ -1148,7 +1150,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         const uint32_t lp = vload(q.l_tail) - vload(q.l_head);
         const uint32_t hp = vload(q.h_tail) - vload(q.h_head);
         const bool drained = vload(q.drained) != 0u;
-        if (lp >= kLongBatch || (drained && lp > 0u)) {
+        if (lp >= long_batch || (drained && lp > 0u)) {
             do_shadow();
             continue;
         }
@@ -1320,6 +1322,15 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     uint32_t need = (m.n_units + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
+    // scheduler knobs of k_trace (RT_LONG_BATCH / RT_REFILL_IDLE override for experiments)
+    static const uint32_t tune_long_batch = [] {
+        const char* e = getenv("RT_LONG_BATCH");
+        return e ? (uint32_t)atoi(e) : kLongBatch;
+    }();
+    static const uint32_t tune_refill_idle = [] {
+        const char* e = getenv("RT_REFILL_IDLE");
+        return e ? (uint32_t)atoi(e) : kRefillIdle;
+    }();
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
@@ -1336,7 +1347,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         else
             hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
                                a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
-                               a.stats);
+                               a.stats, tune_long_batch, tune_refill_idle);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,

@@ -422,7 +422,7 @@ int check_texture(Shader* s)
 // colour (16 B), one primary RayResult (48 B), one hit-list slot (4 B), the
 // shading inputs of a long shadow ray (48 B) and an AO occlusion count (4 B); the
 // global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
-// (64 B each).
+// (48 B each).
 int ensure_split_buffers(rt_device dev, int aa, int ao)
 {
     size_t need = rt_split_samples(dev->width, dev->height, aa);
@@ -449,7 +449,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao)
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dev->shrec, long_need * 4 * sizeof(float4)));
+    HIP_TRY(hipMalloc(&dev->shrec, long_need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->aocc, need * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * sizeof(uint32_t)));
