@@ -930,6 +930,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 constexpr uint32_t kHitRing = 512;
 constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
 constexpr uint32_t kLongBatch = 128; // queued long rays that make a wave switch to them
+constexpr uint32_t kCompactLive = 40; // live lanes below which a dry wave hands its rays back
 
 struct TraceQueues {
     uint32_t lock;
@@ -972,7 +973,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
                                                 float4* __restrict__ shrec, uint32_t long_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
-                                                RtStats* stats, uint32_t long_batch, uint32_t refill_idle)
+                                                RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
+                                                uint32_t compact_live)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
@@ -1046,7 +1048,16 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 if (lane == 0) q.l_head = head + take;
                 q_unlock(&q.lock, lane);
             }
-            if (__ballot(live) == 0ull) return;
+            const uint64_t lv = __ballot(live);
+            if (lv == 0ull) return;
+            // The ring ran dry and few lanes are left: rather than march them on
+            // mostly empty lanes, hand them back to the ring (another wave will merge
+            // them with new rays) and go do other work, while there still is some.
+            if ((uint32_t)__popcll(lv) < compact_live && vload(q.l_tail) == vload(q.l_head) &&
+                vload(q.drained) == 0u) {
+                push_long(live, st, t, type);
+                return;
+            }
             if (live) march_step<L, true, true>(c, st);
         }
     };
@@ -1331,6 +1342,10 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         const char* e = getenv("RT_REFILL_IDLE");
         return e ? (uint32_t)atoi(e) : kRefillIdle;
     }();
+    static const uint32_t tune_compact_live = [] {
+        const char* e = getenv("RT_COMPACT_LIVE");
+        return e ? (uint32_t)atoi(e) : kCompactLive;
+    }();
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
@@ -1347,7 +1362,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         else
             hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
                                a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
-                               a.stats, tune_long_batch, tune_refill_idle);
+                               a.stats, tune_long_batch, tune_refill_idle, tune_compact_live);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
