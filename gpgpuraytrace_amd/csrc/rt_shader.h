@@ -171,6 +171,7 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 struct GroupOctaves {
     float sx, sy;  // noise-input scales of this lane's octave
     bool steep;    // this lane evaluates the steep noise
+    uint32_t octave; // N of this lane's octave (lanes 0..16)
     float rcp[RT_NP_OCTAVES + 1];
 };
 
@@ -179,6 +180,7 @@ __device__ __forceinline__ GroupOctaves group_octaves(const Ctx& c, uint32_t j)
     GroupOctaves g;
     g.steep = j >= (uint32_t)RT_NP_OCTAVES;
     const uint32_t o = g.steep ? 1u : j + 1u;
+    g.octave = o;
     g.sx = c.k->np_scale[o];
     g.sy = c.k->np_scale_y[o];
 #pragma unroll
@@ -200,17 +202,19 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const G
         ny = p1.z * 0.007138f;
         nzz = 0.0f;
     }
+    // N = 1 .. floor(detail) in order.  A dead octave's lane contributes +0 instead of
+    // being skipped: fma(+0, w, s) == s bit for bit because s is never -0 (it starts
+    // at +0 and an exact cancellation rounds to +0), so the serial chain needs no
+    // selects: each lane zeroes its own value before the gather.
+    const int n_oct = (int)detail;
     const float n = noise3d(c.nz, nx, ny, nzz);
+    const float nl = (g.steep || (int)(g.octave) <= n_oct) ? n : 0.0f;
     float on[RT_NP_OCTAVES + 1];
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES + 1; ++N) on[N - 1] = __shfl(n, (int)(base + N - 1), 64);
-    // N = 1 .. floor(detail) in order.  A dead octave adds n*0 = +-0 instead of being
-    // skipped: s + (+-0) == s bit for bit because s is never -0 (it starts at +0 and
-    // an exact cancellation rounds to +0), so the chain needs no branches.
-    const int n_oct = (int)detail;
+    for (int N = 1; N <= RT_NP_OCTAVES + 1; ++N) on[N - 1] = __shfl(nl, (int)(base + N - 1), 64);
     float s = 0.0f;
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N - 1], N <= n_oct ? g.rcp[N] : 0.0f, s);
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N - 1], g.rcp[N], s);
     *octaves = (uint32_t)n_oct;
     s = rtm::pow_nonneg_flat(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((on[RT_NP_OCTAVES] - 0.2f) * 6.0f) * 7.5f;
@@ -224,7 +228,11 @@ __device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const G
     s = fma(-(t * t), floorsize, s);
     t = rtm::sat((p1.y - 22.0f) * steep);
     s = fma(-(t * t), floorsize, s);
-    s = fma(rtm::pow_nonneg_flat(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
+    // floor lift: pow(0, 1.5) == 0 exactly, so a wave whose bases are all 0 (every
+    // sample above y = 25, the common case) skips the polynomial
+    const float lb = rtm::sat((-p1.y + 10.0f) * 1.6f);
+    const float lift = __ballot(lb != 0.0f) ? rtm::pow_nonneg_flat(lb, 1.5f) : 0.0f;
+    s = fma(lift, 19.0f, s);
     return d + s;
 }
 
@@ -417,7 +425,9 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
     } else {
         const float sx = rtm::abs(rtm::min(m.d + 5.0f, 0.0f));
         float stepmult;
-        if constexpr (FLAT) stepmult = 1.0f + rtm::pow_nonneg_flat(sx, k->density_factor);
+        // pow(0, y > 0) == 0: a wave of zero bases (all samples within 5 of the
+        // surface) skips the polynomial
+        if constexpr (FLAT) stepmult = 1.0f + (__ballot(sx != 0.0f) ? rtm::pow_nonneg_flat(sx, k->density_factor) : 0.0f);
         else stepmult = 1.0f + rtm::pow_nonneg(sx, k->density_factor);
         m.step = m.step * k->step_factor;
         m.lastStep = m.step * stepmult;
