@@ -16,9 +16,16 @@ N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (str
 scaling: the frame is fixed), each rank packs its tiles and one RCCL gather to rank 0
 assembles the frame, which rank 0 unpacks into its framebuffer.
 
+Frames in flight (--frames-in-flight, default 3): the timed loop deals frames round-robin
+over D complete frame contexts, each on its own HIP stream (engine.FrameRing), so frame
+i+1's prepass and primary phase fill the CUs that frame i's ray tail leaves idle.  Every
+frame is still computed in full; value / ms_per_step are the steady-state frame rate, and
+config.frame_latency_ms is the one-frame-at-a-time time of the same frame.
+
 Prints ONE JSON line on rank 0 (driver contract), with "roofline" for the dominant
-kernel (tracescreen, timed by HIP events on its own stream) and "cpu_baseline"
-(the C oracle on a bounded row sample, rank 0 at N=1 only).
+kernel (tracescreen, timed by HIP events on its own stream in a pass with one frame in
+flight, so launches do not overlap) and "cpu_baseline" (the C oracle on a bounded row
+sample, rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -65,6 +72,8 @@ def parse():
                     help="BASELINE.json config preset (resolution, step cap, AO rays); explicit flags override")
     ap.add_argument("--max-steps", type=int, default=None, help="primary-march cap (build extension); 0 = reference")
     ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
+    ap.add_argument("--frames-in-flight", type=int, default=3,
+                    help="frame contexts (HIP streams) kept in flight; 1 = one frame at a time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -154,38 +163,39 @@ def main():
     rays_per_frame = W * H + hits + hits * a.ao + 1024
     sdev.destroy()
 
-    # --- timed device ---
-    dev, ter = make(stats=False)
-    stream = torch.cuda.current_stream()
-    dev.set_stream(stream.cuda_stream)
-    ter.update_shaders()
-    packed = None
-    gathered = None
+    # --- timed: D frames in flight (FrameRing: one full frame context + HIP stream per slot) ---
+    camera = G.Camera(W, H, euler=euler)
+    ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao)
+    packed, gathered = {}, {}
     if world > 1:
-        nb = [E.shard_bytes(dev, r, world) for r in range(world)]
+        nb = [E.shard_bytes(ring.slots[0][0], r, world) for r in range(world)]
         maxb = max(nb)
-        packed = torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}")
-        if rank == 0:
-            gathered = [torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(world)]
+        for k, (dev, _) in enumerate(ring.slots):
+            packed[k] = torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}")
+            if rank == 0:
+                gathered[k] = [torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(world)]
+        slot_streams = [torch.cuda.ExternalStream(dev.stream(), device=f"cuda:{local}") for dev, _ in ring.slots]
 
     def frame():
-        ter.render_device(rank if world > 1 else 0, world)
+        k = ring.frame % ring.depth
+        dev = ring.render(rank if world > 1 else 0, world, present=world == 1)
         if world > 1:
-            E.shard_pack(dev, rank, world, packed.data_ptr())
-            dist.gather(packed, gathered if rank == 0 else None, dst=0)
-            if rank == 0:
-                for r in range(1, world):
-                    E.shard_unpack(dev, r, world, gathered[r].data_ptr())
-        dev.present()
+            # the gather rides on this slot's stream, so the other slots' frames keep running
+            with torch.cuda.stream(slot_streams[k]):
+                E.shard_pack(dev, rank, world, packed[k].data_ptr())
+                dist.gather(packed[k], gathered[k] if rank == 0 else None, dst=0)
+                if rank == 0:
+                    for r in range(1, world):
+                        E.shard_unpack(dev, r, world, gathered[k][r].data_ptr())
+            dev.present()
 
-    for _ in range(a.warmup):
+    for _ in range(a.warmup + ring.depth):
         frame()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    G.lib().rt_device_set_profiling(dev._h, 1)
-    G.lib().rt_device_kernel_time(dev._h, None, None)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         frame()
@@ -194,14 +204,26 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    import ctypes as C
-    kms, kn = C.c_double(), C.c_int()
-    G.lib().rt_device_kernel_time(dev._h, C.byref(kms), C.byref(kn))
-    k_avg_ms = kms.value / max(1, kn.value)
+
+    # --- roofline pass: the same frames one at a time on slot 0 (launches do not overlap), HIP
+    # events around every tracescreen launch on the stream it runs on; also the frame latency ---
+    dev0, ter0 = ring.slots[0]
+    ring.set_profiling(True)
+    ring.kernel_time()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        ter0.render_device(rank if world > 1 else 0, world)
+        dev0.present()
+    dev0.synchronize()
+    latency_ms = (time.perf_counter() - t1) / a.steps * 1e3
+    kms, kn = ring.kernel_time()
+    ring.set_profiling(False)
+    k_avg_ms = kms / max(1, kn)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, latency_ms = float(t[0].item()), float(t[1].item())
 
     ms_per_frame = elapsed / a.steps * 1e3
     value = rays_per_frame * a.steps / elapsed / 1e6
@@ -234,12 +256,16 @@ def main():
                 "hit_fraction": round(hits / (W * H), 4),
                 "noise3d_per_frame_tracescreen": shard_noise if world == 1 else None,
                 "parallelism": "single GPU" if world == 1 else f"tile-cyclic 32x32 shards x{world} + RCCL gather",
+                "frames_in_flight": a.frames_in_flight,
+                "frame_latency_ms": round(latency_ms, 4),
             },
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_VECTOR_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_VECTOR_TFLOPS, 4), "traffic": traffic,
                 "kernel": TRACESCREEN_KERNELS.get(os.environ.get("RT_PIPELINE", "split"), TRACESCREEN_KERNELS["split"]),
-                "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn.value,
+                "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
+                "timing": "HIP events per launch on its stream, one frame in flight (the last "
+                          f"{kn} tracescreen launches of the run)",
                 "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per launch",
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "
                         "= FP32 dense matrix peak = 157.3 TFLOP/s",
@@ -250,7 +276,7 @@ def main():
             threads = a.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(consts, a.landscape, a.max_steps, a.ao, a.cpu_row_step, threads)
         print(json.dumps(out), flush=True)
-    dev.destroy()
+    ring.destroy()
     if world > 1:
         dist.destroy_process_group()
 

@@ -416,3 +416,70 @@ def shard_pack(device, rank, count, dst_ptr):
 
 def shard_unpack(device, rank, count, src_ptr):
     check(lib().rt_shard_unpack(device._h, rank, count, src_ptr), "shard_unpack")
+
+
+class FrameRing:
+    """Frames in flight: `depth` complete frame contexts (Device + Terrain: own constants,
+    CameraResults/CellDistance, ray buffers and framebuffer), each on its own non-blocking HIP
+    stream, with frames dealt round-robin.  This is the D3D swap chain's queued frames
+    (IDevice::present with a frame-latency queue, DeviceDirect3D.cpp:234-257) made explicit:
+    frame i+1's camerarays prepass and primary phase run on the CUs that frame i's ray tail
+    leaves idle, instead of waiting for it.  Every frame is still computed in full and
+    independently; a slot is reused only after its previous frame (i - depth) has completed on
+    that slot's stream.  depth=1 is the reference's one-frame-at-a-time behaviour."""
+
+    def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
+                 **terrain_kw):
+        self.depth, self.frame = int(depth), 0
+        self.slots = []
+        for _ in range(self.depth):
+            dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu)
+            if dev is None:
+                raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
+            ter = Terrain(dev, theme, **terrain_kw)
+            ter.create()
+            if not ter.reload():
+                raise RuntimeError("shader load failed: " + lib().rt_last_error().decode())
+            if camera is not None:
+                ter.set_camera(camera)
+            ter.set_time_of_day(time_of_day)
+            ter.update_shaders()
+            self.slots.append((dev, ter))
+
+    def next_slot(self):
+        return self.slots[self.frame % self.depth]
+
+    def render(self, shard_rank=0, shard_count=1, camera=None, present=True):
+        """Queue one frame on the next slot; returns its Device (the frame is complete once
+        that device's stream reaches this point: Device.synchronize / readback)."""
+        dev, ter = self.next_slot()
+        if camera is not None:
+            ter.set_camera(camera)
+            ter.update_terrain()
+        ter.render_device(shard_rank, shard_count)
+        if present:
+            dev.present()
+        self.frame += 1
+        return dev
+
+    def synchronize(self):
+        for dev, _ in self.slots:
+            dev.synchronize()
+
+    def set_profiling(self, on):
+        for dev, _ in self.slots:
+            check(lib().rt_device_set_profiling(dev._h, 1 if on else 0), "set_profiling")
+
+    def kernel_time(self):
+        """(total ms, launches) of tracescreen launches recorded since the last call, all slots."""
+        tot, n = 0.0, 0
+        for dev, _ in self.slots:
+            kms, kn = C.c_double(), C.c_int()
+            check(lib().rt_device_kernel_time(dev._h, C.byref(kms), C.byref(kn)), "kernel_time")
+            tot, n = tot + kms.value, n + kn.value
+        return tot, n
+
+    def destroy(self):
+        for dev, _ in self.slots:
+            dev.destroy()
+        self.slots = []

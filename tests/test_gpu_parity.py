@@ -284,3 +284,30 @@ def test_reference_error_behaviour():
     assert not cs.create("shaders", "tracescreen.hlsl", "CSMain", (16, 16, 1))  # benchmark does not compile
     G.vfs_add_path("Media/nomadplains")
     dev.destroy()
+
+
+def test_frame_ring_in_flight_bitexact():
+    """engine.FrameRing (bench.py's frames in flight): 6 frames over 3 slots, the camera switching
+    every frame while the other slots' frames are still running; each slot's last frame equals
+    the golden frame of its camera."""
+    import gpgpuraytrace_amd as G
+    os.environ["RT_PIPELINE"] = "split"
+    gold = GI.load()
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]  # nomadplains 64x48, reset / lookdown
+    cams = []
+    for spec in specs:
+        land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+        cams.append((FixedCamera(GI.consts(w, h, pose)), GI.frame_key(*spec)))
+    w, h = cams[0][0].width, cams[0][0].height
+    ring = G.FrameRing(w, h, depth=3, camera=cams[0][0])
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cams[0][0].c["sun"])
+    last = {}
+    for i in range(6):
+        cam, key = cams[i % 2]
+        dev = ring.render(camera=cam)
+        last[id(dev)] = key
+    ring.synchronize()
+    for dev, _ in ring.slots:
+        assert np.array_equal(dev.readback(), gold[last[id(dev)] + "_rgba8"]), last[id(dev)]
+    ring.destroy()
