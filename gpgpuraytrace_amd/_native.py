@@ -7,7 +7,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "librt_hip.so")
+# RT_LIB_VARIANT=trace loads the debug build with k_trace's wave timeline (make trace)
+LIB_PATH = os.path.join(HERE, "_build", "librt_hip_trace.so" if os.environ.get("RT_LIB_VARIANT") == "trace"
+                        else "librt_hip.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "frosttrace.h")
 

@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
 // camerarays.hlsl:12-21 for nomadplains with one 32-lane group per prepass ray:
 // the prepass is 1024 sequential marches of ~350 steps, so it is bound by the
 // latency of one step, and spreading each step's 17 FBM octaves + steep noise over
-// a lane group (rts::density_nomadplains_group) shortens that chain ~4x.
+// a lane group (rts::density_nomadplains_seg<32>) shortens that chain ~4x.
 template <bool STATS>
 __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __restrict__ k,
                                                           const uint32_t* __restrict__ perm2d,
@@ -111,7 +111,7 @@ __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __rest
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
     Ctx c = make_ctx(k, lds);
     const uint32_t j = threadIdx.x & 31u, base = threadIdx.x & 32u;
-    const GroupOctaves g = group_octaves(c, j);
+    const SegOctaves<32> g = seg_octaves<32>(c, j);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
     const float r31 = rtm::rcp(31.0f);
     uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __rest
     while (march_live<L, false, true>(c, st, RT_CAMERA_FAR, 0)) {
         auto dens = [&](f3 q) {
             uint32_t used;
-            float d = density_nomadplains_group(c, g, q, base, &used);
+            float d = density_nomadplains_seg<32>(c, g, q, j, base, &used);
             noise += used + 1u;
             return d;
         };
@@ -368,6 +368,12 @@ __device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane,
 }
 
 // Per-sample RayResult of the primary march: 3 float4 (pd, fcolord, density).
+// the unit index a wave takes first: wave-slot-major over the grid, see k_trace
+__device__ __forceinline__ uint32_t first_unit_index()
+{
+    return (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+}
+
 __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t t, const RayResult& rr)
 {
     res[3u * t + 0u] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
@@ -565,8 +571,9 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
     const int max_steps = k->max_steps;
     float psteps = 0.0f;
     uint32_t nhits = 0;
-    for (;;) {
-        const uint32_t q = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+    const uint32_t n_static = gridDim.x * (blockDim.x >> 6); // first unit dealt statically (k_trace)
+    for (bool first = true;; first = false) {
+        const uint32_t q = first ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
         if (q >= m.n_units) break;
         const uint32_t u = __builtin_amdgcn_readfirstlane(order[q >> 4]) * 16u + (q & 15u);
         uint32_t px, py;
@@ -965,6 +972,119 @@ __device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
     if (lane == 0) atomicExch(lock, 0u);
 }
 
+// ---------------------------------------------------------------------------
+// Octave-parallel tail (nomadplains).  A wave left with a few live rays would march them
+// on a few of its 64 lanes, one full FBM per lane per step, its LDS latency exposed: the
+// frame's last rays then set its length (and, on N GPUs, every rank's).  seg_finish
+// instead re-packs the live rays into segments of LPR lanes (16 rays x 4 lanes, 8 x 8,
+// 4 x 16, 2 x 32) that each march one ray with its octaves spread over the segment
+// (density_nomadplains_seg: the same fma chain in octave order, so every state bit is what
+// the single-lane march gives).  A phase runs until half its rays are done, hands the
+// states back to the owning lanes, and the survivors re-pack twice as wide.
+constexpr uint32_t kSegLive = 16; // live rays at or below which a wave switches to segment form
+
+template <int L, bool CF>
+__device__ __forceinline__ void march_shfl(March<L, CF>& d, const March<L, CF>& s, uint32_t src)
+{
+    auto f = [&](float x) { return __shfl(x, (int)src, 64); };
+    d.p = rtm::mk(f(s.p.x), f(s.p.y), f(s.p.z));
+    d.dir = rtm::mk(f(s.dir.x), f(s.dir.y), f(s.dir.z));
+    d.rayp = rtm::mk(f(s.rayp.x), f(s.rayp.y), f(s.rayp.z));
+    d.dist = f(s.dist);
+    d.step = f(s.step);
+    d.lastStep = f(s.lastStep);
+    d.d = f(s.d);
+    d.f = {f(s.f.x), f(s.f.y), f(s.f.z), f(s.f.w)};
+    d.iters = __shfl(s.iters, (int)src, 64);
+    d.fog = __shfl(s.fog ? 1 : 0, (int)src, 64) != 0;
+}
+
+// One phase at width LPR: segment k marches the k-th live ray (<= 64/LPR of them) until
+// at most `stop` segments are still live, then the states go back to their owners.
+template <int LPR, bool SKIPREFINE>
+__device__ __forceinline__ void seg_phase(const Ctx& c, March<RT_NOMADPLAINS, true>& st, bool& live, float enddist,
+                                          int max_steps, uint32_t lane, uint32_t stop, uint32_t& own)
+{
+    constexpr int L = RT_NOMADPLAINS;
+    const uint32_t seg = lane / LPR, j = lane % LPR, base = seg * LPR;
+    const uint64_t lb = __ballot(live);
+    const uint32_t n = (uint32_t)__popcll(lb);
+    uint32_t owner = 0;
+    {
+        uint64_t b = lb;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t o = (uint32_t)__builtin_ctzll(b);
+            b &= b - 1ull;
+            owner = k == seg ? o : owner;
+        }
+    }
+    March<L, true> gs;
+    march_shfl(gs, st, owner);
+    const float ge = __shfl(enddist, (int)owner, 64);
+    const int gm = __shfl(max_steps, (int)owner, 64);
+    const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
+    uint32_t cnt = 0;
+    bool glive = seg < n;
+    for (;;) {
+        glive = glive && march_live<L, true, SKIPREFINE>(c, gs, ge, gm);
+        if ((uint32_t)__popcll(__ballot(glive)) <= stop * LPR) break;
+        if (glive) {
+            auto dens = [&](f3 q) {
+                uint32_t used;
+                const float d = density_nomadplains_seg<LPR>(c, g, q, j, base, &used);
+                cnt += used + 1u;
+                return d;
+            };
+            march_step_with<L, true, SKIPREFINE, decltype(dens), true>(c, gs, dens);
+        }
+    }
+    // owner of rank r takes segment r's first lane
+    const bool mine = (lb >> lane) & 1ull;
+    const uint32_t src = mine ? (uint32_t)__popcll(lb & ((1ull << lane) - 1ull)) * LPR : lane;
+    March<L, true> back;
+    march_shfl(back, gs, src);
+    const bool bl = __shfl(glive ? 1 : 0, (int)src, 64) != 0;
+    const uint32_t bc = (uint32_t)__shfl((int)cnt, (int)src, 64);
+    if (mine) {
+        st = back;
+        live = bl;
+        own += bc;
+    }
+}
+
+// Finish every live ray of the wave (the caller checked there are at most kSegLive) in
+// segment form.  enddist/max_steps are the lane's own (shadow and AO rays differ); all
+// lanes must be active.  On return each owning lane's st is the final state of its ray.
+template <bool SKIPREFINE>
+__device__ __forceinline__ void seg_finish(const Ctx& c, March<RT_NOMADPLAINS, true>& st, bool live, float enddist,
+                                           int max_steps, uint32_t lane)
+{
+    const uint32_t calls0 = c.nz.calls;
+    uint32_t own = 0; // noise3d of this lane's own ray (STATS)
+    __builtin_amdgcn_s_setprio(3);
+    for (;;) {
+        const uint32_t n = (uint32_t)__popcll(__ballot(live));
+        if (n == 0u) break;
+        if (n > 8u) seg_phase<4, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
+        else if (n > 4u) seg_phase<8, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
+        else if (n > 2u) seg_phase<16, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
+        else seg_phase<32, SKIPREFINE>(c, st, live, enddist, max_steps, lane, 0u, own);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    c.nz.calls = calls0 + own;
+}
+
+// Debug build only (make trace, -DRT_WAVE_TRACE): per-wave timeline of k_trace for
+// scheduler studies (scripts/wave_trace.py).  RT_WT_FIELDS u64 per wave slot.
+#ifdef RT_WAVE_TRACE
+#define RT_WT_FIELDS 18
+#define RT_WT_MAX_WAVES 8192
+__device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
+#define WT(...) __VA_ARGS__
+#else
+#define WT(...)
+#endif
+
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad, const float2* __restrict__ cells,
@@ -974,7 +1094,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 float4* __restrict__ shrec, uint32_t long_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live)
+                                                uint32_t compact_live, uint32_t seg_live)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
@@ -997,6 +1117,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
     uint32_t nhits = 0;
 
+    // wt: begin, end, t_unit, t_shade, t_long, n_unit, n_shade, n_long, last unit end, t_idle, hw_id, xcc_id,
+    // loop iterations, long rays finished (lane), max long-ray iters (lane), last iteration, max primary iters (lane)
+    WT(unsigned long long wt[RT_WT_FIELDS] = {}; wt[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+       wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or
     // to the global list when the ring is full
     auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t type) {
@@ -1027,6 +1151,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         for (;;) {
             if (live && !march_live<L, true, true>(c, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
                 long_finish<L, true>(k, fin, samples, aocc, t, type, st);
+                WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 live = false;
                 if constexpr (STATS) {
                     if (type == RT_LONG_AO) aosteps += (float)st.iters;
@@ -1057,6 +1182,13 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 vload(q.drained) == 0u) {
                 push_long(live, st, t, type);
                 return;
+            }
+            if constexpr (L == RT_NOMADPLAINS) {
+                // drained, nothing queued and only a few rays left: finish them in group form
+                if ((uint32_t)__popcll(lv) <= seg_live && vload(q.l_tail) == vload(q.l_head)) {
+                    seg_finish<true>(c, st, live, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0, lane);
+                    continue;
+                }
             }
             if (live) march_step<L, true, true>(c, st);
         }
@@ -1123,7 +1255,14 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             __builtin_amdgcn_s_setprio(0);
             for (uint32_t it = 0;; ++it) {
                 lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
-                if (__ballot(lv) == 0ull) break;
+                const uint64_t lb = __ballot(lv);
+                if (lb == 0ull) break;
+                if constexpr (L == RT_NOMADPLAINS) {
+                    if ((uint32_t)__popcll(lb) <= seg_live) {
+                        seg_finish<false>(c, st, lv, RT_CAMERA_FAR, max_steps, lane);
+                        break;
+                    }
+                }
                 if (lv) march_step<L, true, false>(c, st);
                 if (it == 96u) __builtin_amdgcn_s_setprio(1);
                 else if (it == 224u) __builtin_amdgcn_s_setprio(2);
@@ -1131,6 +1270,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             }
             __builtin_amdgcn_s_setprio(0);
             const bool hit = valid && st.d > 0.0f;
+            WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
+            WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
             if (valid) {
                 RayResult rr = march_result(st);
                 store_ray(res, t, rr);
@@ -1157,32 +1298,60 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         }
     };
 
+    // First unit of every wave is dealt statically, wave-slot-major (wave w of block b takes
+    // order index w * blocks + b): the costliest units (k_order puts them first) land one per
+    // SIMD instead of filling the first few CUs' SIMDs four deep, which sets the frame time
+    // when there are barely more units than waves (an 8-way shard has ~4k units for 4k waves).
+    const uint32_t n_static = gridDim.x * (blockDim.x >> 6);
+    bool first_unit = true;
+    WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
         const uint32_t lp = vload(q.l_tail) - vload(q.l_head);
         const uint32_t hp = vload(q.h_tail) - vload(q.h_head);
         const bool drained = vload(q.drained) != 0u;
+        WT(const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); wt[12]++;
+           wt[15] = t0;)
         if (lp >= long_batch || (drained && lp > 0u)) {
             do_shadow();
+            WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
             continue;
         }
         if (hp >= 64u || (drained && hp > 0u)) {
             if (lane == 0) atomicAdd(&q.active, 1u);
             do_shade();
             if (lane == 0) atomicSub(&q.active, 1u);
+            WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }
-        if (!drained) {
+        if (!drained || first_unit) { // a wave's static first unit is taken even after the queue drained
             if (lane == 0) atomicAdd(&q.active, 1u);
-            const uint32_t qi = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
-            if (qi < m.n_units) do_unit(__builtin_amdgcn_readfirstlane(order[qi >> 4]) * 16u + (qi & 15u));
-            else if (lane == 0) q.drained = 1u;
+            const uint32_t qi = first_unit ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+            first_unit = false;
+            if (qi < m.n_units) {
+                do_unit(__builtin_amdgcn_readfirstlane(order[qi >> 4]) * 16u + (qi & 15u));
+                WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
+            } else if (lane == 0) q.drained = 1u;
             if (lane == 0) atomicSub(&q.active, 1u);
             continue;
         }
         // drained and nothing queued: leave once no wave of the block can still push
         if (vload(q.active) == 0u && vload(q.l_tail) == vload(q.l_head) && vload(q.h_tail) == vload(q.h_head)) break;
         __builtin_amdgcn_s_sleep(2);
+        WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
     }
+    WT(wt[1] = __builtin_amdgcn_s_memrealtime();
+       for (int o = 32; o >= 1; o >>= 1) {
+           wl_rays += __shfl_xor(wl_rays, o, 64);
+           wl_maxit = max(wl_maxit, (uint32_t)__shfl_xor(wl_maxit, o, 64));
+           wp_maxit = max(wp_maxit, (uint32_t)__shfl_xor(wp_maxit, o, 64));
+       }
+       wt[13] = wl_rays; wt[14] = wl_maxit; wt[16] = wp_maxit;
+       const uint32_t slot = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+       if (lane < RT_WT_FIELDS && slot < RT_WT_MAX_WAVES) {
+           unsigned long long v = 0;
+           for (int f = 0; f < RT_WT_FIELDS; ++f) v = (lane == (uint32_t)f) ? wt[f] : v;
+           g_wave_trace[slot * RT_WT_FIELDS + lane] = v;
+       })
     if constexpr (STATS) {
         atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
@@ -1346,6 +1515,11 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         const char* e = getenv("RT_COMPACT_LIVE");
         return e ? (uint32_t)atoi(e) : kCompactLive;
     }();
+    static const uint32_t tune_seg_live = [] {
+        const char* e = getenv("RT_SEG_LIVE");
+        const uint32_t v = e ? (uint32_t)atoi(e) : kSegLive;
+        return v < kSegLive ? v : kSegLive; // seg_finish packs at most 16 rays (4 lanes each)
+    }();
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
@@ -1362,7 +1536,7 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         else
             hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
                                a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
-                               a.stats, tune_long_batch, tune_refill_idle, tune_compact_live);
+                               a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
@@ -1479,3 +1653,14 @@ void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int 
     default: hipLaunchKernelGGL(k_debug_noise<RT_NOMADPLAINS>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
     }
 }
+
+#ifdef RT_WAVE_TRACE
+// copies the last k_trace launch's per-wave timeline (RT_WT_FIELDS u64 per wave slot)
+extern "C" int rt_debug_wave_trace(unsigned long long* out, int max_waves)
+{
+    const int n = max_waves < RT_WT_MAX_WAVES ? max_waves : RT_WT_MAX_WAVES;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_trace), (size_t)n * RT_WT_FIELDS * 8) != hipSuccess) return -1;
+    return RT_WT_FIELDS;
+}
+#endif

@@ -159,65 +159,79 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     return d + s;
 }
 
-// density_nomadplains with the FBM spread over a 32-lane group that marches ONE ray
-// (latency-bound passes: the camerarays prepass has 1024 rays for 256 CUs).  Lane
-// j < 17 evaluates octave N = j+1, lane 17 the steep noise; the octave sum is then
-// gathered in N order with the same fma chain, so the value is bit-identical to
-// density_nomadplains.  `base` = first lane of the group within the wave.  Every
-// lane of the group must be active (the gathers read all of them).
-// Per-lane constants of the group form, loaded once per kernel: this lane's octave
-// scales (lane j < 17: octave j+1; the steep-noise lane takes its own constants) and
-// the octave weights 1/S (uniform).
-struct GroupOctaves {
-    float sx, sy;  // noise-input scales of this lane's octave
-    bool steep;    // this lane evaluates the steep noise
-    uint32_t octave; // N of this lane's octave (lanes 0..16)
-    float rcp[RT_NP_OCTAVES + 1];
+// density_nomadplains with the FBM spread over a segment of LPR lanes that march ONE
+// ray together (latency-bound passes: the camerarays prepass has 1024 rays for 256 CUs;
+// the last rays of a k_trace wave).  The 18 noise values of a sample are numbered
+// v = 0 (the steep noise) and v = N (octave N = 1..17); lane j of the segment evaluates
+// v = j, j + LPR, j + 2 LPR, ... (rounds), then every lane gathers the values in v order
+// and runs the same fma chain, so the result is bit-identical to density_nomadplains.
+// `base` = first lane of the segment within the wave; every lane of a segment must be
+// active (the gathers read all of them).
+template <int LPR>
+struct SegOctaves {
+    static constexpr int NV = RT_NP_OCTAVES + 1;   // values per sample
+    static constexpr int R = (NV + LPR - 1) / LPR; // rounds per lane
+    float sx[R], sy[R];                            // noise-input scales of this lane's values
+    float rcp[RT_NP_OCTAVES + 1];                  // octave weights 1/S (uniform)
 };
 
-__device__ __forceinline__ GroupOctaves group_octaves(const Ctx& c, uint32_t j)
+template <int LPR>
+__device__ __forceinline__ SegOctaves<LPR> seg_octaves(const Ctx& c, uint32_t j)
 {
-    GroupOctaves g;
-    g.steep = j >= (uint32_t)RT_NP_OCTAVES;
-    const uint32_t o = g.steep ? 1u : j + 1u;
-    g.octave = o;
-    g.sx = c.k->np_scale[o];
-    g.sy = c.k->np_scale_y[o];
+    SegOctaves<LPR> g;
+#pragma unroll
+    for (int r = 0; r < SegOctaves<LPR>::R; ++r) {
+        const uint32_t v = (uint32_t)(r * LPR) + j;
+        const uint32_t o = v >= 1u && v <= (uint32_t)RT_NP_OCTAVES ? v : 1u;
+        g.sx[r] = c.k->np_scale[o];
+        g.sy[r] = c.k->np_scale_y[o];
+    }
 #pragma unroll
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) g.rcp[N] = c.k->np_rcp[N];
     return g;
 }
 
-__device__ __forceinline__ float density_nomadplains_group(const Ctx& c, const GroupOctaves& g, f3 p, uint32_t base,
-                                                           uint32_t* octaves)
+template <int LPR>
+__device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const SegOctaves<LPR>& g, f3 p, uint32_t j,
+                                                         uint32_t base, uint32_t* octaves)
 {
+    constexpr int NV = SegOctaves<LPR>::NV, R = SegOctaves<LPR>::R;
     float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
     float d = -p.y;
     f3 p1 = rtm::scale(p, 0.4f);
     float detail = rtm::max(18.0f - rtm::pow_nonneg_flat(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
-    float nx = q0.x * g.sx, ny = q0.y * g.sy, nzz = q0.z * g.sx;
-    if (g.steep) {
-        nx = p1.x * 0.007138f;
-        ny = p1.z * 0.007138f;
-        nzz = 0.0f;
-    }
-    // N = 1 .. floor(detail) in order.  A dead octave's lane contributes +0 instead of
-    // being skipped: fma(+0, w, s) == s bit for bit because s is never -0 (it starts
-    // at +0 and an exact cancellation rounds to +0), so the serial chain needs no
-    // selects: each lane zeroes its own value before the gather.
+    // N = 1 .. floor(detail) in order.  A dead octave's value is +0 instead of being
+    // skipped: fma(+0, w, s) == s bit for bit because s is never -0 (it starts at +0 and
+    // an exact cancellation rounds to +0), so the serial chain needs no selects.  A round
+    // no lane of the wave needs (all its octaves dead) is not evaluated at all.
     const int n_oct = (int)detail;
-    const float n = noise3d(c.nz, nx, ny, nzz);
-    const float nl = (g.steep || (int)(g.octave) <= n_oct) ? n : 0.0f;
-    float on[RT_NP_OCTAVES + 1];
+    float nv[R];
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES + 1; ++N) on[N - 1] = __shfl(nl, (int)(base + N - 1), 64);
+    for (int r = 0; r < R; ++r) {
+        const uint32_t v = (uint32_t)(r * LPR) + j;
+        const bool need = v < (uint32_t)NV && (v == 0u || (int)v <= n_oct);
+        float n = 0.0f;
+        if (__ballot(need)) {
+            float nx = q0.x * g.sx[r], ny = q0.y * g.sy[r], nzz = q0.z * g.sx[r];
+            if (r == 0 && v == 0u) {
+                nx = p1.x * 0.007138f;
+                ny = p1.z * 0.007138f;
+                nzz = 0.0f;
+            }
+            n = noise3d_raw(c.nz, nx, ny, nzz);
+        }
+        nv[r] = need ? n : 0.0f;
+    }
+    float on[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) on[v] = __shfl(nv[v / LPR], (int)(base + (uint32_t)(v % LPR)), 64);
     float s = 0.0f;
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N - 1], g.rcp[N], s);
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N], g.rcp[N], s);
     *octaves = (uint32_t)n_oct;
     s = rtm::pow_nonneg_flat(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
-    float steep = rtm::sat((on[RT_NP_OCTAVES] - 0.2f) * 6.0f) * 7.5f;
+    float steep = rtm::sat((on[0] - 0.2f) * 6.0f) * 7.5f;
     float floorsize = steep * 1.8f;
     float t;
     t = rtm::sat((p1.y - 13.0f) * steep);

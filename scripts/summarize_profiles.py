@@ -50,6 +50,35 @@ def main(src, dst):
         ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k)
         f.write(f"\ntracescreen (uninstrumented k_order + k_trace + k_shade_pre + k_shadow + k_finish) avg sum: {ts:.4f} ms\n")
         f.write(f"\nbench line of the same run:\n\n```\n{bench}\n```\n")
+    # the bench's roofline pass = its last K tracescreen launches (one frame in flight): per-kernel
+    # means and the launch span (k_order start -> k_finish end) over exactly those dispatches
+    kt = glob.glob(os.path.join(src, "kt", "**", "*kernel_trace.csv"), recursive=True)
+    b0 = json.loads(bench)
+    K = int(b0["roofline"].get("kernel_launches", 0))
+    if kt and K:
+        disp = sorted(((short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                       for r in csv.DictReader(open(kt[0]))), key=lambda x: x[1])
+        ts_disp = [d for d in disp if any(d[0].startswith(t) for t in TRACESCREEN) and "true>" not in d[0]]
+        starts = [i for i, d in enumerate(ts_disp) if d[0].startswith(("k_order", "k_tracescreen", "k_march"))]
+        last = ts_disp[starts[-K]:] if len(starts) >= K else []
+        per = defaultdict(list)
+        for n, t0, t1 in last:
+            per[n].append((t1 - t0) / 1e6)
+        spans, cur = [], None
+        for n, t0, t1 in last:
+            if n.startswith(("k_order", "k_tracescreen", "k_march")):
+                cur = t0
+            if n.startswith(("k_finish", "k_tracescreen")) and cur is not None:
+                spans.append((t1 - cur) / 1e6)
+        with open(os.path.join(dst, "kernels.md"), "a") as f:
+            f.write(f"\n## Roofline pass: the last {K} tracescreen launches (one frame in flight)\n\n")
+            f.write("| kernel | calls | avg ms |\n|---|---:|---:|\n")
+            for n in sorted(per, key=lambda n: -sum(per[n])):
+                f.write(f"| {n} | {len(per[n])} | {sum(per[n]) / len(per[n]):.4f} |\n")
+            if spans:
+                f.write(f"\ntracescreen launch span (k_order start -> k_finish end), mean of {len(spans)}: "
+                        f"{sum(spans) / len(spans):.4f} ms; bench.py HIP-event kernel_avg_ms: "
+                        f"{b0['roofline']['kernel_avg_ms']} ms\n")
     m = pmc_means(src)
     with open(os.path.join(dst, "pmc.md"), "w") as f:
         f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group)\n\n")

@@ -1,0 +1,79 @@
+"""k_trace per-wave timeline (debug build: make -C gpgpuraytrace_amd/csrc trace).
+
+Renders rank r of an N-way shard (default the whole frame) with the trace library and
+reports, from the last k_trace launch: the spread of wave end times, what the
+last-finishing waves spent their time on, and the per-SIMD load.
+Usage: RT_LIB_VARIANT=trace python scripts/wave_trace.py [--n 8 --rank 0]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+os.environ.setdefault("RT_LIB_VARIANT", "trace")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+F = 18
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--max-steps", type=int, default=512)
+    ap.add_argument("--ao", type=int, default=1)
+    ap.add_argument("--top", type=int, default=12)
+    a = ap.parse_args()
+    import numpy as np
+    import gpgpuraytrace_amd as G
+    W, H = 1920, 1080
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=0)
+    ter = G.Terrain(dev, "nomadplains", max_steps=a.max_steps, ao_samples=a.ao)
+    ter.create()
+    assert ter.reload()
+    ter.set_camera(G.Camera(W, H))
+    ter.set_time_of_day(0.3)
+    for _ in range(3):
+        ter.render_device(a.rank, a.n)
+    dev.synchronize()
+    L = G.lib()
+    L.rt_debug_wave_trace.argtypes = [C.c_void_p, C.c_int]
+    nw = 256 * 16
+    buf = np.zeros(nw * F, np.uint64)
+    assert L.rt_debug_wave_trace(buf.ctypes.data, nw) == F
+    t = buf.reshape(nw, F).astype(np.int64)
+    t = t[t[:, 0] > 0]
+    t0 = t[:, 0].min()
+    us = lambda x: x * 0.01  # 100 MHz realtime clock -> us
+    beg, end = us(t[:, 0] - t0), us(t[:, 1] - t0)
+    print(f"waves {len(t)}  span {end.max():.1f} us  begin spread {beg.max():.1f} us")
+    for q in (50, 90, 99, 100):
+        print(f"  end p{q}: {np.percentile(end, q):.1f} us")
+    tot = lambda c: us(t[:, c])
+    print(f"mean per wave: unit {tot(2).mean():.1f} us ({t[:, 5].mean():.2f} units), shade {tot(3).mean():.1f} us "
+          f"({t[:, 6].mean():.2f}), long {tot(4).mean():.1f} us ({t[:, 7].mean():.2f}), idle {tot(9).mean():.1f} us")
+    order = np.argsort(-end)[:a.top]
+    print("last waves: end  units(us,n)  shade(us,n)  long(us,n)  last-unit-end  idle  hw_id  xcc  iters  long-rays  "
+          "max-long-iters  max-primary-iters")
+    for i in order:
+        r = t[i]
+        print(f"  {end[i]:8.1f}  {us(r[2]):8.1f},{r[5]:3d}  {us(r[3]):8.1f},{r[6]:3d}  {us(r[4]):8.1f},{r[7]:3d}  "
+              f"{us(r[8] - t0) if r[8] else 0:8.1f}  {us(r[9]):7.1f}  {r[10]:#010x}  {r[11]}  {r[12]}  {r[13]}  "
+              f"{r[14]}  {r[16]}")
+    # per SIMD busy (unit+shade+long) from hw_id: simd [5:4], cu [11:8], sh [12], se [15:13], + xcc
+    hw = t[:, 10]
+    simd = (hw >> 4) & 3
+    key = (t[:, 11] << 16) | (((hw >> 8) & 0xFF) << 2) | simd
+    busy = tot(2) + tot(3) + tot(4)
+    sums = {}
+    for k_, b in zip(key, busy):
+        sums[k_] = sums.get(k_, 0.0) + b
+    v = np.array(list(sums.values()))
+    print(f"per-SIMD busy (sum over its waves): mean {v.mean():.1f} us  max {v.max():.1f} us  p99 {np.percentile(v, 99):.1f}")
+    # longest single activity
+    print(f"longest single unit (wave total/units, max): {(tot(2) / np.maximum(t[:, 5], 1)).max():.1f} us")
+    dev.destroy()
+
+
+if __name__ == "__main__":
+    main()
