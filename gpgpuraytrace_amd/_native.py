@@ -46,6 +46,7 @@ SIGNATURES = {
     "rt_device_synchronize": (_i, [_vp]),
     "rt_device_readback": (_i, [_vp, _vp, _sz]),
     "rt_device_readback_float": (_i, [_vp, _vp]),
+    "rt_device_readback_bgrx": (_i, [_vp, _vp, _sz]),
     "rt_device_size": (_i, [_vp, C.POINTER(_i), C.POINTER(_i)]),
     "rt_device_framebuffer": (_vp, [_vp]),
     "rt_device_stream": (_vp, [_vp]),
@@ -81,6 +82,14 @@ SIGNATURES = {
     "rt_shard_unpack": (_i, [_vp, _i, _i, _vp]),
     "rt_noise_generate": (_i, [C.c_uint32, _i, _vp, _vp]),
     "rt_terrain_set_target_depths": (_i, [_vp, _vp]),
+    "rt_recorder_create": (_i, [_vp, _i, _i, _cp, C.POINTER(_vp)]),
+    "rt_recorder_start": (_i, [_vp]),
+    "rt_recorder_stop": (_i, [_vp]),
+    "rt_recorder_is_recording": (_i, [_vp]),
+    "rt_recorder_set_frame_time": (_i, [_vp, C.c_float]),
+    "rt_recorder_write": (_i, [_vp, _vp, _i]),
+    "rt_recorder_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
+    "rt_recorder_destroy": (None, [_vp]),
     "rt_debug_math": (_i, [_vp, _i, _vp, _vp, _vp, _i]),
     "rt_debug_noise": (_i, [_vp, _vp, _vp, _i, _i]),
 }

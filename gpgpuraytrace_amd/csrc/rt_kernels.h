@@ -53,6 +53,8 @@ inline size_t rt_shard_tiles(int w, int h, int rank, int count)
     return total > (size_t)rank ? (total - (size_t)rank + (size_t)count - 1) / (size_t)count : 0;
 }
 // pack != 0: framebuffer tiles of shard `rank` -> packed (1024 px per tile); else packed -> framebuffer.
+// RGBA8 framebuffer -> BGRX rows (RecorderWinAPI::write's swizzle), dst pitch in uint32 words
+void rt_launch_bgrx(hipStream_t s, const uint32_t* fb, uint32_t* dst, int w, int h, int pitch_words);
 void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack);
 
 // diagnostics (primitive-level parity tests)

@@ -1426,6 +1426,35 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
 }
 
 // Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
+// RecorderWinAPI::write's pixel conversion (RecorderWinAPI.cpp:244-253): the R8G8B8A8
+// backbuffer DWORD dwc becomes dwc & 0xFF00 | (dwc & 0xFF) << 16 | (dwc & 0xFF0000) >> 16,
+// i.e. bytes (B, G, R, 0) = MFVideoFormat_RGB32, row y at dst + y * pitch.  One v_perm_b32
+// per pixel, 4 pixels (16 B) per thread: a pure HBM stream (read W*H*4 B, write W*H*4 B).
+__global__ void __launch_bounds__(256) k_bgrx(const uint32_t* __restrict__ fb, uint32_t* __restrict__ dst, int w,
+                                              int h, int pitch_words)
+{
+    const int quads = (w + 3) >> 2;
+    const int y = blockIdx.y;
+    for (int qx = blockIdx.x * blockDim.x + threadIdx.x; qx < quads; qx += gridDim.x * blockDim.x) {
+        const int x = qx << 2;
+        const uint32_t* src = fb + (size_t)y * w + x;
+        uint32_t* out = dst + (size_t)y * pitch_words + x;
+        // perm selector: result bytes (B, G, R, 0) from (R, G, B, A) = bytes 2, 1, 0 and constant 0 (0x0c)
+        constexpr uint32_t sel = 0x0c000102u;
+        if (x + 4 <= w && ((w & 3) == 0) && ((pitch_words & 3) == 0)) {
+            const uint4 v = *reinterpret_cast<const uint4*>(src);
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(0u, v.x, sel);
+            o.y = __builtin_amdgcn_perm(0u, v.y, sel);
+            o.z = __builtin_amdgcn_perm(0u, v.z, sel);
+            o.w = __builtin_amdgcn_perm(0u, v.w, sel);
+            *reinterpret_cast<uint4*>(out) = o;
+        } else {
+            for (int i = 0; i < 4 && x + i < w; ++i) out[i] = __builtin_amdgcn_perm(0u, src[i], sel);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, uint32_t* __restrict__ packed, int w,
                                                     int h, int rank, int count, int pack)
 {
@@ -1584,6 +1613,13 @@ void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out
     case RT_GREENROCKS: launch_split_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
     default: launch_split_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
     }
+}
+
+void rt_launch_bgrx(hipStream_t s, const uint32_t* fb, uint32_t* dst, int w, int h, int pitch_words)
+{
+    const int quads = (w + 3) / 4;
+    const int bx = (quads + 255) / 256;
+    hipLaunchKernelGGL(k_bgrx, dim3(bx, h), dim3(256), 0, s, fb, dst, w, h, pitch_words);
 }
 
 void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack)

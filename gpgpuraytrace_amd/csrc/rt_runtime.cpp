@@ -120,10 +120,16 @@ struct rt_device_s {
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
+    // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
+    uint32_t* bgrx = nullptr;
+    struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
     // children (IDevice::createCompute / createTexture); destroyed with the device
     std::vector<struct rt_compute_s*> computes;
     std::vector<struct rt_texture_s*> textures;
 };
+
+static int recorder_capture(rt_recorder r);
+static void recorder_detach(rt_recorder r);
 
 namespace {
 // bracket one tracescreen launch with a pair of events when profiling is on
@@ -539,6 +545,8 @@ void rt_device_destroy(rt_device d)
     if (d->shrec) (void)hipFree(d->shrec);
     if (d->fin) (void)hipFree(d->fin);
     if (d->aocc) (void)hipFree(d->aocc);
+    if (d->bgrx) (void)hipFree(d->bgrx);
+    if (d->recorder) recorder_detach(d->recorder); // the recorder outlives its device: it stops capturing
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -547,10 +555,13 @@ void rt_device_destroy(rt_device d)
     delete d;
 }
 
+
 int rt_device_present(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
     HIP_TRY(hipGetLastError());
+    // DeviceDirect3D.cpp:242-256: while recording, the frame goes to the recorder
+    if (d->recorder && rt_recorder_is_recording(d->recorder) == 1) return recorder_capture(d->recorder);
     return RT_OK;
 }
 
@@ -575,6 +586,27 @@ int rt_device_readback(rt_device d, void* dst, size_t row_pitch)
     if (row_pitch == 0) row_pitch = (size_t)d->width * 4;
     if (row_pitch < (size_t)d->width * 4) return fail(RT_ERR_INVALID, "row pitch smaller than a row");
     HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->fb8, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
+                             hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return RT_OK;
+}
+
+// GPU swizzle into the device BGRX buffer (rt_launch_bgrx), on the device stream
+static int device_bgrx(rt_device d)
+{
+    if (!d->bgrx) HIP_TRY(hipMalloc(&d->bgrx, (size_t)d->width * d->height * 4));
+    rt_launch_bgrx(d->stream, d->fb8, d->bgrx, d->width, d->height, d->width);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+int rt_device_readback_bgrx(rt_device d, void* dst, size_t row_pitch)
+{
+    if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
+    if (row_pitch == 0) row_pitch = (size_t)d->width * 4;
+    if (row_pitch < (size_t)d->width * 4) return fail(RT_ERR_INVALID, "row pitch smaller than a row");
+    if (int rc = device_bgrx(d)) return rc;
+    HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->bgrx, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
                              hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
     return RT_OK;
@@ -1072,4 +1104,151 @@ extern "C" int rt_debug_noise(rt_compute c, const float* xyz, float* out, int n,
     HIP_TRY(hipFree(dx));
     HIP_TRY(hipFree(dy));
     return RT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// IRecorder / RecorderWinAPI (Factories/IRecorder.h, Adapters/RecorderWinAPI.cpp) over a
+// raw-video sink: Media Foundation's WMV sink writer does not exist here, so the frames
+// are appended as raw MFVideoFormat_RGB32 (B, G, R, 0) rows to `path` (ffmpeg reads it as
+// -f rawvideo -pix_fmt bgr0 -s WxH -r <rate>) and every sample's time stamp and duration
+// (100 ns units, IMFSample::SetSampleTime/SetSampleDuration) go to `path`.txt.
+struct rt_recorder_s {
+    rt_device dev = nullptr;
+    int width = 0, height = 0, frame_rate = 0;
+    bool fixed_speed = true;
+    bool recording = false, begun = false, finalized = false;
+    std::string path;
+    FILE* video = nullptr;
+    FILE* index = nullptr;
+    uint64_t rt_start = 0, rt_duration = 0; // RecorderWinAPI::rtStart / rtDuration
+    float frame_time = 0.0f;                 // Timer::getConstant() of the frame being written
+    uint64_t frames = 0;
+    uint32_t* host = nullptr;                // pinned W*H*4 staging (swapStaging's role)
+    std::vector<uint32_t> conv;              // CPU conversion buffer of rt_recorder_write (pBuffer's role)
+    ~rt_recorder_s()
+    {
+        if (video) fclose(video);
+        if (index) fclose(index);
+        if (host) (void)hipHostFree(host);
+        if (dev && dev->recorder == this) dev->recorder = nullptr; // ~RecorderWinAPI: setRecorder(nullptr)
+    }
+};
+
+static void recorder_detach(rt_recorder r) { r->dev = nullptr; }
+
+static int recorder_sample(rt_recorder r, const uint32_t* bgrx)
+{
+    // RecorderWinAPI.cpp:264-274: fixed speed = 1/frameRate per frame, else the frame's
+    // own time in float (10000000.0f * modifier, truncated)
+    uint64_t dur = r->rt_duration;
+    if (!r->fixed_speed) dur = (uint64_t)(10000000.0f * r->frame_time);
+    const size_t n = (size_t)r->width * r->height;
+    if (fwrite(bgrx, 4, n, r->video) != n) return fail(RT_ERR_STATE, "recorder: short write to %s", r->path.c_str());
+    fprintf(r->index, "%llu %llu %llu\n", (unsigned long long)r->frames, (unsigned long long)r->rt_start,
+            (unsigned long long)dur);
+    r->rt_start += dur;
+    r->frames++;
+    return RT_OK;
+}
+
+static int recorder_capture(rt_recorder r)
+{
+    if (!r->begun || r->finalized) return fail(RT_ERR_STATE, "recorder: write outside BeginWriting/Finalize");
+    rt_device d = r->dev;
+    if (int rc = device_bgrx(d)) return rc;
+    HIP_TRY(hipMemcpyAsync(r->host, d->bgrx, (size_t)d->width * d->height * 4, hipMemcpyDeviceToHost, d->stream));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    return recorder_sample(r, r->host);
+}
+
+int rt_recorder_create(rt_device d, int frame_rate, int fixed_speed, const char* path, rt_recorder* out)
+{
+    if (!d || !out || frame_rate <= 0) return fail(RT_ERR_INVALID, "bad recorder arguments");
+    *out = nullptr;
+    auto r = std::make_unique<rt_recorder_s>();
+    r->dev = d;
+    r->width = d->width;
+    r->height = d->height;
+    r->frame_rate = frame_rate;
+    r->fixed_speed = fixed_speed != 0;
+    r->path = path && *path ? path : "output.rgb32"; // RecorderWinAPI.cpp:80 "output.wmv"
+    r->video = fopen(r->path.c_str(), "wb");
+    if (!r->video) return fail(RT_ERR_STATE, "recorder: cannot open %s", r->path.c_str());
+    r->index = fopen((r->path + ".txt").c_str(), "w");
+    if (!r->index) {
+        fclose(r->video);
+        return fail(RT_ERR_STATE, "recorder: cannot open %s.txt", r->path.c_str());
+    }
+    fprintf(r->index, "# rgb32 (B,G,R,0) %dx%d @ %d fps; frame sample_time duration (100 ns units)\n", r->width,
+            r->height, frame_rate);
+    // MFFrameRateToAverageTimePerFrame(frameRate, 1): 10^7 / rate 100-ns units (exact for 25 fps)
+    r->rt_start = 0;
+    r->rt_duration = 10000000ull / (uint64_t)frame_rate;
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipHostMalloc(&r->host, (size_t)d->width * d->height * 4));
+    d->recorder = r.get(); // RecorderWinAPI.cpp:199 setRecorder(this)
+    *out = r.release();
+    return RT_OK;
+}
+
+int rt_recorder_start(rt_recorder r)
+{
+    if (!r) return fail(RT_ERR_INVALID, "null recorder");
+    r->recording = true; // IRecorder::start
+    if (r->finalized) return fail(RT_ERR_STATE, "recorder: BeginWriting after Finalize");
+    r->begun = true;
+    return RT_OK;
+}
+
+int rt_recorder_stop(rt_recorder r)
+{
+    if (!r) return fail(RT_ERR_INVALID, "null recorder");
+    r->recording = false; // IRecorder::stop, then Finalize
+    if (!r->begun || r->finalized) return RT_OK;
+    r->finalized = true;
+    if (fflush(r->video) != 0 || fflush(r->index) != 0) return fail(RT_ERR_STATE, "recorder: flush failed");
+    return RT_OK;
+}
+
+int rt_recorder_is_recording(rt_recorder r) { return r && r->recording ? 1 : 0; }
+
+int rt_recorder_set_frame_time(rt_recorder r, float seconds)
+{
+    if (!r) return fail(RT_ERR_INVALID, "null recorder");
+    r->frame_time = seconds;
+    return RT_OK;
+}
+
+int rt_recorder_write(rt_recorder r, const void* frame, int stride)
+{
+    if (!r || !frame || stride < r->width * 4) return fail(RT_ERR_INVALID, "bad recorder write arguments");
+    if (!r->begun || r->finalized) return fail(RT_ERR_STATE, "recorder: write outside BeginWriting/Finalize");
+    // RecorderWinAPI.cpp:244-253 on host memory, as the interface receives it
+    r->conv.resize((size_t)r->width * r->height);
+    for (int y = 0; y < r->height; ++y) {
+        const uint32_t* row = reinterpret_cast<const uint32_t*>(static_cast<const char*>(frame) + (size_t)y * stride);
+        uint32_t* o = r->conv.data() + (size_t)y * r->width;
+        for (int x = 0; x < r->width; ++x) {
+            const uint32_t dwc = row[x];
+            o[x] = (dwc & 0x0000FF00u) | (dwc & 0x000000FFu) << 16 | (dwc & 0x00FF0000u) >> 16;
+        }
+    }
+    return recorder_sample(r, r->conv.data());
+}
+
+int rt_recorder_info(rt_recorder r, unsigned long long* frames, unsigned long long* next_sample_time,
+                     unsigned long long* frame_duration)
+{
+    if (!r) return fail(RT_ERR_INVALID, "null recorder");
+    if (frames) *frames = r->frames;
+    if (next_sample_time) *next_sample_time = r->rt_start;
+    if (frame_duration) *frame_duration = r->rt_duration;
+    return RT_OK;
+}
+
+void rt_recorder_destroy(rt_recorder r)
+{
+    if (!r) return;
+    if (r->recording) (void)rt_recorder_stop(r);
+    delete r;
 }

@@ -195,6 +195,13 @@ class Device:
         check(lib().rt_device_readback_float(self._h, out.ctypes.data), "readback_float")
         return out
 
+    def readback_bgrx(self):
+        """The recorder's view of the frame: (H, W) uint32 (B, G, R, 0) rows, swizzled on the GPU
+        (DeviceDirect3D.cpp:242-256 + RecorderWinAPI.cpp:244-253)."""
+        out = np.empty((self.height, self.width), np.uint32)
+        check(lib().rt_device_readback_bgrx(self._h, out.ctypes.data, self.width * 4), "readback_bgrx")
+        return out
+
     def stats(self, reset=True):
         s = _native.RtStats()
         check(lib().rt_device_stats(self._h, C.byref(s), 1 if reset else 0), "stats")
@@ -223,6 +230,62 @@ class DeviceFactory:
             return None
         d = Device(width, height, gpu, **kw)
         return d if d.create() else None
+
+
+class Recorder:
+    """IRecorder / RecorderWinAPI (Factories/IRecorder.h, Adapters/RecorderWinAPI.cpp) over the
+    raw-video sink of rt_recorder_create: frames as raw (B, G, R, 0) rows in `path`, sample time
+    stamps in `path`.txt.  Attached to its device: Device.present() writes each frame while
+    recording, as DeviceDirect3D::present does."""
+
+    def __init__(self, handle, device, path):
+        self._h, self.device, self.path = handle, device, path
+
+    def start(self):
+        check(lib().rt_recorder_start(self._h), "recorder start")
+
+    def stop(self):
+        check(lib().rt_recorder_stop(self._h), "recorder stop")
+
+    def is_recording(self):
+        return lib().rt_recorder_is_recording(self._h) == 1
+
+    def set_frame_time(self, seconds):
+        """Timer::getConstant() of the next frame (used when not fixed speed)."""
+        check(lib().rt_recorder_set_frame_time(self._h, float(seconds)), "recorder frame time")
+
+    def write(self, frame, stride=None):
+        """IRecorder::write(frame, stride) with host RGBA8 rows (an (H, W, 4) uint8 array)."""
+        a = np.ascontiguousarray(frame)
+        check(lib().rt_recorder_write(self._h, a.ctypes.data, int(stride or a.strides[0])), "recorder write")
+
+    def info(self):
+        f, t, d = C.c_ulonglong(), C.c_ulonglong(), C.c_ulonglong()
+        check(lib().rt_recorder_info(self._h, C.byref(f), C.byref(t), C.byref(d)), "recorder info")
+        return {"frames": f.value, "next_sample_time": t.value, "frame_duration": d.value}
+
+    def destroy(self):
+        if self._h:
+            lib().rt_recorder_destroy(self._h)
+            self._h = None
+
+
+class RecorderFactory:
+    @staticmethod
+    def construct(device, frame_rate, fixed_speed, path="output.rgb32"):
+        """RecorderFactory::construct (RecorderFactory.cpp:6-19): None on failure."""
+        h = C.c_void_p()
+        if lib().rt_recorder_create(device._h, int(frame_rate), 1 if fixed_speed else 0, path.encode(), C.byref(h)):
+            return None
+        return Recorder(h.value, device, path)
+
+
+def read_recording(path, width, height):
+    """(frames (F, H, W) uint32 BGRX, samples (F, 3) uint64 [frame, time, duration]) of a recording."""
+    raw = np.fromfile(path, np.uint32)
+    frames = raw.reshape(-1, height, width)
+    rows = [ln.split() for ln in open(path + ".txt") if ln.strip() and not ln.startswith("#")]
+    return frames, np.array(rows, np.uint64).reshape(-1, 3)
 
 
 class Noise:

@@ -52,6 +52,7 @@ typedef struct rt_compute_s* rt_compute;
 typedef struct rt_texture_s* rt_texture;
 typedef struct rt_variable_s* rt_variable;
 typedef struct rt_array_s* rt_array;
+typedef struct rt_recorder_s* rt_recorder;
 
 typedef struct {
     unsigned long long primary_steps; /* traceRay iterations, primary rays */
@@ -85,6 +86,10 @@ int rt_device_flush(rt_device dev);
 int rt_device_synchronize(rt_device dev);
 int rt_device_readback(rt_device dev, void* dst, size_t row_pitch);
 int rt_device_readback_float(rt_device dev, float* dst); /* W*H*4 floats, needs RT_DEVICE_FLOAT_OUTPUT */
+/* rt_device_readback_bgrx <- the recorder's readback (DeviceDirect3D.cpp:242-256) with
+ * RecorderWinAPI::write's pixel conversion (RecorderWinAPI.cpp:244-253) done on the GPU:
+ * rows of W uint32 (B, G, R, 0) = MFVideoFormat_RGB32, `row_pitch` bytes apart. */
+int rt_device_readback_bgrx(rt_device dev, void* dst, size_t row_pitch);
 int rt_device_size(rt_device dev, int* width, int* height);
 void* rt_device_framebuffer(rt_device dev);       /* device pointer, W*H uint32 RGBA8 */
 void* rt_device_stream(rt_device dev);            /* hipStream_t */
@@ -175,6 +180,29 @@ int rt_terrain_set_target_depths(const float* camera_results, float* cell_distan
  *   current tables and constants. */
 int rt_debug_math(rt_device dev, int op, const float* a, const float* b, float* out, int n);
 int rt_debug_noise(rt_compute cs, const float* xyz, float* out, int n, int density);
+
+/* ---- IRecorder (Factories/IRecorder.h; RecorderWinAPI.cpp; RecorderFactory.cpp) ----
+ * rt_recorder_create   <- RecorderFactory::construct(device, frameRate, fixedSpeed) + create():
+ *                         attaches to the device (DeviceDirect3D::setRecorder, :229-232).  The
+ *                         Media Foundation WMV sink (:80, "output.wmv") becomes a raw-video sink:
+ *                         `path` (default "output.rgb32") receives the frames as raw
+ *                         MFVideoFormat_RGB32 rows (B, G, R, 0), `path`.txt one line per sample
+ *                         "frame sample_time duration" in 100 ns units (IMFSample time stamps).
+ * rt_recorder_start    <- IRecorder::start + BeginWriting (:205-216)
+ * rt_recorder_stop     <- IRecorder::stop + Finalize (:218-224); no start after it (as the sink writer)
+ * rt_recorder_write    <- RecorderWinAPI::write(frame, stride) on host RGBA8 rows (:226-279)
+ * rt_device_present    writes the frame to an attached, recording recorder (DeviceDirect3D.cpp:242-256),
+ *                      with the swizzle on the GPU.
+ * rt_recorder_set_frame_time: Timer::getConstant() the next sample uses when !fixed_speed (:264-269). */
+int rt_recorder_create(rt_device dev, int frame_rate, int fixed_speed, const char* path, rt_recorder* out);
+int rt_recorder_start(rt_recorder rec);
+int rt_recorder_stop(rt_recorder rec);
+int rt_recorder_is_recording(rt_recorder rec);
+int rt_recorder_set_frame_time(rt_recorder rec, float seconds);
+int rt_recorder_write(rt_recorder rec, const void* frame, int stride);
+int rt_recorder_info(rt_recorder rec, unsigned long long* frames, unsigned long long* next_sample_time,
+                     unsigned long long* frame_duration);
+void rt_recorder_destroy(rt_recorder rec);
 
 #ifdef __cplusplus
 }

@@ -1001,3 +1001,32 @@ void ro_get_density_batch(const ro_noise* nz, const ro_frame* fr, const float* x
     ctx_init(&c, nz, fr);
     for (int64_t i = 0; i < n; ++i) out[i] = get_density(&c, v3(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]));
 }
+
+/* ---- output path (test infrastructure for k_bgrx / the recorder) ---- */
+/* RecorderWinAPI.cpp:244-253 */
+void ro_bgrx(const uint8_t* frame, int width, int height, int stride, uint32_t* out)
+{
+    for (int y = 0; y < height; y++) {
+        for (int x = 0; x < width; x++) {
+            uint32_t dwc;
+            memcpy(&dwc, frame + (size_t)y * stride + (size_t)x * 4, 4);
+            out[(size_t)y * width + x] = (dwc & 0x0000FF00u) | (dwc & 0x000000FFu) << 16 | (dwc & 0x00FF0000u) >> 16;
+        }
+    }
+}
+
+/* RecorderWinAPI.cpp:196-197 (rtStart = 0; rtDuration = 10^7 / frameRate for integer rates)
+ * and :264-274 (per-sample duration, rtStart += duration) */
+void ro_sample_times(int frame_rate, int fixed_speed, const float* frame_times, int n, uint64_t* sample_time,
+                     uint64_t* duration)
+{
+    const uint64_t rt_duration = 10000000ull / (uint64_t)frame_rate;
+    uint64_t rt_start = 0;
+    for (int i = 0; i < n; i++) {
+        uint64_t d = rt_duration;
+        if (!fixed_speed) d = (uint64_t)(10000000.0f * frame_times[i]);
+        sample_time[i] = rt_start;
+        duration[i] = d;
+        rt_start += d;
+    }
+}

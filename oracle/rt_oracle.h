@@ -102,6 +102,14 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
 void ro_render_frame(const ro_noise* nz, const ro_frame* fr, float* camera_results, float* cell_distance,
                      float* rgba32f, uint8_t* rgba8, float* primary_steps, ro_stats* st);
 
+/* Output path: RecorderWinAPI::write's conversion of the R8G8B8A8
+ * backbuffer rows (RecorderWinAPI.cpp:244-253) into MFVideoFormat_RGB32 DWORDs, and the
+ * sample time stamps it sets (:264-274, rtDuration from MFFrameRateToAverageTimePerFrame,
+ * :197).  frame_times[i] = Timer::getConstant() of frame i (used when !fixed_speed). */
+void ro_bgrx(const uint8_t* frame, int width, int height, int stride, uint32_t* out);
+void ro_sample_times(int frame_rate, int fixed_speed, const float* frame_times, int n, uint64_t* sample_time,
+                     uint64_t* duration);
+
 #ifdef __cplusplus
 }
 #endif

@@ -74,8 +74,27 @@ def lib():
                                      C.POINTER(Stats)]
         L.ro_render_frame.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, fp, C.POINTER(C.c_uint8), fp,
                                       C.POINTER(Stats)]
+        L.ro_bgrx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.ro_sample_times.argtypes = [C.c_int, C.c_int, fp, C.c_int, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
+
+
+def bgrx(frame):
+    """RecorderWinAPI::write's conversion of (H, W, 4) uint8 RGBA rows -> (H, W) uint32."""
+    f = np.ascontiguousarray(frame, np.uint8)
+    h, w = f.shape[:2]
+    out = np.empty((h, w), np.uint32)
+    lib().ro_bgrx(f.ctypes.data, w, h, f.strides[0], out.ctypes.data)
+    return out
+
+
+def sample_times(frame_rate, fixed_speed, frame_times):
+    ft = np.ascontiguousarray(frame_times, np.float32)
+    n = len(ft)
+    t, d = np.empty(n, np.uint64), np.empty(n, np.uint64)
+    lib().ro_sample_times(frame_rate, 1 if fixed_speed else 0, _fp(ft), n, t.ctypes.data, d.ctypes.data)
+    return t, d
 
 
 def _fp(a):

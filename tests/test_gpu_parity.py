@@ -311,3 +311,73 @@ def test_frame_ring_in_flight_bitexact():
     for dev, _ in ring.slots:
         assert np.array_equal(dev.readback(), gold[last[id(dev)] + "_rgba8"]), last[id(dev)]
     ring.destroy()
+
+
+# --- output path: GPU swizzle + recorder --------------------------
+@pytest.mark.parametrize("w,h", [(64, 48), (50, 36)])
+def test_bgrx_readback_bitexact(w, h):
+    """k_bgrx (rt_device_readback_bgrx) == RecorderWinAPI::write's conversion (oracle) of the
+    same frame's RGBA8 readback; odd widths take the per-pixel tail path."""
+    import gpgpuraytrace_amd as G
+    dev, ter = make(GI.consts(64, 48, "lookdown") if (w, h) == (64, 48) else G.frame_constants(w, h))
+    ter.render_device()
+    dev.present()
+    rgba = dev.readback()
+    got = dev.readback_bgrx()
+    assert np.array_equal(got, O.bgrx(rgba))
+    if (w, h) == (64, 48):
+        assert np.array_equal(got, O.bgrx(GI.load()[GI.frame_key(*GI.FRAMES[1]) + "_rgba8"]))
+    dev.destroy()
+
+
+def test_recorder_present_and_write(tmp_path):
+    """IRecorder over the raw-video sink: present() while recording writes the GPU-swizzled frame
+    with RecorderWinAPI's sample time stamps; write() on host rows gives the same bytes; nothing
+    is written when not recording or after Finalize."""
+    import gpgpuraytrace_amd as G
+    w, h = 64, 48
+    dev, ter = make(GI.consts(w, h, "reset"))
+    path = str(tmp_path / "out.rgb32")
+    rec = G.RecorderFactory.construct(dev, 25, True, path)
+    assert rec is not None and not rec.is_recording()
+    ter.render_device()
+    dev.present()  # not recording: no sample
+    rec.start()
+    frames = []
+    for i in range(3):
+        ter.set_time_of_day(0.3 + 0.05 * i)
+        ter.render_device()
+        dev.present()
+        frames.append(dev.readback())
+    rec.write(frames[0])  # host path, fixed speed
+    info = rec.info()
+    assert info["frames"] == 4 and info["frame_duration"] == 400000
+    rec.stop()
+    assert not rec.is_recording()
+    dev.present()  # after stop: no sample
+    with pytest.raises(Exception):
+        rec.start()  # BeginWriting after Finalize
+    rec.destroy()
+    vid, samples = G.read_recording(path, w, h)
+    assert vid.shape == (4, h, w)
+    for i in range(3):
+        assert np.array_equal(vid[i], O.bgrx(frames[i]))
+    assert np.array_equal(vid[3], vid[0])
+    t, d = O.sample_times(25, True, np.zeros(4, np.float32))
+    assert samples[:, 0].tolist() == [0, 1, 2, 3]
+    assert samples[:, 1].tolist() == t.tolist() and samples[:, 2].tolist() == d.tolist()
+    # timer-driven durations (not fixed speed)
+    path2 = str(tmp_path / "out2.rgb32")
+    rec2 = G.RecorderFactory.construct(dev, 25, False, path2)
+    rec2.start()
+    fts = np.array([0.04, 0.0333333, 0.1], np.float32)
+    for ft in fts:
+        rec2.set_frame_time(ft)
+        ter.render_device()
+        dev.present()
+    rec2.stop()
+    rec2.destroy()
+    _, s2 = G.read_recording(path2, w, h)
+    t2, d2 = O.sample_times(25, False, fts)
+    assert s2[:, 1].tolist() == t2.tolist() and s2[:, 2].tolist() == d2.tolist()
+    dev.destroy()
