@@ -77,6 +77,8 @@ SIGNATURES = {
     "rt_array_stride": (_sz, [_vp]),
     "rt_array_device_pointer": (_vp, [_vp]),
     "rt_terrain_render": (_i, [_vp, _vp, _i, _i]),
+    "rt_terrain_render_feed": (_i, [_vp, _vp, _i, _i]),
+    "rt_terrain_feed_wait": (_i, [_vp, _vp]),
     "rt_shard_bytes": (_sz, [_vp, _i, _i]),
     "rt_shard_pack": (_i, [_vp, _i, _i, _vp]),
     "rt_shard_unpack": (_i, [_vp, _i, _i, _vp]),

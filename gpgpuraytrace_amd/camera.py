@@ -105,8 +105,12 @@ def cbuffer_bytes_matrix(m_hlsl):
     return np.ascontiguousarray(np.asarray(m_hlsl, np.float32).T).tobytes()
 
 
-def frame_constants(width, height, position=INITIAL_POSITION, euler=INITIAL_ROTATION_EULER, time_of_day=0.3):
-    cam = Camera(width, height, position, euler)
-    return {"width": int(width), "height": int(height), "eye": cam.eye(),
+def camera_constants(cam, time_of_day=0.3):
+    """The shader constants of a camera's current state (after Camera.update)."""
+    return {"width": cam.width, "height": cam.height, "eye": cam.eye(),
             "view_inverse": cam.view_inverse_hlsl(), "projection": cam.projection_hlsl(),
             "sun": sun_direction(time_of_day)}
+
+
+def frame_constants(width, height, position=INITIAL_POSITION, euler=INITIAL_ROTATION_EULER, time_of_day=0.3):
+    return camera_constants(Camera(width, height, position, euler), time_of_day)

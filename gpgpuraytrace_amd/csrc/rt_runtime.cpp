@@ -241,10 +241,16 @@ struct rt_compute_s {
     rt_device dev = nullptr;
     Shader* shader = nullptr;
     Shader* new_shader = nullptr;
+    // camera feed (rt_terrain_render_feed): pinned copy of CameraResults + the event after it
+    float4* feed_host = nullptr;
+    hipEvent_t feed_ev = nullptr;
+    bool feed_pending = false;
     ~rt_compute_s()
     {
         delete shader;
         delete new_shader;
+        if (feed_ev) (void)hipEventDestroy(feed_ev);
+        if (feed_host) (void)hipHostFree(feed_host);
     }
 };
 
@@ -959,7 +965,29 @@ size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
 void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
 
 // ---- Terrain::render on the device -------------------------------------------
+static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count, bool feed);
+
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
+{
+    return terrain_render(cam, scr, shard_rank, shard_count, false);
+}
+
+int rt_terrain_render_feed(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
+{
+    return terrain_render(cam, scr, shard_rank, shard_count, true);
+}
+
+int rt_terrain_feed_wait(rt_compute cam, float* camera_results)
+{
+    if (!cam || !camera_results) return fail(RT_ERR_INVALID, "bad arguments");
+    if (!cam->feed_pending) return fail(RT_ERR_STATE, "no camera feed pending (rt_terrain_render_feed)");
+    HIP_TRY(hipEventSynchronize(cam->feed_ev));
+    memcpy(camera_results, cam->feed_host, 1024 * sizeof(float4));
+    cam->feed_pending = false;
+    return RT_OK;
+}
+
+static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count, bool feed)
 {
     if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
     if (!cam->shader || !scr->shader) return fail(RT_ERR_STATE, "both computes need a current shader (swap)");
@@ -976,6 +1004,14 @@ int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_
     if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
     float4* crp = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : dev->scratch_cam;
     rt_launch_camerarays(make_launch(dev, cam->shader), crp);
+    if (feed) {
+        // Flyby's view of this frame, on the host as soon as the prepass is done
+        if (!cam->feed_host) HIP_TRY(hipHostMalloc(&cam->feed_host, 1024 * sizeof(float4)));
+        if (!cam->feed_ev) HIP_TRY(hipEventCreateWithFlags(&cam->feed_ev, hipEventDisableTiming));
+        HIP_TRY(hipMemcpyAsync(cam->feed_host, crp, 1024 * sizeof(float4), hipMemcpyDeviceToHost, dev->stream));
+        HIP_TRY(hipEventRecord(cam->feed_ev, dev->stream));
+        cam->feed_pending = true;
+    }
     rt_launch_cell_depths(dev->stream, crp, (float2*)cd->dev_ptr);
     {
         KernelTimer kt(dev);

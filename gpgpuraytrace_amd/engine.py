@@ -457,11 +457,21 @@ class Terrain:
         else:
             self.compute.run(self.dispatch_x * self.tiles_x, self.dispatch_y * self.tiles_y, 1)
 
-    def render_device(self, shard_rank=0, shard_count=1):
-        """Terrain::render with setTargetDepths on the GPU: no host round trip, all on one stream."""
+    def render_device(self, shard_rank=0, shard_count=1, feed=False):
+        """Terrain::render with setTargetDepths on the GPU: no host round trip, all on one stream.
+        feed=True also sends this frame's CameraResults to the host right after the prepass
+        (camera_feed() collects them) -- what Flyby reads, without waiting for the whole frame."""
         self.update_shaders()
-        check(lib().rt_terrain_render(self.camera_compute._h, self.compute._h, shard_rank, shard_count),
-              "terrain_render")
+        fn = lib().rt_terrain_render_feed if feed else lib().rt_terrain_render
+        check(fn(self.camera_compute._h, self.compute._h, shard_rank, shard_count), "terrain_render")
+
+    def camera_feed(self):
+        """Wait for the feed of the last render_device(feed=True); it becomes the camera view
+        (Terrain::getCameraView, Terrain.cpp:441-452) and is returned, (1024, 4) float32."""
+        out = np.empty((CAMERA_VIEW_RES * CAMERA_VIEW_RES, 4), np.float32)
+        check(lib().rt_terrain_feed_wait(self.camera_compute._h, out.ctypes.data), "camera feed")
+        self.camera_view[:] = out
+        return self.camera_view
 
 
 def _cbuffer_matrix(m):

@@ -155,6 +155,13 @@ void* rt_array_device_pointer(rt_array arr);
  * write; tiled run(...).  With shard_count > 1 only screen tiles t (32x32 pixels,
  * row-major tile index) with t % shard_count == shard_rank are traced. */
 int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
+/* rt_terrain_render_feed: rt_terrain_render that also hands the frame's 1024 CameraResults
+ * (camerarays.hlsl:12-21, Terrain::getCameraView) to the host as soon as the prepass ends,
+ * without waiting for tracescreen -- the feed of Flyby::fly (Gameplay/Flyby.cpp:26-196, which
+ * reads the previous frame's view).  rt_terrain_feed_wait blocks until that copy has landed and
+ * copies it (1024 x float4: hit xyz, depth) to `camera_results`. */
+int rt_terrain_render_feed(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
+int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
 /* Tile-cyclic shard transport: pack this rank's tiles from the framebuffer into a
  * contiguous device buffer (RGBA8, 32x32-pixel tiles in tile order), or unpack a rank's
  * packed tiles into the framebuffer.  Byte counts from rt_shard_bytes. */

@@ -381,3 +381,45 @@ def test_recorder_present_and_write(tmp_path):
     t2, d2 = O.sample_times(25, False, fts)
     assert s2[:, 1].tolist() == t2.tolist() and s2[:, 2].tolist() == d2.tolist()
     dev.destroy()
+
+
+# --- Flyby fed by the device prepass ------------------------------
+def test_fly_through_device_feed_matches_oracle_feed():
+    """Flyby steering from the GPU's CameraResults (rt_terrain_render_feed) follows exactly the
+    path it follows from the oracle's camerarays, one frame at a time and with 3 frames in flight."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import camera as CAM
+    from gpgpuraytrace_amd.flyby import Flyby, fly_through
+    os.environ["RT_PIPELINE"] = "split"
+    W, H, frames, dt = 64, 48, 6, 1.0 / 25.0
+    cam = CAM.Camera(W, H)
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H)
+    ter = G.Terrain(dev, "nomadplains")
+    ter.create()
+    assert ter.reload()
+    ter.set_camera(cam)
+    ter.set_time_of_day(0.3)
+    ter.update_shaders()
+    path_dev = fly_through(ter, cam, frames, dt)
+    dev.destroy()
+    cam2 = CAM.Camera(W, H)
+    ring = G.FrameRing(W, H, depth=3, camera=cam2)
+    path_ring = fly_through(ring, cam2, frames, dt)
+    ring.destroy()
+    nz = O.noise_tables()
+    cam3 = CAM.Camera(W, H)
+    fly = Flyby(cam3)
+    view = np.zeros((1024, 4), np.float32)
+    path = []
+    for _ in range(frames):
+        fly.fly(dt, view)
+        cam3.update()
+        path.append((cam3.position.copy(), np.asarray(cam3.front, float).copy()))
+        fr = O.make_frame(CAM.camera_constants(cam3))
+        cr = np.zeros(1024 * 4, np.float32)
+        st = O.Stats()
+        O.lib().ro_camerarays(C.byref(nz), C.byref(fr), O._fp(cr), C.byref(st))
+        view = cr.reshape(1024, 4)
+    path = np.array(path)
+    assert np.array_equal(path_dev, path)
+    assert np.array_equal(path_ring, path)
