@@ -92,6 +92,10 @@ SIGNATURES = {
     "rt_recorder_write": (_i, [_vp, _vp, _i]),
     "rt_recorder_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     "rt_recorder_destroy": (None, [_vp]),
+    "rt_varmgr_start": (_i, [_i, _cp]),
+    "rt_varmgr_stop": (_i, []),
+    "rt_varmgr_count": (_i, []),
+    "rt_varmgr_register_compute": (_i, [_vp]),
     "rt_debug_math": (_i, [_vp, _i, _vp, _vp, _vp, _i]),
     "rt_debug_noise": (_i, [_vp, _vp, _vp, _i, _i]),
 }

@@ -9,7 +9,13 @@
 // shader and invalidates its variables, exactly as the reference does.
 #include <hip/hip_runtime.h>
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -17,6 +23,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/frosttrace.h"
@@ -185,6 +192,12 @@ enum { KIND_CAMERARAYS = 0, KIND_TRACESCREEN = 1 };
 enum { CB_XTWEAK = 0, CB_FRAME = 1, CB_PERM = 2, CB_NOISE = 3, CB_DISPATCH = 4, CB_COUNT = 5 };
 static const int kCbSize[CB_COUNT] = {12, 84, 80, 2048, 8};
 
+struct Shader;
+static void varmgr_forget(Shader* s);
+static void varmgr_clear();
+static void varmgr_register(Shader* s);
+static std::mutex g_cb_mu; // cbuffer shadows: written by the live-tweak thread (VariableManager) and the API
+
 struct Shader {
     int kind = KIND_TRACESCREEN;
     int landscape = RT_NOMADPLAINS;
@@ -204,6 +217,7 @@ struct Shader {
 
     ~Shader()
     {
+        varmgr_forget(this);
         if (d_consts) (void)hipFree(d_consts);
         if (d_grad) (void)hipFree(d_grad);
         for (auto& a : arrays)
@@ -384,6 +398,7 @@ int sync_shader(rt_device dev, Shader* s)
 {
     if (!s->d_consts) HIP_TRY(hipMalloc(&s->d_consts, sizeof(RtConsts)));
     if (!s->d_grad) HIP_TRY(hipMalloc(&s->d_grad, 128 * sizeof(float4)));
+    std::lock_guard<std::mutex> lk(g_cb_mu);
     if (s->cb_dirty) {
         // cbuffer shadows -> device (ConstantBufferD3D::update on run, ShaderVariableDirect3D.cpp:59-66)
         build_consts(*s, *dev, s->host_consts);
@@ -747,6 +762,7 @@ int rt_compute_load(rt_compute c, const char* directory, const char* file, const
 {
     (void)directory;
     if (!c || !file) return fail(RT_ERR_INVALID, "bad arguments");
+    varmgr_clear(); // ComputeDirect3D.cpp:408: every create clears the live-tweak registry (and tells the client)
     if (entry && strcmp(entry, "CSMain") != 0) return fail(RT_ERR_NOT_FOUND, "entry point %s not found", entry);
     std::string f = file;
     int kind;
@@ -798,6 +814,7 @@ int rt_compute_load(rt_compute c, const char* directory, const char* file, const
     s->add_var("permGradients", CB_NOISE, 0, 2048);
     for (int i = 0; i < CB_COUNT; ++i)
         if (s->has_cb[i]) s->cb[i].assign(kCbSize[i], 0); // ConstantBufferD3D zero-fills (ShaderVariableDirect3D.cpp:10-11)
+    varmgr_register(s.get()); // ComputeDirect3D.cpp:188-197: variables of 'X' cbuffers
     delete c->new_shader;
     c->new_shader = s.release();
     return RT_OK;
@@ -903,6 +920,7 @@ int rt_variable_write(rt_variable v, const void* data)
 {
     if (!v || !data) return fail(RT_ERR_INVALID, "bad arguments");
     Shader* s = v->owner;
+    std::lock_guard<std::mutex> lk(g_cb_mu);
     memcpy(s->cb[v->cbuf].data() + v->offset, data, v->size);
     if (v->cbuf != CB_DISPATCH) s->cb_dirty = true; // ThreadOffset is a launch argument
     return RT_OK;
@@ -1288,3 +1306,213 @@ void rt_recorder_destroy(rt_recorder r)
     if (r->recording) (void)rt_recorder_stop(r);
     delete r;
 }
+
+// ---------------------------------------------------------------------------
+// VariableManager (Common/VariableManager.{h,cpp}): the live-tweak TCP protocol on a thread.
+//   server -> client: [1][nlen:1][name][tlen:1][type][size:2 LE][data]   add
+//                     [2]                                                 remove all
+//   client -> server: [nlen:1][name][data: the variable's size]          write
+// Variables are the members of cbuffers whose name starts with 'X' (XTweakable.SunDirection,
+// tracing.hlsl:6-9); a write lands in the owning shader's cbuffer shadow and marks it dirty
+// (ComputeDirect3D::onVariableChangedCallback, :212-216), so the next launch uploads it.
+// Unlike the reference (which writes the shadow from its network thread unlocked), shadow
+// writes take g_cb_mu.  bind_address defaults to the loopback interface (the reference binds
+// INADDR_ANY).
+namespace {
+struct VarEntry {
+    std::string name, type;
+    int size = 0, cbuf = 0, offset = 0;
+    Shader* owner = nullptr;
+};
+std::vector<VarEntry> g_vars; // under g_cb_mu
+std::atomic<int> g_client{-1};
+int g_listener = -1;
+std::thread g_net;
+std::atomic<bool> g_running{false};
+
+void send_all_bytes(int fd, const void* p, size_t n)
+{
+    const char* c = static_cast<const char*>(p);
+    while (n) {
+        ssize_t k = ::send(fd, c, n, MSG_NOSIGNAL);
+        if (k <= 0) return;
+        c += k;
+        n -= (size_t)k;
+    }
+}
+
+void send_variable(int fd, const VarEntry& v) // VariableManager.cpp:89-111
+{
+    std::vector<uint8_t> m;
+    m.push_back(1);
+    m.push_back((uint8_t)v.name.size());
+    m.insert(m.end(), v.name.begin(), v.name.end());
+    m.push_back((uint8_t)v.type.size());
+    m.insert(m.end(), v.type.begin(), v.type.end());
+    const uint16_t len = (uint16_t)v.size;
+    m.push_back((uint8_t)(len & 0xff));
+    m.push_back((uint8_t)(len >> 8));
+    const uint8_t* d = v.owner->cb[v.cbuf].data() + v.offset;
+    m.insert(m.end(), d, d + len);
+    send_all_bytes(fd, m.data(), m.size());
+}
+
+bool read_bytes(int fd, void* out, size_t n) // VariableManager.cpp:47-72
+{
+    char* c = static_cast<char*>(out);
+    while (n) {
+        ssize_t k = ::recv(fd, c, n, 0);
+        if (k <= 0) return false;
+        c += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+
+void net_loop() // VariableManager.cpp:124-188
+{
+    while (g_running.load()) {
+        int fd = ::accept(g_listener, nullptr, nullptr);
+        if (fd < 0) {
+            if (!g_running.load()) break;
+            continue;
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_cb_mu);
+            g_client.store(fd);
+            for (auto& v : g_vars) send_variable(fd, v); // sendAllVariables on connect
+        }
+        for (;;) {
+            uint8_t nlen = 0;
+            if (!read_bytes(fd, &nlen, 1)) break;
+            std::string name(nlen, '\0');
+            if (nlen && !read_bytes(fd, &name[0], nlen)) break;
+            int size = -1;
+            {
+                std::lock_guard<std::mutex> lk(g_cb_mu);
+                for (auto& v : g_vars)
+                    if (v.name == name) {
+                        size = v.size;
+                        break;
+                    }
+            }
+            if (size < 0) break; // "Var not found": the reference closes the client
+            std::vector<uint8_t> data((size_t)size);
+            if (size && !read_bytes(fd, data.data(), (size_t)size)) break;
+            std::lock_guard<std::mutex> lk(g_cb_mu);
+            for (auto& v : g_vars)
+                if (v.name == name && v.size == size) {
+                    memcpy(v.owner->cb[v.cbuf].data() + v.offset, data.data(), (size_t)size);
+                    v.owner->cb_dirty = true;
+                    break;
+                }
+        }
+        {
+            std::lock_guard<std::mutex> lk(g_cb_mu);
+            g_client.store(-1);
+        }
+        ::close(fd);
+    }
+}
+} // namespace
+
+static void varmgr_clear() // VariableManager::clear: tell the client, drop every variable
+{
+    std::lock_guard<std::mutex> lk(g_cb_mu);
+    const int fd = g_client.load();
+    if (fd >= 0) {
+        const uint8_t two = 2;
+        send_all_bytes(fd, &two, 1);
+    }
+    g_vars.clear();
+}
+
+static void varmgr_register(Shader* s)
+{
+    if (!s->has_cb[CB_XTWEAK]) return;
+    std::lock_guard<std::mutex> lk(g_cb_mu);
+    for (auto& v : s->vars) {
+        if (v->cbuf != CB_XTWEAK) continue;
+        VarEntry e;
+        e.name = v->name;
+        e.type = v->size == 12 ? "float3" : v->size == 16 ? "float4" : v->size == 8 ? "float2" : "float";
+        e.size = v->size;
+        e.cbuf = v->cbuf;
+        e.offset = v->offset;
+        e.owner = s;
+        g_vars.push_back(e);
+    }
+}
+
+static void varmgr_forget(Shader* s)
+{
+    std::lock_guard<std::mutex> lk(g_cb_mu);
+    g_vars.erase(std::remove_if(g_vars.begin(), g_vars.end(), [s](const VarEntry& e) { return e.owner == s; }),
+                 g_vars.end());
+}
+
+extern "C" {
+
+int rt_varmgr_start(int port, const char* bind_address)
+{
+    if (g_running.load()) return fail(RT_ERR_STATE, "variable manager already running");
+    if (port <= 0 || port > 65535) port = 10666; // VariableManager.cpp:131
+    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd < 0) return fail(RT_ERR_STATE, "socket failed");
+    int one = 1;
+    (void)setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons((uint16_t)port);
+    if (inet_pton(AF_INET, bind_address && *bind_address ? bind_address : "127.0.0.1", &a.sin_addr) != 1) {
+        ::close(fd);
+        return fail(RT_ERR_INVALID, "bad bind address");
+    }
+    if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) != 0 || ::listen(fd, 5) != 0) {
+        ::close(fd);
+        return fail(RT_ERR_STATE, "bind/listen on port %d failed", port); // LOGERROR "bind"
+    }
+    g_listener = fd;
+    g_running.store(true);
+    g_net = std::thread(net_loop);
+    return RT_OK;
+}
+
+int rt_varmgr_stop(void)
+{
+    if (!g_running.load()) return RT_OK;
+    g_running.store(false);
+    ::shutdown(g_listener, SHUT_RDWR);
+    {
+        std::lock_guard<std::mutex> lk(g_cb_mu);
+        const int c = g_client.load();
+        if (c >= 0) ::shutdown(c, SHUT_RDWR);
+    }
+    if (g_net.joinable()) g_net.join();
+    ::close(g_listener);
+    g_listener = -1;
+    return RT_OK;
+}
+
+int rt_varmgr_count(void)
+{
+    std::lock_guard<std::mutex> lk(g_cb_mu);
+    return (int)g_vars.size();
+}
+
+int rt_varmgr_register_compute(rt_compute c)
+{
+    if (!c) return fail(RT_ERR_INVALID, "null compute");
+    Shader* s = c->new_shader ? c->new_shader : c->shader;
+    if (!s) return fail(RT_ERR_STATE, "no shader");
+    varmgr_forget(s);
+    varmgr_register(s);
+    std::lock_guard<std::mutex> lk(g_cb_mu);
+    const int fd = g_client.load();
+    if (fd >= 0)
+        for (auto& v : g_vars)
+            if (v.owner == s) send_variable(fd, v);
+    return RT_OK;
+}
+
+} // extern "C"

@@ -288,6 +288,27 @@ def read_recording(path, width, height):
     return frames, np.array(rows, np.uint64).reshape(-1, 3)
 
 
+class VariableManager:
+    """Common/VariableManager (the live-tweak TCP server, main.cpp:99 `-m`), native in the runtime:
+    start() serves the protocol of varclient.VariableClient on a thread."""
+
+    @staticmethod
+    def start(port=10666, bind_address="127.0.0.1"):
+        check(lib().rt_varmgr_start(int(port), bind_address.encode()), "variable manager start")
+
+    @staticmethod
+    def stop():
+        check(lib().rt_varmgr_stop(), "variable manager stop")
+
+    @staticmethod
+    def count():
+        return int(lib().rt_varmgr_count())
+
+    @staticmethod
+    def register_compute(compute):
+        check(lib().rt_varmgr_register_compute(compute._h), "variable manager register")
+
+
 class Noise:
     """Graphics/Noise.cpp:39-94 via rt_noise_generate (seed 300 unless random)."""
     TEXTURE_SIZE = 128

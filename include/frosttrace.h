@@ -211,6 +211,22 @@ int rt_recorder_info(rt_recorder rec, unsigned long long* frames, unsigned long 
                      unsigned long long* frame_duration);
 void rt_recorder_destroy(rt_recorder rec);
 
+/* ---- VariableManager (Common/VariableManager.{h,cpp}; main.cpp:99 `-m`) ----
+ * The live-tweak TCP protocol (VariableManager.cpp:76-83): on connect the server sends every
+ * registered variable as [1][name len:1][name][type len:1][type][size:2 LE][data]; a clear sends
+ * [2]; the client writes a variable as [name len:1][name][data] (an unknown name closes the
+ * connection).  Registered variables are the members of cbuffers named 'X...' (XTweakable's
+ * SunDirection, tracing.hlsl:6-9); a write updates the compute's cbuffer shadow, uploaded on the
+ * next launch.  As in ComputeDirect3D::create (:408, :188-197) every rt_compute_load clears the
+ * registry and registers its own shader's variables -- so after Terrain::reload (tracescreen, then
+ * camerarays, which has no 'X' cbuffer) the registry is empty, as in the reference.
+ * rt_varmgr_register_compute (not in the reference) re-registers one compute's variables and
+ * sends them to a connected client.  port <= 0 means 10666; bind_address NULL = 127.0.0.1. */
+int rt_varmgr_start(int port, const char* bind_address);
+int rt_varmgr_stop(void);
+int rt_varmgr_count(void);
+int rt_varmgr_register_compute(rt_compute cs);
+
 #ifdef __cplusplus
 }
 #endif

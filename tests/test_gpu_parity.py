@@ -423,3 +423,42 @@ def test_fly_through_device_feed_matches_oracle_feed():
     path = np.array(path)
     assert np.array_equal(path_dev, path)
     assert np.array_equal(path_ring, path)
+
+
+# --- VariableManager: a live SunDirection tweak reaches the frame ----
+def test_variable_manager_live_tweak_changes_frame():
+    import socket
+
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import camera as CAM
+    from gpgpuraytrace_amd import varclient as VC
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    consts = GI.consts(64, 48, "reset")
+    G.VariableManager.start(port)
+    try:
+        dev, ter = make(consts)  # reload: tracescreen then camerarays -> registry cleared again
+        assert G.VariableManager.count() == 0  # the reference's order leaves nothing registered
+        G.VariableManager.register_compute(ter.compute)
+        assert G.VariableManager.count() == 1
+        cl = VC.VariableClient("127.0.0.1", port)
+        assert cl.poll() == "add"
+        assert cl.variables["SunDirection"][0] == "float3"
+        assert np.array_equal(cl.value("SunDirection"), np.asarray(consts["sun"], np.float32))
+        sun = CAM.sun_direction(0.36)
+        cl.send("SunDirection", sun)
+        cl.close()
+        cl2 = VC.VariableClient("127.0.0.1", port)  # served after the first client is done
+        assert cl2.poll() == "add" and np.array_equal(cl2.value("SunDirection"), sun)
+        cl2.close()
+        ter.render_device()
+        dev.present()
+        img = dev.readback_float()
+        c2 = dict(consts, sun=sun)
+        ref = O.render(O.noise_tables(), O.make_frame(c2))
+        assert bits_equal(img, ref["rgba32f"])
+        dev.destroy()
+    finally:
+        G.VariableManager.stop()
