@@ -7,9 +7,10 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# RT_LIB_VARIANT=trace loads the debug build with k_trace's wave timeline (make trace)
-LIB_PATH = os.path.join(HERE, "_build", "librt_hip_trace.so" if os.environ.get("RT_LIB_VARIANT") == "trace"
-                        else "librt_hip.so")
+# RT_LIB_VARIANT=<name> loads an experiment build _build/librt_hip_<name>.so instead (make trace:
+# k_trace's wave timeline; make variant NAME=<name> FLAGS=...: A/B builds of compile-time switches)
+_VARIANT = os.environ.get("RT_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, "_build", f"librt_hip_{_VARIANT}.so" if _VARIANT else "librt_hip.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "frosttrace.h")
 

@@ -982,6 +982,9 @@ __device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
 // the single-lane march gives).  A phase runs until half its rays are done, hands the
 // states back to the owning lanes, and the survivors re-pack twice as wide.
 constexpr uint32_t kSegLive = 16; // live rays at or below which a wave switches to segment form
+// k_trace<.., SEG=true> carries the tail code; inlined, it costs the hot loops some spills
+// (scratch traffic, no measurable time at one GPU), so it is launched only when the shard
+// has few units per wave -- the strong-scaling regime where the last rays set the frame.
 
 template <int L, bool CF>
 __device__ __forceinline__ void march_shfl(March<L, CF>& d, const March<L, CF>& s, uint32_t src)
@@ -1085,7 +1088,7 @@ __device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
 #define WT(...)
 #endif
 
-template <int L, bool STATS>
+template <int L, bool STATS, bool SEG>
 __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad, const float2* __restrict__ cells,
                                                 UnitMap m, const uint32_t* __restrict__ order,
@@ -1183,7 +1186,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 push_long(live, st, t, type);
                 return;
             }
-            if constexpr (L == RT_NOMADPLAINS) {
+            if constexpr (L == RT_NOMADPLAINS && SEG) {
                 // drained, nothing queued and only a few rays left: finish them in group form
                 if ((uint32_t)__popcll(lv) <= seg_live && vload(q.l_tail) == vload(q.l_head)) {
                     seg_finish<true>(c, st, live, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0, lane);
@@ -1257,7 +1260,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
                 const uint64_t lb = __ballot(lv);
                 if (lb == 0ull) break;
-                if constexpr (L == RT_NOMADPLAINS) {
+                if constexpr (L == RT_NOMADPLAINS && SEG) {
                     if ((uint32_t)__popcll(lb) <= seg_live) {
                         seg_finish<false>(c, st, lv, RT_CAMERA_FAR, max_steps, lane);
                         break;
@@ -1549,6 +1552,11 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         const uint32_t v = e ? (uint32_t)atoi(e) : kSegLive;
         return v < kSegLive ? v : kSegLive; // seg_finish packs at most 16 rays (4 lanes each)
     }();
+    // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
+    const char* seg_env = getenv("RT_SEG"); // RT_SEG=0/1 forces it off/on (read per launch: tests flip it)
+    const int seg_mode = seg_env ? atoi(seg_env) : -1;
+    const bool seg = L == RT_NOMADPLAINS && tune_seg_live > 0 &&
+                     (seg_mode >= 0 ? seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
@@ -1562,10 +1570,14 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
         else if (pipe == RT_PIPELINE_STAGED)
             hipLaunchKernelGGL((k_primary<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
                                m, a.order, a.res, a.hitlist, a.queue, a.stats);
+        else if (seg)
+            hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
+                               cells, m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+                               a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
         else
-            hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
-                               a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
-                               a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
+            hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
+                               cells, m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+                               a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,

@@ -1,6 +1,8 @@
 // hip_adapter.cpp -- see hip_adapter.h.
 #include "hip_adapter.h"
 
+#include "Common/Timer.h"
+
 TextureHIP::TextureHIP(rt_device dev) { rt_texture_create(dev, &tex); }
 TextureHIP::~TextureHIP() { rt_texture_destroy(tex); }
 
@@ -84,9 +86,29 @@ bool DeviceHIP::create()
     return rt_device_create(ws.gpu < 0 ? 0 : ws.gpu, ws.width, ws.height, 0, &dev) == RT_OK;
 }
 
-void DeviceHIP::present() { rt_device_present(dev); }
+void DeviceHIP::present()
+{
+    // the recorder's sample duration when not fixed speed (RecorderWinAPI.cpp:264-269)
+    if (recorder) rt_recorder_set_frame_time(recorder->handle(), Timer::get()->getConstant());
+    rt_device_present(dev);
+}
 void DeviceHIP::flush() { rt_device_flush(dev); }
 ICompute* DeviceHIP::createCompute() { return new ComputeHIP(dev); }
 ITexture* DeviceHIP::createTexture() { return new TextureHIP(dev); }
 
 bool DeviceHIP::readback(void* dst, size_t rowPitch) const { return rt_device_readback(dev, dst, rowPitch) == RT_OK; }
+
+bool RecorderHIP::create()
+{
+    DeviceHIP* d = dynamic_cast<DeviceHIP*>(device);
+    if (!d || rt_recorder_create(d->handle(), frameRate, fixedSpeed ? 1 : 0, "output.rgb32", &rec) != RT_OK)
+        return false;
+    d->setRecorder(this);
+    return true;
+}
+
+RecorderHIP::~RecorderHIP()
+{
+    if (DeviceHIP* d = dynamic_cast<DeviceHIP*>(device)) d->setRecorder(nullptr);
+    rt_recorder_destroy(rec);
+}

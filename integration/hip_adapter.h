@@ -13,6 +13,7 @@
 
 #include "Factories/ICompute.h"
 #include "Factories/IDevice.h"
+#include "Factories/IRecorder.h"
 #include "Factories/ITexture.h"
 #include "frosttrace.h"
 
@@ -98,7 +99,32 @@ public:
     ITexture* createTexture() override;
     bool readback(void* dst, size_t rowPitch) const;
     rt_device handle() const { return dev; }
+    void setRecorder(class RecorderHIP* r) { recorder = r; } // DeviceDirect3D::setRecorder (:229-232)
 
 private:
     rt_device dev = nullptr;
+    class RecorderHIP* recorder = nullptr;
+};
+
+// RecorderWinAPI (Adapters/RecorderWinAPI.cpp) over rt_recorder_*: RecorderFactory::construct
+// makes one for a DeviceHIP; it attaches to the device, whose present() then writes every
+// frame while recording (DeviceDirect3D.cpp:242-256), swizzled to RGB32 on the GPU.  The sink
+// is a raw-video file (+ time-stamp index) instead of Media Foundation's output.wmv.
+class RecorderHIP : public IRecorder
+{
+public:
+    RecorderHIP(IDevice* device, int frameRate, bool fixedSpeed) : device(device), frameRate(frameRate),
+        fixedSpeed(fixedSpeed) { }
+    ~RecorderHIP() override;
+    bool create() override;
+    void start() override { IRecorder::start(); rt_recorder_start(rec); }
+    void stop() override { IRecorder::stop(); rt_recorder_stop(rec); }
+    void write(void* frame, int stride) override { rt_recorder_write(rec, frame, stride); }
+    rt_recorder handle() const { return rec; }
+
+private:
+    IDevice* device;
+    int frameRate;
+    bool fixedSpeed;
+    rt_recorder rec = nullptr;
 };

@@ -41,7 +41,10 @@ def main(src, dst):
     shutil.copy(ks[0], os.path.join(dst, "kernel_stats.csv"))
     bench = open(os.path.join(src, "kt_bench.json")).read().strip().splitlines()[-1]
     with open(os.path.join(dst, "kernels.md"), "w") as f:
-        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`\n\n")
+        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`\n\n"
+                "All launches of the run.  The timed loop keeps 3 frames in flight, so those launches share the\n"
+                "GPU and each one spans longer than it would alone; the per-launch cost the roofline uses is the\n"
+                "bench's one-frame-in-flight pass, tabulated at the end from the same trace.\n\n")
         f.write("| kernel | calls | avg ms | total ms |\n|---|---:|---:|---:|\n")
         for r in rows:
             f.write(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
@@ -81,7 +84,8 @@ def main(src, dst):
                         f"{b0['roofline']['kernel_avg_ms']} ms\n")
     m = pmc_means(src)
     with open(os.path.join(dst, "pmc.md"), "w") as f:
-        f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group)\n\n")
+        f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group, "
+                "`bench.py --frames-in-flight 1`: the counters are chip-wide, so no frame may overlap)\n\n")
         for k in sorted(m):
             f.write(f"## {k}\n\n")
             for c in sorted(m[k]):
