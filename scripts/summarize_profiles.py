@@ -10,11 +10,17 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 from collections import defaultdict
 
 TRACESCREEN = ("k_order", "k_trace", "k_primary", "k_shade", "k_shadow", "k_finish", "k_march")
+
+
+def instrumented(name):
+    """STATS instantiations (the untimed counting frame): k_x<L, true, ..> / k_x<true>."""
+    return re.search(r"<(\d+, )?true", name) is not None
 
 
 def short(name):
@@ -50,7 +56,7 @@ def main(src, dst):
             f.write(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
                     f"{float(r['TotalDurationNs']) / 1e6:.3f} |\n")
         plain = {short(r["Name"]): float(r["AverageNs"]) / 1e6 for r in rows}
-        ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k)
+        ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and not instrumented(k))
         f.write(f"\ntracescreen (uninstrumented k_order + k_trace + k_shade_pre + k_shadow + k_finish) avg sum: {ts:.4f} ms\n")
         f.write(f"\nbench line of the same run:\n\n```\n{bench}\n```\n")
     # the bench's roofline pass = its last K tracescreen launches (one frame in flight): per-kernel
@@ -61,7 +67,7 @@ def main(src, dst):
     if kt and K:
         disp = sorted(((short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
                        for r in csv.DictReader(open(kt[0]))), key=lambda x: x[1])
-        ts_disp = [d for d in disp if any(d[0].startswith(t) for t in TRACESCREEN) and "true>" not in d[0]]
+        ts_disp = [d for d in disp if any(d[0].startswith(t) for t in TRACESCREEN) and not instrumented(d[0])]
         starts = [i for i, d in enumerate(ts_disp) if d[0].startswith(("k_order", "k_tracescreen", "k_march"))]
         last = ts_disp[starts[-K]:] if len(starts) >= K else []
         per = defaultdict(list)
@@ -94,7 +100,7 @@ def main(src, dst):
     tr = {}
     fetch = write = rd = wr = 0.0
     for k, cs in m.items():
-        if any(k.startswith(t) for t in TRACESCREEN) and "true>" not in k:
+        if any(k.startswith(t) for t in TRACESCREEN) and not instrumented(k):
             fetch += cs.get("FETCH_SIZE", 0.0)
             write += cs.get("WRITE_SIZE", 0.0)
             rd += cs.get("TCC_EA0_RDREQ_sum", 0.0)
