@@ -27,9 +27,14 @@ using rtm::fma;
 //           One pair of loads yields both z-layers of a lattice column in register
 //           pairs that v_pk_fma_f32 consumes as they land (no shuffles), and only
 //           the four z-layer indices need extracting.  Entries are lane-private:
-//           entry i for lane slot s at gxy[i*16 + (s&15)], gz[i*32 + (s&31)], so a
-//           ds_read_b128 (16 lanes per pass) or ds_read_b64 (32 lanes per pass) is
-//           conflict-free however random the indices.  Both are i*256 bytes + slot.
+//           entry i for lane slot s at gxy[i*16 + (s&15)] (16 B) and, RT_GZ16, gz at
+//           the same byte offset in the next 32 KiB (8 of the slot's 16 B used), so one
+//           v_perm_b32 addresses both loads (ds_read_b64 ... offset:32768); the b128
+//           loads are conflict-free however random the indices, the b64 loads 2-way.
+//           RT_GZ16=0: gz[i*32 + (s&31)] (8 B slots, conflict-free, own address).
+#ifndef RT_GZ16
+#define RT_GZ16 1
+#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 struct NoiseView {
@@ -37,7 +42,7 @@ struct NoiseView {
     const float4* gxy;
     const float2* gz;
     uint32_t so16;  // (lane & 15) * 16: this lane's byte slot in a gxy entry row
-    uint32_t so32;  // (lane & 31) * 8:  this lane's byte slot in a gz entry row
+    uint32_t so32;  // (lane & 31) * 8:  this lane's byte slot in a gz entry row (RT_GZ16=0)
     mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
 };
 
@@ -78,8 +83,11 @@ __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, floa
     v2f uxy = fade2(xy);
     float uz = fade(z);
     // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
-    uint32_t X = (uint32_t)Px & 127u, Y = (uint32_t)Py & 127u, Z = (uint32_t)Pz & 127u;
-    uint32_t t = nz.perm2d[X + (Y << 7)];
+    // texel (Px & 127, Py & 127) at byte ((Py & 127) << 9) | ((Px & 127) << 2): the low
+    // term stays below 512, so add-then-mask needs no separate Py mask
+    const uint32_t Z = (uint32_t)Pz & 127u;
+    const uint32_t toff = (((uint32_t)Py << 9) + (((uint32_t)Px << 2) & 0x1fcu)) & 0xfffcu;
+    uint32_t t = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(nz.perm2d) + toff);
     // Pu = texel + Pu.z per channel (bytes <= 127+127: no carry), % 128
     uint32_t w = (t + Z * 0x01010101u) & 0x7f7f7f7fu; // AA, AB, BA, BB column indices at z
     // entry i of either plane starts at byte i*256: one v_perm_b32 per corner builds
@@ -90,12 +98,17 @@ __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, floa
         return *reinterpret_cast<const float4*>(gb + __builtin_amdgcn_perm(w, nz.so16, sel));
     };
     auto gz_at = [&](uint32_t sel) {
+#if RT_GZ16
+        return *reinterpret_cast<const float2*>(zb + __builtin_amdgcn_perm(w, nz.so16, sel));
+#else
         return *reinterpret_cast<const float2*>(zb + __builtin_amdgcn_perm(w, nz.so32, sel));
+#endif
     };
     const float4 a0 = gxy_at(0x0c0c0400u), a1 = gxy_at(0x0c0c0500u), b0 = gxy_at(0x0c0c0600u), b1 = gxy_at(0x0c0c0700u);
     const float2 za0 = gz_at(0x0c0c0400u), za1 = gz_at(0x0c0c0500u), zb0 = gz_at(0x0c0c0600u), zb1 = gz_at(0x0c0c0700u);
     const float x = xy.x, y = xy.y;
-    const float x1 = x + -1.0f, y1 = y + -1.0f;
+    const v2f xy1 = xy + v2(-1.0f, -1.0f);
+    const float x1 = xy1.x, y1 = xy1.y;
     const v2f zz = v2(z, z + -1.0f);
     v2f g00 = gdot2(a0, za0, x, y, zz);   // (g000, g001)
     v2f g10 = gdot2(b0, zb0, x1, y, zz);  // (g100, g101)
