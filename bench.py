@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
     ap.add_argument("--frames-in-flight", type=int, default=3,
                     help="frame contexts (HIP streams) kept in flight; 1 = one frame at a time")
+    ap.add_argument("--graph", type=int, default=None,
+                    help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
+                         "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -84,6 +87,8 @@ def parse():
     for key in ("width", "height", "max_steps", "ao"):
         if getattr(a, key) is None:
             setattr(a, key, preset[key])
+    if a.graph is None:
+        a.graph = 1 if a.config == "c5" else 0
     return a
 
 
@@ -166,7 +171,7 @@ def main():
     # --- timed: D frames in flight (FrameRing: one full frame context + HIP stream per slot) ---
     camera = G.Camera(W, H, euler=euler)
     ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
-                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao)
+                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph))
     packed, gathered = {}, {}
     if world > 1:
         nb = [E.shard_bytes(ring.slots[0][0], r, world) for r in range(world)]
@@ -257,6 +262,8 @@ def main():
                 "noise3d_per_frame_tracescreen": shard_noise if world == 1 else None,
                 "parallelism": "single GPU" if world == 1 else f"tile-cyclic 32x32 shards x{world} + RCCL gather",
                 "frames_in_flight": a.frames_in_flight,
+                "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
+                              else "direct launches",
                 "frame_latency_ms": round(latency_ms, 4),
             },
             "roofline": {

@@ -17,6 +17,7 @@ HEADER = os.path.join(ROOT, "include", "frosttrace.h")
 RT_OK = 0
 RT_DEVICE_FLOAT_OUTPUT = 1
 RT_DEVICE_STATS = 2
+RT_DEVICE_GRAPH = 4
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -55,6 +56,7 @@ SIGNATURES = {
     "rt_device_stats": (_i, [_vp, C.POINTER(RtStats), _i]),
     "rt_device_set_profiling": (_i, [_vp, _i]),
     "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
+    "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     "rt_texture_create": (_i, [_vp, C.POINTER(_vp)]),
     "rt_texture_init": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i]),
     "rt_texture_destroy": (None, [_vp]),

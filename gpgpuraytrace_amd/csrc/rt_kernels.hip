@@ -1663,6 +1663,22 @@ __global__ void k_debug_math(int op, const float* __restrict__ a, const float* _
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    if (op == 12) {
+        // octave-count sweep: d2 = the float with bits bits(a[0]) + i; counts (in y[0..2] as
+        // uint32) unflagged estimates that differ from np_octaves_exact, flagged lanes, and
+        // how many of the swept d2 exist
+        const float d2 = rtm::fbits(rtm::bits(a[0]) + (uint32_t)i);
+        bool near;
+        const int est = rts::np_octaves_estimate(d2, &near);
+        uint32_t* cnt = reinterpret_cast<uint32_t*>(y);
+        if (!near && est != rts::np_octaves_exact(d2)) atomicAdd(&cnt[0], 1u);
+        const uint64_t bn = __ballot(near), ba = __ballot(true);
+        if (__lane_id() == 0) {
+            if (bn) atomicAdd(&cnt[1], (uint32_t)__popcll(bn));
+            atomicAdd(&cnt[2], (uint32_t)__popcll(ba));
+        }
+        return;
+    }
     float x = a[i], v = 0.0f;
     switch (op) {
     case 0: v = rtm::exp2(x); break;

@@ -127,6 +127,13 @@ struct rt_device_s {
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
     size_t ev_used = 0;
+    // RT_DEVICE_GRAPH: rt_terrain_render replays two captured graphs per frame, the prepass
+    // (camerarays + setTargetDepths) and tracescreen, re-captured when any launch argument changes
+    struct FrameGraph {
+        std::vector<uint64_t> key;
+        hipGraphExec_t exec = nullptr;
+    } graph_pre, graph_trace;
+    unsigned long long graph_captures = 0, graph_launches = 0;
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -568,6 +575,8 @@ void rt_device_destroy(rt_device d)
     if (d->aocc) (void)hipFree(d->aocc);
     if (d->bgrx) (void)hipFree(d->bgrx);
     if (d->recorder) recorder_detach(d->recorder); // the recorder outlives its device: it stops capturing
+    if (d->graph_pre.exec) (void)hipGraphExecDestroy(d->graph_pre.exec);
+    if (d->graph_trace.exec) (void)hipGraphExecDestroy(d->graph_trace.exec);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -696,6 +705,14 @@ int rt_device_kernel_time(rt_device d, double* total_ms, int* launches)
     if (total_ms) *total_ms = tot;
     if (launches) *launches = (int)d->ev_used;
     d->ev_used = 0;
+    return RT_OK;
+}
+
+int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned long long* launches)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (captures) *captures = d->graph_captures;
+    if (launches) *launches = d->graph_launches;
     return RT_OK;
 }
 
@@ -1005,6 +1022,63 @@ int rt_terrain_feed_wait(rt_compute cam, float* camera_results)
     return RT_OK;
 }
 
+extern "C++" {
+namespace {
+// every value a captured launch bakes in: pointers, sizes, modes, and the environment
+// switches the launch code reads per call
+void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
+{
+    const uint64_t v[] = {(uint64_t)(uintptr_t)a.stream, (uint64_t)a.landscape, (uint64_t)(uintptr_t)a.consts,
+                          (uint64_t)(uintptr_t)a.perm2d, (uint64_t)(uintptr_t)a.grad, (uint64_t)(uintptr_t)a.stats,
+                          (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)a.pipeline,
+                          (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.hitlist,
+                          (uint64_t)(uintptr_t)a.shrec, (uint64_t)a.long_cap, (uint64_t)(uintptr_t)a.fin,
+                          (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
+                          (uint64_t)(uintptr_t)a.order};
+    k.insert(k.end(), std::begin(v), std::end(v));
+}
+
+void key_env(std::vector<uint64_t>& k)
+{
+    const char* seg = getenv("RT_SEG"); // read per tracescreen launch (launch_split_l)
+    k.push_back(seg ? (uint64_t)(1 + atoi(seg)) : 0);
+}
+
+// Replay g (capturing `launches` on dev->stream first when its key changed).  Stream
+// capture records the same launches the direct path issues, so a replay is the same work.
+template <class F>
+int graph_run(rt_device dev, rt_device_s::FrameGraph& g, std::vector<uint64_t>&& key, F launches)
+{
+    if (!g.exec || g.key != key) {
+        if (g.exec) HIP_TRY(hipGraphExecDestroy(g.exec));
+        g.exec = nullptr;
+        g.key.clear();
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(dev->stream, hipStreamCaptureModeThreadLocal));
+        launches();
+        const hipError_t launch_err = hipGetLastError();
+        const hipError_t end_err = hipStreamEndCapture(dev->stream, &graph);
+        if (launch_err != hipSuccess || end_err != hipSuccess) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return fail(RT_ERR_HIP, "graph capture failed: %s",
+                        hipGetErrorString(launch_err != hipSuccess ? launch_err : end_err));
+        }
+        const hipError_t inst_err = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(graph);
+        if (inst_err != hipSuccess) {
+            g.exec = nullptr;
+            return fail(RT_ERR_HIP, "graph instantiate failed: %s", hipGetErrorString(inst_err));
+        }
+        g.key = std::move(key);
+        ++dev->graph_captures;
+    }
+    HIP_TRY(hipGraphLaunch(g.exec, dev->stream));
+    ++dev->graph_launches;
+    return RT_OK;
+}
+} // namespace
+} // extern "C++"
+
 static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count, bool feed)
 {
     if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
@@ -1021,7 +1095,23 @@ static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int sh
     rt_array_s* cd = scr->shader->array("CellDistance");
     if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
     float4* crp = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : dev->scratch_cam;
-    rt_launch_camerarays(make_launch(dev, cam->shader), crp);
+    const RtLaunch la_cam = make_launch(dev, cam->shader), la_scr = make_launch(dev, scr->shader);
+    float2* cells = (float2*)cd->dev_ptr;
+    const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr;
+    if (graphs) {
+        // the constant uploads (sync_shader) stay outside: they precede the replay on this stream
+        std::vector<uint64_t> kp;
+        key_launch(kp, la_cam);
+        kp.push_back((uint64_t)(uintptr_t)crp);
+        kp.push_back((uint64_t)(uintptr_t)cells);
+        if ((rc = graph_run(dev, dev->graph_pre, std::move(kp), [&] {
+                 rt_launch_camerarays(la_cam, crp);
+                 rt_launch_cell_depths(dev->stream, crp, cells);
+             })))
+            return rc;
+    } else {
+        rt_launch_camerarays(la_cam, crp);
+    }
     if (feed) {
         // Flyby's view of this frame, on the host as soon as the prepass is done
         if (!cam->feed_host) HIP_TRY(hipHostMalloc(&cam->feed_host, 1024 * sizeof(float4)));
@@ -1030,11 +1120,25 @@ static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int sh
         HIP_TRY(hipEventRecord(cam->feed_ev, dev->stream));
         cam->feed_pending = true;
     }
-    rt_launch_cell_depths(dev->stream, crp, (float2*)cd->dev_ptr);
+    if (!graphs) rt_launch_cell_depths(dev->stream, crp, cells);
+    auto trace = [&] {
+        rt_launch_tracescreen(la_scr, cells, dev->fb8, dev->fb32, 0, 0, (uint32_t)dev->width, (uint32_t)dev->height,
+                              (uint32_t)shard_rank, (uint32_t)shard_count);
+    };
     {
         KernelTimer kt(dev);
-        rt_launch_tracescreen(make_launch(dev, scr->shader), (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, 0, 0,
-                              (uint32_t)dev->width, (uint32_t)dev->height, (uint32_t)shard_rank, (uint32_t)shard_count);
+        if (graphs) {
+            std::vector<uint64_t> kt_key;
+            key_launch(kt_key, la_scr);
+            key_env(kt_key);
+            const uint64_t extra[] = {(uint64_t)(uintptr_t)cells, (uint64_t)(uintptr_t)dev->fb8,
+                                      (uint64_t)(uintptr_t)dev->fb32, (uint64_t)dev->width, (uint64_t)dev->height,
+                                      (uint64_t)shard_rank, (uint64_t)shard_count};
+            kt_key.insert(kt_key.end(), std::begin(extra), std::end(extra));
+            if ((rc = graph_run(dev, dev->graph_trace, std::move(kt_key), trace))) return rc;
+        } else {
+            trace();
+        }
     }
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -1123,6 +1227,20 @@ extern "C" int rt_debug_math(rt_device d, int op, const float* a, const float* b
 {
     if (!d || !a || !y || n <= 0) return fail(RT_ERR_INVALID, "bad arguments");
     float *da = nullptr, *db = nullptr, *dy = nullptr;
+    if (op == 12) {
+        // octave-count sweep over n bit patterns from bits(a[0]): 3 counters out
+        HIP_TRY(hipMalloc(&da, 4));
+        HIP_TRY(hipMalloc(&dy, 12));
+        HIP_TRY(hipMemcpy(da, a, 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(dy, 0, 12));
+        rt_launch_debug_math(d->stream, op, da, da, dy, n);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipStreamSynchronize(d->stream));
+        HIP_TRY(hipMemcpy(y, dy, 12, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(da));
+        HIP_TRY(hipFree(dy));
+        return RT_OK;
+    }
     size_t bytes = (size_t)n * 4;
     HIP_TRY(hipMalloc(&da, bytes));
     HIP_TRY(hipMalloc(&db, bytes));

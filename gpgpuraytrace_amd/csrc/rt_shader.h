@@ -137,18 +137,51 @@ struct Ctx {
     f3 sun;
 };
 
+// The FBM's octave count (Media/nomadplains/shaders/terrain.hlsl:16-22): N runs 1 ..
+// floor(detail), detail = max(18 - pow(dist, 0.33), 2), dist = max(length(p - Eye), 0.01).
+// detail in [2, 17.79] so N <= 17 (RT_NP_OCTAVES), and (float)N <= detail <=> N <= (int)detail.
+// Only this integer leaves the expression.  np_octaves_exact is the rule-R5 evaluation (the
+// oracle's); np_octaves_estimate gets t ~ 18 - dist^0.33 from the hardware v_log_f32/v_exp_f32
+// of d2 = dot(p - Eye, p - Eye) (no sqrt, no polynomial pow) and flags lanes whose t lies within
+// kOctEps of an integer, where the estimate and the exact value could floor differently.  Away
+// from integers the two agree: tests/test_gpu_parity.py sweeps every finite d2 >= 0 and checks
+// (rt_debug_math op 12) that each unflagged estimate equals np_octaves_exact.
+constexpr float kOctEps = 1.0f / 2048.0f;
+
+__device__ __forceinline__ int np_octaves_exact(float d2)
+{
+    const float dist = rtm::max(rtm::sqrt(d2), 0.01f);
+    return (int)rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
+}
+
+__device__ __forceinline__ int np_octaves_estimate(float d2, bool* near)
+{
+    // dist^0.33 = 2^(0.165 * log2(d2))
+    const float t = 18.0f - __builtin_amdgcn_exp2f(0.165f * __builtin_amdgcn_logf(d2));
+    const float ft = rtm::floor(t);
+    *near = rtm::abs((t - ft) - 0.5f) > 0.5f - kOctEps;
+    const int n = (int)ft;
+    return n < 2 ? 2 : (n > RT_NP_OCTAVES ? RT_NP_OCTAVES : n);
+}
+
+__device__ __forceinline__ int np_octaves(const Ctx& c, f3 p)
+{
+    const f3 v = rtm::sub(p, c.eye);
+    const float d2 = rtm::dot(v, v);
+    bool near;
+    int n = np_octaves_estimate(d2, &near);
+    if (near) n = np_octaves_exact(d2); // skipped (execz) unless some lane sits near an integer
+    return n;
+}
+
 // Media/nomadplains/shaders/terrain.hlsl:8-39
 __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 {
-    float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
     float d = -p.y;
     f3 p1 = rtm::scale(p, 0.4f);
     float s = 0.0f;
-    float detail = rtm::max(18.0f - rtm::pow_nonneg(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
-    // N = 1 .. floor(detail); detail in [2, 17.79] so N <= 17 (RT_NP_OCTAVES) and
-    // (float)N <= detail <=> N <= (int)detail
-    const int n_oct = (int)detail;
+    const int n_oct = np_octaves(c, p);
     #pragma unroll 1
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
         if (N > n_oct) break;
@@ -209,16 +242,14 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
                                                          uint32_t base, uint32_t* octaves)
 {
     constexpr int NV = SegOctaves<LPR>::NV, R = SegOctaves<LPR>::R;
-    float dist = rtm::max(rtm::length(rtm::sub(p, c.eye)), 0.01f);
     float d = -p.y;
     f3 p1 = rtm::scale(p, 0.4f);
-    float detail = rtm::max(18.0f - rtm::pow_nonneg_flat(dist, 0.33f), 2.0f);
     f3 q0 = rtm::scale(p1, 0.006f);
     // N = 1 .. floor(detail) in order.  A dead octave's value is +0 instead of being
     // skipped: fma(+0, w, s) == s bit for bit because s is never -0 (it starts at +0 and
     // an exact cancellation rounds to +0), so the serial chain needs no selects.  A round
     // no lane of the wave needs (all its octaves dead) is not evaluated at all.
-    const int n_oct = (int)detail;
+    const int n_oct = np_octaves(c, p);
     float nv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {

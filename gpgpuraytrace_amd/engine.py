@@ -157,9 +157,10 @@ class Compute:
 class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
-    def __init__(self, width, height, gpu=0, float_output=False, stats=False):
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False):
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
-        self.flags = (_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
+        self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
+                      | (_native.RT_DEVICE_GRAPH if graph else 0))
         self._h = None
 
     def create(self):
@@ -206,6 +207,12 @@ class Device:
         s = _native.RtStats()
         check(lib().rt_device_stats(self._h, C.byref(s), 1 if reset else 0), "stats")
         return {n: int(getattr(s, n)) for n, _ in s._fields_}
+
+    def graph_info(self):
+        """RT_DEVICE_GRAPH: (graphs captured, graph launches) since creation."""
+        cap, lau = C.c_ulonglong(), C.c_ulonglong()
+        check(lib().rt_device_graph_info(self._h, C.byref(cap), C.byref(lau)), "graph_info")
+        return int(cap.value), int(lau.value)
 
     def framebuffer_pointer(self):
         return lib().rt_device_framebuffer(self._h)
@@ -520,14 +527,15 @@ class FrameRing:
     frame i+1's camerarays prepass and primary phase run on the CUs that frame i's ray tail
     leaves idle, instead of waiting for it.  Every frame is still computed in full and
     independently; a slot is reused only after its previous frame (i - depth) has completed on
-    that slot's stream.  depth=1 is the reference's one-frame-at-a-time behaviour."""
+    that slot's stream.  depth=1 is the reference's one-frame-at-a-time behaviour.
+    graph=True: each slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH)."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 **terrain_kw):
+                 graph=False, **terrain_kw):
         self.depth, self.frame = int(depth), 0
         self.slots = []
         for _ in range(self.depth):
-            dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu)
+            dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph)
             if dev is None:
                 raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
             ter = Terrain(dev, theme, **terrain_kw)

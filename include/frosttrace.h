@@ -41,7 +41,11 @@ enum {
 /* DeviceDirect3D.cpp:113-126 swap-chain format R8G8B8A8_UNORM is always
  * produced; RT_DEVICE_FLOAT_OUTPUT additionally keeps the pre-quantisation
  * float4 colour (texOut's float4 value, tracescreen.hlsl:75) for parity. */
-enum { RT_DEVICE_FLOAT_OUTPUT = 1u, RT_DEVICE_STATS = 2u };
+enum { RT_DEVICE_FLOAT_OUTPUT = 1u, RT_DEVICE_STATS = 2u, RT_DEVICE_GRAPH = 4u };
+/* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
+ * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
+ * every frame; a changed launch argument (shader swap, buffers, shard, stats) re-captures.
+ * No reference counterpart (the D3D frame loop re-records its dispatches every frame). */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };
@@ -100,6 +104,8 @@ int rt_device_stats(rt_device dev, rt_stats* out, int reset); /* needs RT_DEVICE
  * since the last call (synchronises). */
 int rt_device_set_profiling(rt_device dev, int enable);
 int rt_device_kernel_time(rt_device dev, double* total_ms, int* launches);
+/* RT_DEVICE_GRAPH bookkeeping: graphs captured and graph launches since device creation. */
+int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned long long* launches);
 
 /* ---- ITexture (IDevice::createTexture + ITexture::create(dims, fmt, w, h, data, binding, cpu)) ---- */
 int rt_texture_create(rt_device dev, rt_texture* out);
@@ -182,6 +188,9 @@ int rt_terrain_set_target_depths(const float* camera_results, float* cell_distan
  * rt_debug_math: device evaluation of the numeric primitives of DESIGN.md §Numerics
  *   (op 0 exp2, 1 log2, 2 exp, 3 sin, 4 cos, 5 sqrt, 6 rcp, 7 rsqrt, 8 pow, 9 max,
  *   10 min, 11 pow for x >= 0); host arrays of n floats (b may be NULL for unary ops).
+ *   op 12 sweeps the nomadplains octave-count estimate over the n floats whose bit
+ *   patterns follow bits(a[0]) and writes 3 uint32 to out: unflagged estimates that differ
+ *   from the exact count, flagged estimates, patterns swept.
  * rt_debug_noise: noise3d (density = 0, noise.hlsl:153-179) or the compute's landscape
  *   getDensity (density = 1) at n points (xyz interleaved), with the compute's
  *   current tables and constants. */

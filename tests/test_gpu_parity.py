@@ -31,11 +31,11 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         pipeline="split", ao=0):
+         pipeline="split", ao=0, graph=False):
     import gpgpuraytrace_amd as G
     os.environ["RT_PIPELINE"] = pipeline
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
-                                    stats=stats)
+                                    stats=stats, graph=graph)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -91,6 +91,33 @@ def test_binary_primitives_bitexact(gop, oop):
     assert G.lib().rt_debug_math(dev._h, gop, a.ctypes.data, b.ctypes.data, y.ctypes.data, a.size) == 0
     assert bits_equal(y, O.binary(oop, a, b))
     dev.destroy()
+
+
+def test_octave_estimate_exhaustive():
+    """nomadplains' octave count from the hardware log/exp estimate (rt_shader.h np_octaves)
+    equals the rule-R5 count (sqrt + polynomial pow, the oracle's) for EVERY finite float
+    d2 >= 0 the estimate does not flag as near an integer."""
+    import gpgpuraytrace_amd as G
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, 8, 8)
+
+    def sweep(start, end):
+        total = [0, 0, 0]
+        while start < end:
+            n = min(end - start, 1 << 30)
+            a = np.array([start], np.uint32).view(np.float32)
+            out = np.zeros(3, np.uint32)
+            assert G.lib().rt_debug_math(dev._h, 12, a.ctypes.data, None, out.ctypes.data, n) == 0
+            total = [t + int(o) for t, o in zip(total, out)]
+            start += n
+        return total
+
+    every = sweep(0, 0x7F800000)  # +0 .. largest finite
+    lo, hi = (int(np.array([v], np.float32).view(np.uint32)[0]) for v in (1e-4, 4e7))
+    scene = sweep(lo, hi)         # distances 0.01 .. 6300: where the march samples
+    dev.destroy()
+    assert every[2] == 0x7F800000 and scene[2] == hi - lo
+    assert every[0] == 0, f"{every[0]} unflagged estimates differ from the exact octave count"
+    assert scene[1] < scene[2] // 200, scene  # the exact fallback stays rare
 
 
 # --- noise3d and getDensity ---------------------------------------------------------------
@@ -315,6 +342,80 @@ def test_frame_ring_in_flight_bitexact():
     ring.synchronize()
     for dev, _ in ring.slots:
         assert np.array_equal(dev.readback(), gold[last[id(dev)] + "_rgba8"]), last[id(dev)]
+    ring.destroy()
+
+
+@pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
+def test_graph_replay_bitexact(spec):
+    """RT_DEVICE_GRAPH (the C5 hipGraph frame loop): frames replayed from the captured graphs
+    equal the golden frames, stats included; replays capture once."""
+    gold = GI.load()
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    key = GI.frame_key(*spec)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True, ao=ao, graph=True)
+    for _ in range(3):
+        ter.render_device()
+        dev.present()
+        img, img8 = dev.readback_float(), dev.readback()
+        st = dev.stats()
+        assert bits_equal(img, gold[key + "_rgba32f"])
+        assert np.array_equal(img8, gold[key + "_rgba8"])
+        ref = gold[key + "_stats"]
+        assert (st["noise_calls"], st["primary_steps"], st["shadow_steps"], st["ao_steps"]) == \
+            (ref[0], ref[2], ref[3], ref[6])
+    assert dev.graph_info() == (2, 6)
+    dev.destroy()
+
+
+def test_graph_constants_shards_and_swap():
+    """A replay reads the constants uploaded before it (camera switch: no re-capture); a new
+    shard or a shader swap re-captures; shards replayed from graphs assemble to the frame."""
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    ka, kb = GI.frame_key(*GI.FRAMES[0]), GI.frame_key(*GI.FRAMES[1])  # 64x48 reset / lookdown
+    ca, cb = GI.consts(64, 48, "reset"), GI.consts(64, 48, "lookdown")
+    dev, ter = make(ca, graph=True)
+    for consts, key in ((ca, ka), (cb, kb), (ca, ka)):
+        ter.set_camera(FixedCamera(consts))
+        ter.set_time_of_day_vec(consts["sun"])
+        ter.update_terrain()
+        ter.render_device()
+        assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), key
+    assert dev.graph_info() == (2, 6)
+    # two shards replayed on one device, packed, then assembled
+    bufs = [torch.zeros(E.shard_bytes(dev, r, 2), dtype=torch.uint8, device="cuda:0") for r in range(2)]
+    for r in (1, 0):
+        ter.render_device(r, 2)
+        E.shard_pack(dev, r, 2, bufs[r].data_ptr())
+    E.shard_unpack(dev, 1, 2, bufs[1].data_ptr())
+    assert np.array_equal(dev.readback(), gold[ka + "_rgba8"])
+    assert dev.graph_info()[0] == 4  # tracescreen re-captured per shard (the prepass graph is reused)
+    # Terrain.reload + swap: new shaders, new graphs
+    assert ter.reload()
+    ter.render_device()
+    assert np.array_equal(dev.readback(), gold[ka + "_rgba8"])
+    assert dev.graph_info()[0] >= 5  # (a key equal in every baked pointer may reuse a graph)
+    dev.destroy()
+
+
+def test_frame_ring_graphs_bitexact():
+    import gpgpuraytrace_amd as G
+    os.environ["RT_PIPELINE"] = "split"
+    gold = GI.load()
+    spec = GI.FRAMES[1]
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    cam = FixedCamera(GI.consts(w, h, pose))
+    ring = G.FrameRing(w, h, depth=3, camera=cam, graph=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cam.c["sun"])
+    for _ in range(7):
+        ring.render()
+    ring.synchronize()
+    for dev, _ in ring.slots:
+        assert np.array_equal(dev.readback(), gold[GI.frame_key(*spec) + "_rgba8"])
+        assert dev.graph_info()[0] == 2
     ring.destroy()
 
 
