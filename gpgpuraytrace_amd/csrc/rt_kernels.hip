@@ -106,8 +106,8 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
 // the prepass is 1024 sequential marches of ~350 steps, so it is bound by the
 // latency of one step, and spreading each step's 17 FBM octaves + steep noise over
 // a lane group (rts::density_nomadplains_seg<32>) shortens that chain ~4x.
-template <bool STATS>
-__global__ void __launch_bounds__(256) k_camerarays_group(const RtConsts* __restrict__ k,
+template <bool STATS, int BS>
+__global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restrict__ k,
                                                           const uint32_t* __restrict__ perm2d,
                                                           const float4* __restrict__ grad, float4* __restrict__ out,
                                                           RtStats* stats)
@@ -1486,13 +1486,28 @@ template <int L>
 void launch_camerarays_l(const RtLaunch& a, float4* out)
 {
     if constexpr (L == RT_NOMADPLAINS) {
+        // one 32-lane group per ray; RT_PREPASS_BLOCK=1024 packs 32 rays per CU instead of 8
+        static const bool wide = [] {
+            const char* e = getenv("RT_PREPASS_BLOCK");
+            return e && atoi(e) == 1024;
+        }();
+        if (wide) {
+            dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 32), block(1024);
+            if (a.stats)
+                hipLaunchKernelGGL((k_camerarays_group<true, 1024>), grid, block, 0, a.stream, a.consts, a.perm2d,
+                                   a.grad, out, a.stats);
+            else
+                hipLaunchKernelGGL((k_camerarays_group<false, 1024>), grid, block, 0, a.stream, a.consts, a.perm2d,
+                                   a.grad, out, a.stats);
+            return;
+        }
         dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 8), block(256);
         if (a.stats)
-            hipLaunchKernelGGL((k_camerarays_group<true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out,
-                               a.stats);
+            hipLaunchKernelGGL((k_camerarays_group<true, 256>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad,
+                               out, a.stats);
         else
-            hipLaunchKernelGGL((k_camerarays_group<false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out,
-                               a.stats);
+            hipLaunchKernelGGL((k_camerarays_group<false, 256>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad,
+                               out, a.stats);
         return;
     }
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64), block(64);

@@ -546,6 +546,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
                       : strcmp(p, "staged") == 0 ? RT_PIPELINE_STAGED
                                                  : RT_PIPELINE_SPLIT;
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
+    if (const char* g = getenv("RT_GRID_CUS")) // persistent-grid cap (experiments: CU share per frame in flight)
+        if (atoi(g) > 0 && atoi(g) < d->num_cus) d->num_cus = atoi(g);
     *out = d.release();
     return RT_OK;
 }
