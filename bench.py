@@ -73,7 +73,11 @@ def parse():
     ap.add_argument("--max-steps", type=int, default=None, help="primary-march cap (build extension); 0 = reference")
     ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
     ap.add_argument("--frames-in-flight", type=int, default=3,
-                    help="frame contexts (HIP streams) kept in flight; 1 = one frame at a time")
+                    help="frame contexts (HIP streams) kept in flight; 1 = one frame at a time (with --batch B: "
+                         "batches of B frames in flight)")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="frames per rt_terrain_render_batch launch sequence (1..8); the timed loop renders whole "
+                         "batches (steps rounded up to a multiple)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
@@ -170,69 +174,80 @@ def main():
 
     # --- timed: D frames in flight (FrameRing: one full frame context + HIP stream per slot) ---
     camera = G.Camera(W, H, euler=euler)
+    B = max(1, min(8, a.batch))
     ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
-                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph))
+                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     packed, gathered = {}, {}
     if world > 1:
         nb = [E.shard_bytes(ring.slots[0][0], r, world) for r in range(world)]
         maxb = max(nb)
-        for k, (dev, _) in enumerate(ring.slots):
-            packed[k] = torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}")
+        for g in range(ring.depth):  # one packed buffer per batch slot: the batch's B shards back to back
+            packed[g] = torch.zeros(B * maxb, dtype=torch.uint8, device=f"cuda:{local}")
             if rank == 0:
-                gathered[k] = [torch.zeros(maxb, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(world)]
-        slot_streams = [torch.cuda.ExternalStream(dev.stream(), device=f"cuda:{local}") for dev, _ in ring.slots]
+                gathered[g] = [torch.zeros(B * maxb, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(world)]
+        group_streams = [torch.cuda.ExternalStream(ring.slots[g * B][0].stream(), device=f"cuda:{local}")
+                         for g in range(ring.depth)]
 
-    def frame():
-        k = ring.frame % ring.depth
-        dev = ring.render(rank if world > 1 else 0, world, present=world == 1)
+    def batch_step():
+        g = (ring.frame // B) % ring.depth
+        devs = ring.render_batch(rank if world > 1 else 0, world, present=world == 1)
         if world > 1:
-            # the gather rides on this slot's stream, so the other slots' frames keep running
-            with torch.cuda.stream(slot_streams[k]):
-                E.shard_pack(dev, rank, world, packed[k].data_ptr())
-                dist.gather(packed[k], gathered[k] if rank == 0 else None, dst=0)
+            # one gather per batch rides on the batch's stream, so the other batches keep running
+            with torch.cuda.stream(group_streams[g]):
+                # (a batch's devices share its stream: FrameRing)
+                for f, dev in enumerate(devs):
+                    E.shard_pack(dev, rank, world, packed[g].data_ptr() + f * maxb)
+                dist.gather(packed[g], gathered[g] if rank == 0 else None, dst=0)
                 if rank == 0:
                     for r in range(1, world):
-                        E.shard_unpack(dev, r, world, gathered[k][r].data_ptr())
-            dev.present()
+                        for f, dev in enumerate(devs):
+                            E.shard_unpack(dev, r, world, gathered[g][r].data_ptr() + f * maxb)
+            for dev in devs:
+                dev.present()
 
-    for _ in range(a.warmup + ring.depth):
-        frame()
+    n_batches = -(-a.steps // B)
+    frames_timed = n_batches * B
+    for _ in range(-(-a.warmup // B) + ring.depth):
+        batch_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        frame()
+    for _ in range(n_batches):
+        batch_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    # --- roofline pass: the same frames one at a time on slot 0 (launches do not overlap), HIP
-    # events around every tracescreen launch on the stream it runs on; also the frame latency ---
-    dev0, ter0 = ring.slots[0]
+    # --- roofline pass: the same batches one at a time on slot group 0 (launches do not overlap),
+    # HIP events around every tracescreen launch on the stream it runs on; also the latency ---
+    group0 = ring.slots[:B]
+    dev0 = group0[0][0]
     ring.set_profiling(True)
     ring.kernel_time()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(a.steps):
-        ter0.render_device(rank if world > 1 else 0, world)
-        dev0.present()
-    dev0.synchronize()
-    latency_ms = (time.perf_counter() - t1) / a.steps * 1e3
+    for _ in range(n_batches):
+        E.render_batch([t for _, t in group0], rank if world > 1 else 0, world)
+        for d, _ in group0:
+            d.present()
+    for d, _ in group0:
+        d.synchronize()
+    latency_ms = (time.perf_counter() - t1) / n_batches * 1e3
     kms, kn = ring.kernel_time()
     ring.set_profiling(False)
-    k_avg_ms = kms / max(1, kn)
+    k_avg_ms = kms / max(1, kn)  # one launch = a batch of B frames
     if world > 1:
         t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, latency_ms = float(t[0].item()), float(t[1].item())
 
-    ms_per_frame = elapsed / a.steps * 1e3
-    value = rays_per_frame * a.steps / elapsed / 1e6
-    achieved = shard_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
+    ms_per_frame = elapsed / frames_timed * 1e3
+    value = rays_per_frame * frames_timed / elapsed / 1e6
+    achieved = B * shard_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
@@ -245,7 +260,7 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": world, "steps": a.steps,
+            "metric": METRIC, "value": round(value, 3), "unit": "Mray/s", "n_gpus": world, "steps": frames_timed,
             "warmup": a.warmup, "ms_per_step": round(ms_per_frame, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: procedural nomadplains terrain, noise seed 300 (MSVC rand), fixed camera",
@@ -261,10 +276,11 @@ def main():
                 "hit_fraction": round(hits / (W * H), 4),
                 "noise3d_per_frame_tracescreen": shard_noise if world == 1 else None,
                 "parallelism": "single GPU" if world == 1 else f"tile-cyclic 32x32 shards x{world} + RCCL gather",
-                "frames_in_flight": a.frames_in_flight,
+                "frames_in_flight": a.frames_in_flight * B,
+                "batch": B,
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
                               else "direct launches",
-                "frame_latency_ms": round(latency_ms, 4),
+                "frame_latency_ms": round(latency_ms, 4),  # one batch of B frames at a time
             },
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_VECTOR_TFLOPS, "unit": "TFLOP/s",
@@ -273,7 +289,8 @@ def main():
                 "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
                 "timing": "HIP events per launch on its stream, one frame in flight (the last "
                           f"{kn} tracescreen launches of the run)",
-                "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per launch",
+                "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per frame x {B} "
+                             f"frame(s) per launch",
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "
                         "= FP32 dense matrix peak = 157.3 TFLOP/s",
             },

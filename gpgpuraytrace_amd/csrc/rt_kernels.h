@@ -11,6 +11,20 @@ enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2, RT_CTR_FINISH = 3,
 
 enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2, RT_PIPELINE_STAGED = 3 };
 
+// A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by
+// one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
+// block (camera, sun), CameraResults, CellDistance and framebuffer; the kernels find them
+// through this table in device memory.  A single frame is a batch of one.
+#define RT_MAX_BATCH 8
+struct FrameTable {
+    const RtConsts* k[RT_MAX_BATCH];    // tracescreen's constant block
+    const RtConsts* kcam[RT_MAX_BATCH]; // camerarays' constant block (its own cbuffers)
+    float4* cam[RT_MAX_BATCH];   // CameraResults, float4[1024]
+    float2* cells[RT_MAX_BATCH]; // CellDistance, float2[1024]
+    uint32_t* out8[RT_MAX_BATCH];
+    float4* out32[RT_MAX_BATCH]; // may be null
+};
+
 struct RtLaunch {
     hipStream_t stream;
     int landscape;
@@ -31,15 +45,22 @@ struct RtLaunch {
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension)
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
-    uint32_t* order;          // k_primary tile order (rt_split_samples/1024 entries)
+    uint32_t* order;          // k_primary tile order (rt_split_samples/1024 entries per frame)
+    const FrameTable* frames; // device table of the batch's frames (split pipeline, prepass batch)
+    FrameTable frames_host;   // the same pointers on the host (single-frame pipelines)
+    uint32_t n_frames;        // frames in the batch (1..RT_MAX_BATCH)
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);
 void rt_launch_cell_depths(hipStream_t s, const float4* camera_results, float2* cells);
-// Trace the region [off, off+ext) in 32x32-pixel tiles; tiles t (row-major over the
-// region) with t % tile_stride == tile_first are traced (tile-cyclic sharding).
-void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t off_x,
-                           uint32_t off_y, uint32_t ext_x, uint32_t ext_y, uint32_t tile_first, uint32_t tile_stride);
+// the prepass and setTargetDepths of every frame of a.frames (CameraResults -> CellDistance)
+void rt_launch_camerarays_batch(const RtLaunch& a);
+void rt_launch_cell_depths_batch(const RtLaunch& a);
+// Trace the region [off, off+ext) in 32x32-pixel tiles of every frame of a.frames (cells and
+// outputs from the table); tiles t (row-major over the region) with t % tile_stride ==
+// tile_first are traced (tile-cyclic sharding).
+void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, uint32_t ext_x, uint32_t ext_y,
+                           uint32_t tile_first, uint32_t tile_stride);
 
 #define RT_TILE 32
 // samples the split pipeline addresses for a w x h frame: whole 32x32 tiles x AA

@@ -70,23 +70,42 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     c.nz.so32 = (threadIdx.x & 31u) * 8u;
     c.nz.calls = 0;
     c.k = k;
+    c.kf = k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
     c.sun = rtm::mk(k->sun[0], k->sun[1], k->sun[2]);
     return c;
 }
 
+__device__ __forceinline__ float uniform_f(float x)
+{
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
+// prepass frame f of a batch: its camerarays block (camera) as kf, Eye/Sun uniform
+__device__ __forceinline__ Ctx frame_ctx_cam(const Ctx& c, const FrameTable* __restrict__ ft, uint32_t f)
+{
+    Ctx cf = c;
+    cf.kf = ft->kcam[f];
+    cf.eye = rtm::mk(uniform_f(cf.kf->eye[0]), uniform_f(cf.kf->eye[1]), uniform_f(cf.kf->eye[2]));
+    cf.sun = rtm::mk(uniform_f(cf.kf->sun[0]), uniform_f(cf.kf->sun[1]), uniform_f(cf.kf->sun[2]));
+    return cf;
+}
+
 // ---------------------------------------------------------------------------
 // camerarays.hlsl:12-21.  One thread per prepass cell (32x32).
+// ft != null: frame blockIdx.y of a batch (its constants and CameraResults from the table).
 template <int L, bool STATS>
 __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
                                                    const float4* __restrict__ grad, float4* __restrict__ out,
-                                                   RtStats* stats)
+                                                   RtStats* stats, const FrameTable* __restrict__ ft)
 {
+    if (ft) out = ft->cam[blockIdx.y];
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return;
     Ctx c = make_ctx(k, lds);
+    if (ft) c = frame_ctx_cam(c, ft, blockIdx.y);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
     const float r31 = rtm::rcp(31.0f);
     uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
@@ -110,14 +129,16 @@ template <bool STATS, int BS>
 __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restrict__ k,
                                                           const uint32_t* __restrict__ perm2d,
                                                           const float4* __restrict__ grad, float4* __restrict__ out,
-                                                          RtStats* stats)
+                                                          RtStats* stats, const FrameTable* __restrict__ ft)
 {
     constexpr int L = RT_NOMADPLAINS;
+    if (ft) out = ft->cam[blockIdx.y];
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const int i = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
     Ctx c = make_ctx(k, lds);
+    if (ft) c = frame_ctx_cam(c, ft, blockIdx.y);
     const uint32_t j = threadIdx.x & 31u, base = threadIdx.x & 32u;
     const SegOctaves<32> g = seg_octaves<32>(c, j);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
@@ -182,8 +203,13 @@ __device__ __forceinline__ float cd_interp(const float* d, int x, int y)
     return cd_get_depth(d, x, y);
 }
 
-__global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__ cam, float2* __restrict__ cells)
+__global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__ cam, float2* __restrict__ cells,
+                                                     const FrameTable* __restrict__ ft)
 {
+    if (ft) { // frame blockIdx.x of a batch
+        cam = ft->cam[blockIdx.x];
+        cells = ft->cells[blockIdx.x];
+    }
     __shared__ float s_d[RT_CAMERA_RES * RT_CAMERA_RES];
     int i = threadIdx.x;
     s_d[i] = cam[i].w;
@@ -345,8 +371,12 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
 //                the hit list, then the long shadow rays with lane refill.
 //   R k_finish : sky colour of the misses + in-order AA average + UNORM8.
 // Sample t = (u*64 + j)*AA + a: AA sample a of lane-slot j of 8x8 unit u.
+// A batch of n_frames frames: unit g of the launch is unit g % n_units of frame g / n_units
+// (frame-major, so a frame's tail overlaps the next frame's units), and sample ids are
+// global: frame f's sample t is f * frame_samples + t (frame_samples = n_units * 64 * AA).
 struct UnitMap {
     uint32_t off_x, off_y, ext_x, ext_y, tiles32_x, tile_first, tile_stride, n_units;
+    uint32_t n_frames, frame_samples;
 };
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_t lane, uint32_t W, uint32_t H,
@@ -508,9 +538,13 @@ __global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, 
 // graze).  One workgroup buckets the shard's 32x32 tiles by that key (64 buckets,
 // descending); the order only decides which wave takes a unit when, never what
 // it computes.
-__global__ void __launch_bounds__(1024) k_order(const RtConsts* __restrict__ k, const float2* __restrict__ cells,
-                                                UnitMap m, uint32_t* __restrict__ order)
+// One workgroup per frame of the batch; frame f's order at order + f * (n_units / 16).
+__global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
+                                                uint32_t* __restrict__ order)
 {
+    const RtConsts* k = ft->k[blockIdx.x];
+    const float2* cells = ft->cells[blockIdx.x];
+    order += blockIdx.x * (m.n_units >> 4);
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
     for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) {
@@ -679,10 +713,64 @@ struct ShadeHit {
 
 enum { RT_LONG_SHADOW = 0, RT_LONG_AO = 1 };
 
-// tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.
+// frame f's context (f wave-uniform): its constant block (camera, sun) as cf.kf, its Eye and
+// SunDirection in scalar registers; the launch's block c.k stays the source of every
+// frame-invariant constant (scalar loads in the hot loops)
+__device__ __forceinline__ Ctx frame_ctx(const Ctx& c, const FrameTable* __restrict__ ft, uint32_t f)
+{
+    Ctx cf = c;
+    cf.kf = ft->k[f];
+    cf.eye = rtm::mk(uniform_f(cf.kf->eye[0]), uniform_f(cf.kf->eye[1]), uniform_f(cf.kf->eye[2]));
+    cf.sun = rtm::mk(uniform_f(cf.kf->sun[0]), uniform_f(cf.kf->sun[1]), uniform_f(cf.kf->sun[2]));
+    return cf;
+}
+
+// the frame a global sample id belongs to
+__device__ __forceinline__ uint32_t frame_of(const UnitMap& m, uint32_t t)
+{
+    return m.n_frames == 1u ? 0u : t / m.frame_samples;
+}
+
+// body(f) once per distinct frame f among the `valid` lanes, with exactly the lanes of
+// frame f active (f wave-uniform).  A batch of hits or rays mixes frames only around the
+// point where the frame-major unit order moves on to the next frame.
+template <class Body>
+__device__ __forceinline__ void per_frame(bool valid, uint32_t f_lane, Body body)
+{
+    uint64_t pend = __ballot(valid);
+    while (pend) {
+        const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)f_lane, (int)__builtin_ctzll(pend));
+        const bool mine = valid && f_lane == f;
+        pend &= ~__ballot(mine);
+        if (mine) body(f);
+    }
+}
+
+// Per-frame values a long ray needs on its own lane: the frame's Eye (the octave count of
+// every density sample) and its normalised SunDirection (a shadow ray's direction).
+struct FrameRays {
+    float v[RT_MAX_BATCH][6];
+};
+__device__ __forceinline__ void frame_rays_load(FrameRays& s, const FrameTable* __restrict__ ft, uint32_t n_frames)
+{
+    if (threadIdx.x < n_frames) {
+        const RtConsts* k = ft->k[threadIdx.x];
+        const f3 sun = rtm::mk(k->sun[0], k->sun[1], k->sun[2]);
+        const f3 sd = rtm::scale(sun, rtm::rcp(rtm::length(sun))); // tracing.hlsl:60-61
+        s.v[threadIdx.x][0] = k->eye[0];
+        s.v[threadIdx.x][1] = k->eye[1];
+        s.v[threadIdx.x][2] = k->eye[2];
+        s.v[threadIdx.x][3] = sd.x;
+        s.v[threadIdx.x][4] = sd.y;
+        s.v[threadIdx.x][5] = sd.z;
+    }
+}
+
+// tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.  t: the global
+// sample id (buffers), tl: the sample within its frame (pixel).
 template <int L, bool FRESH>
 __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, const float4* __restrict__ res,
-                                              uint32_t t, March<L, true>& st)
+                                              uint32_t t, uint32_t tl, March<L, true>& st)
 {
     const RtConsts* k = c.k;
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
@@ -691,7 +779,7 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     const float4 dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
     h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
     uint32_t px, py, a;
-    sample_pixel(m, t, aa, W, H, &px, &py, &a);
+    sample_pixel(m, tl, aa, W, H, &px, &py, &a);
     h.px = px;
     h.py = py;
     h.a = a;
@@ -784,7 +872,7 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
 // Shading of the hits a fused k_trace could not keep on its CU (hitlist, counter
 // RT_CTR_HITS): finish the short shadows, append the long ones to the global list.
 template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__ k,
+__global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                     const uint32_t* __restrict__ perm2d,
                                                     const float4* __restrict__ grad, UnitMap m,
                                                     const float4* __restrict__ res,
@@ -812,9 +900,11 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
         uint32_t t = 0;
         March<L, true> st;
         ShadeHit h;
-        if (valid) {
-            t = hitlist[i];
-            h = shade_hit<L, false>(c, m, res, t, st);
+        if (valid) t = hitlist[i];
+        per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
+            const Ctx cf = frame_ctx(c, ft, f);
+            h = shade_hit<L, false>(cf, m, res, t, t - f * m.frame_samples, st);
+            c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
@@ -824,7 +914,7 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
                 fin[3u * t + 1u] = h.fog;
                 fin[3u * t + 2u] = h.ray;
             }
-        }
+        });
         const uint64_t lb = __ballot(more);
         if (lb) {
             const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
@@ -853,7 +943,9 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
 // each lane takes the next ray as soon as its own ends.  A retiring lane finishes
 // its sample from fin[t].
 template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+__global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
+                                                 UnitMap m,
+                                                 const uint32_t* __restrict__ perm2d,
                                                  const float4* __restrict__ grad, const float4* __restrict__ shrec,
                                                  const float4* __restrict__ fin, float4* __restrict__ samples,
                                                  uint32_t* __restrict__ aocc, uint32_t long_cap,
@@ -862,11 +954,12 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     const uint32_t n_long = min(__builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]), long_cap);
     if (n_long == 0u) return; // every long shadow ray was marched inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
+    __shared__ FrameRays s_fr;
+    frame_rays_load(s_fr, ft, m.n_frames);
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Ctx c = make_ctx(k, lds);
-    const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
+    Ctx c = make_ctx(k, lds); // c.eye: the lane's ray's frame (set on refill)
     March<L, true> st;
     st.d = 0.0f;
     st.iters = 0;
@@ -904,7 +997,10 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
                     const bool mine = ((idle >> lane) & 1ull) && rank < take;
                     if (mine) {
                         const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
-                        t = long_unpack(r[0], r[1], r[2], sun_dir, st, &type);
+                        t = long_unpack(r[0], r[1], r[2], rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
+                        const float* fr = s_fr.v[frame_of(m, t)];
+                        c.eye = rtm::mk(fr[0], fr[1], fr[2]);
+                        if (type == RT_LONG_SHADOW) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                         live = true; // AO rays start live; shadow rays were live when stored
                     }
                     idle &= ~__ballot(mine);
@@ -1097,8 +1193,9 @@ __device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
 #endif
 
 template <int L, bool STATS, bool SEG>
-__global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                const float4* __restrict__ grad, const float2* __restrict__ cells,
+__global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
+                                                const uint32_t* __restrict__ perm2d,
+                                                const float4* __restrict__ grad,
                                                 UnitMap m, const uint32_t* __restrict__ order,
                                                 float4* __restrict__ res, float4* __restrict__ samples,
                                                 float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
@@ -1108,9 +1205,9 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 uint32_t compact_live, uint32_t seg_live)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
-    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
+    __shared__ FrameRays s_fr;
     __shared__ TraceQueues q;
-    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
+    frame_rays_load(s_fr, ft, m.n_frames);
     if (threadIdx.x == 0) {
         q.lock = 0;
         q.h_head = q.h_tail = 0;
@@ -1121,10 +1218,9 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Ctx c = make_ctx(k, lds);
+    Ctx c = make_ctx(k, lds); // k: frame-invariant constants (per-frame ones: frame_ctx / s_fr)
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
-    const f3 sun_dir = rtm::scale(c.sun, rtm::rcp(rtm::length(c.sun)));
     float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
     uint32_t nhits = 0;
 
@@ -1159,8 +1255,9 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         st.iters = 0;
         bool live = false;
         uint32_t t = 0, type = RT_LONG_SHADOW;
+        Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         for (;;) {
-            if (live && !march_live<L, true, true>(c, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
+            if (live && !march_live<L, true, true>(cl, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
                 long_finish<L, true>(k, fin, samples, aocc, t, type, st);
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 live = false;
@@ -1178,30 +1275,38 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
                 if (((idle >> lane) & 1ull) && rank < take) {
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
-                    t = long_unpack(r[0], r[1], r[2], sun_dir, st, &type);
+                    t = long_unpack(r[0], r[1], r[2], rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
+                    const float* fr = s_fr.v[frame_of(m, t)];
+                    cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
+                    if (type == RT_LONG_SHADOW) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     live = true;
                 }
                 if (lane == 0) q.l_head = head + take;
                 q_unlock(&q.lock, lane);
             }
             const uint64_t lv = __ballot(live);
-            if (lv == 0ull) return;
+            if (lv == 0ull) {
+                c.nz.calls = cl.nz.calls;
+                return;
+            }
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
             if ((uint32_t)__popcll(lv) < compact_live && vload(q.l_tail) == vload(q.l_head) &&
                 vload(q.drained) == 0u) {
                 push_long(live, st, t, type);
+                c.nz.calls = cl.nz.calls;
                 return;
             }
             if constexpr (L == RT_NOMADPLAINS && SEG) {
                 // drained, nothing queued and only a few rays left: finish them in group form
-                if ((uint32_t)__popcll(lv) <= seg_live && vload(q.l_tail) == vload(q.l_head)) {
-                    seg_finish<true>(c, st, live, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0, lane);
+                // (single frames only: a segment marches another lane's ray with its own eye)
+                if (m.n_frames == 1u && (uint32_t)__popcll(lv) <= seg_live && vload(q.l_tail) == vload(q.l_head)) {
+                    seg_finish<true>(cl, st, live, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0, lane);
                     continue;
                 }
             }
-            if (live) march_step<L, true, true>(c, st);
+            if (live) march_step<L, true, true>(cl, st);
         }
     };
 
@@ -1218,8 +1323,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         bool more = false;
         const bool valid = lane < take;
         ShadeHit h;
-        if (valid) {
-            h = shade_hit<L, true>(c, m, res, t, st);
+        per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
+            const Ctx cf = frame_ctx(c, ft, f);
+            h = shade_hit<L, true>(cf, m, res, t, t - f * m.frame_samples, st);
+            c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
@@ -1229,7 +1336,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 fin[3u * t + 1u] = h.fog;
                 fin[3u * t + 2u] = h.ray;
             }
-        }
+        });
         if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // fin[t] is in L2 before the ray is visible
             push_long(more, st, t, RT_LONG_SHADOW);
@@ -1243,38 +1350,39 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     };
 
     // ---- one 8x8 primary unit (as k_primary) ----
-    auto do_unit = [&](uint32_t u) {
+    auto do_unit = [&](uint32_t f, uint32_t u) {
+        const Ctx cf = frame_ctx(c, ft, f);
         uint32_t px, py;
         const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
         const float pxf = (float)px, pyf = (float)py;
         float plane_x = 0.0f;
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-            plane_x = s_plane[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))];
+            plane_x = ft->cells[f][(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))].x;
         }
         for (uint32_t a = 0; a < aa; ++a) {
-            const uint32_t t = (u * 64u + lane) * aa + a;
+            const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
             March<L, true> st;
             st.d = 0.0f;
             bool lv = false;
             if (valid) {
                 f3 p, dir;
-                get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
-                march_begin(c, st, p, plane_x, 1.0f, dir);
+                get_pixel_ray(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
+                march_begin(cf, st, p, plane_x, 1.0f, dir);
                 lv = true;
             }
             __builtin_amdgcn_s_setprio(0);
             for (uint32_t it = 0;; ++it) {
-                lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
+                lv = lv && march_live<L, true, false>(cf, st, RT_CAMERA_FAR, max_steps);
                 const uint64_t lb = __ballot(lv);
                 if (lb == 0ull) break;
                 if constexpr (L == RT_NOMADPLAINS && SEG) {
                     if ((uint32_t)__popcll(lb) <= seg_live) {
-                        seg_finish<false>(c, st, lv, RT_CAMERA_FAR, max_steps, lane);
+                        seg_finish<false>(cf, st, lv, RT_CAMERA_FAR, max_steps, lane);
                         break;
                     }
                 }
-                if (lv) march_step<L, true, false>(c, st);
+                if (lv) march_step<L, true, false>(cf, st);
                 if (it == 96u) __builtin_amdgcn_s_setprio(1);
                 else if (it == 224u) __builtin_amdgcn_s_setprio(2);
                 else if (it == 384u) __builtin_amdgcn_s_setprio(3);
@@ -1307,6 +1415,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 }
             }
         }
+        c.nz.calls = cf.nz.calls;
     };
 
     // First unit of every wave is dealt statically, wave-slot-major (wave w of block b takes
@@ -1338,8 +1447,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             if (lane == 0) atomicAdd(&q.active, 1u);
             const uint32_t qi = first_unit ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
             first_unit = false;
-            if (qi < m.n_units) {
-                do_unit(__builtin_amdgcn_readfirstlane(order[qi >> 4]) * 16u + (qi & 15u));
+            if (qi < m.n_units * m.n_frames) {
+                // frame-major over the batch: frame f's units in its own longest-first order
+                const uint32_t f = __builtin_amdgcn_readfirstlane(qi / m.n_units), ql = qi - f * m.n_units;
+                do_unit(f, __builtin_amdgcn_readfirstlane(order[f * (m.n_units >> 4) + (ql >> 4)]) * 16u + (ql & 15u));
                 WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
             } else if (lane == 0) q.drained = 1u;
             if (lane == 0) atomicSub(&q.active, 1u);
@@ -1377,25 +1488,31 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
 // strided statically (wave w takes units w, w + n_waves, ...): the per-unit work is
 // so short that a shared queue atomic would serialise the whole pass.
 template <bool STATS>
-__global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+__global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0, const FrameTable* __restrict__ ft,
+                                                 const uint32_t* __restrict__ perm2d,
                                                  const float4* __restrict__ grad, UnitMap m,
                                                  const float4* __restrict__ res, const float4* __restrict__ samples,
-                                                 const uint32_t* __restrict__ aocc, uint32_t* __restrict__ out8,
-                                                 float4* __restrict__ out32, uint32_t* __restrict__ counters,
+                                                 const uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                  RtStats* stats)
 {
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
     const uint32_t lane = threadIdx.x & 63u;
-    Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
+    Ctx c0x = make_ctx(k0, lds);
+    const uint32_t W = (uint32_t)k0->width, H = (uint32_t)k0->height, aa = (uint32_t)k0->aa_samples;
     const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t u = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); u < m.n_units; u += n_waves) {
+    const uint32_t total = m.n_units * m.n_frames;
+    for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < total; g += n_waves) {
+        const uint32_t f = __builtin_amdgcn_readfirstlane(g / m.n_units), u = g - f * m.n_units;
+        const Ctx c = frame_ctx(c0x, ft, f);
+        const RtConsts* k = c.k; // frame-invariant
+        uint32_t* out8 = ft->out8[f];
+        float4* out32 = ft->out32[f];
         uint32_t px, py;
         if (!unit_pixel(m, u, lane, W, H, &px, &py)) continue;
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
-            uint32_t t = (u * 64u + lane) * aa + a;
+            uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
             float4 dn = res[3u * t + 2u];
             float4 v;
             if (dn.x > 0.0f) {
@@ -1432,8 +1549,9 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         size_t o = (size_t)py * (size_t)k->width + px;
         out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
         if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
+        c0x.nz.calls = c.nz.calls;
     }
-    if constexpr (STATS) atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+    if constexpr (STATS) atomicAdd(&stats->noise_calls, (unsigned long long)c0x.nz.calls);
 }
 
 // Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
@@ -1482,45 +1600,46 @@ __global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, u
     }
 }
 
+// ft == nullptr: one frame (a.consts -> out); else frames 0..n-1 of the table (blockIdx.y).
 template <int L>
-void launch_camerarays_l(const RtLaunch& a, float4* out)
+void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, uint32_t n)
 {
     if constexpr (L == RT_NOMADPLAINS) {
-        // one 32-lane group per ray; RT_PREPASS_BLOCK=1024 packs 32 rays per CU instead of 8
-        static const bool wide = [] {
-            const char* e = getenv("RT_PREPASS_BLOCK");
-            return e && atoi(e) == 1024;
-        }();
-        if (wide) {
-            dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 32), block(1024);
+        // one 32-lane group per ray.  A block holds the noise tables (one block per CU), so
+        // a batch packs more rays per block to keep every frame's prepass in one dispatch
+        // round: 8 rays (256 threads) up to 2 frames, 16 up to 4, 32 beyond.
+        auto go = [&](auto bs_tag) {
+            constexpr int BS = decltype(bs_tag)::value;
+            dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / (BS / 32), n), block(BS);
             if (a.stats)
-                hipLaunchKernelGGL((k_camerarays_group<true, 1024>), grid, block, 0, a.stream, a.consts, a.perm2d,
-                                   a.grad, out, a.stats);
+                hipLaunchKernelGGL((k_camerarays_group<true, BS>), grid, block, 0, a.stream, a.consts, a.perm2d,
+                                   a.grad, out, a.stats, ft);
             else
-                hipLaunchKernelGGL((k_camerarays_group<false, 1024>), grid, block, 0, a.stream, a.consts, a.perm2d,
-                                   a.grad, out, a.stats);
-            return;
-        }
-        dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 8), block(256);
-        if (a.stats)
-            hipLaunchKernelGGL((k_camerarays_group<true, 256>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               out, a.stats);
-        else
-            hipLaunchKernelGGL((k_camerarays_group<false, 256>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               out, a.stats);
+                hipLaunchKernelGGL((k_camerarays_group<false, BS>), grid, block, 0, a.stream, a.consts, a.perm2d,
+                                   a.grad, out, a.stats, ft);
+        };
+        if (n <= 2) go(std::integral_constant<int, 256>{});
+        else if (n <= 4) go(std::integral_constant<int, 512>{});
+        else go(std::integral_constant<int, 1024>{});
         return;
     }
-    dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64), block(64);
+    dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64, n), block(64);
     if (a.stats)
-        hipLaunchKernelGGL((k_camerarays<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats);
+        hipLaunchKernelGGL((k_camerarays<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats,
+                           ft);
     else
-        hipLaunchKernelGGL((k_camerarays<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats);
+        hipLaunchKernelGGL((k_camerarays<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, out, a.stats,
+                           ft);
 }
 
 template <int L>
-void launch_tracescreen_l(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t ox,
-                          uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first, uint32_t stride)
+void launch_tracescreen_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,
+                          uint32_t stride)
 {
+    // single-frame pipeline: frame 0 of the table
+    const float2* cells = a.frames_host.cells[0];
+    uint32_t* out8 = a.frames_host.out8[0];
+    float4* out32 = a.frames_host.out32[0];
     uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
     if (first >= total) return;
     uint32_t n_tiles = (total - first + stride - 1) / stride;
@@ -1539,9 +1658,10 @@ void launch_tracescreen_l(const RtLaunch& a, const float2* cells, uint32_t* out8
 }
 
 template <int L>
-void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t ox, uint32_t oy,
-                    uint32_t ex, uint32_t ey, uint32_t first, uint32_t stride)
+void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,
+                    uint32_t stride)
 {
+    const float2* cells = a.frames_host.cells[0]; // single-frame primaries (staged, refill)
     UnitMap m;
     uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
     if (first >= total) return;
@@ -1553,8 +1673,10 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     m.tile_first = first;
     m.tile_stride = stride;
     m.n_units = ((total - first + stride - 1) / stride) * 16u;
+    m.n_frames = a.n_frames;
+    m.frame_samples = m.n_units * 64u * (uint32_t)a.aa;
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
-    uint32_t need = (m.n_units + 15u) / 16u;
+    uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
     // scheduler knobs of k_trace (RT_LONG_BATCH / RT_REFILL_IDLE override for experiments)
@@ -1578,35 +1700,38 @@ void launch_split_l(const RtLaunch& a, const float2* cells, uint32_t* out8, floa
     // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
     const char* seg_env = getenv("RT_SEG"); // RT_SEG=0/1 forces it off/on (read per launch: tests flip it)
     const int seg_mode = seg_env ? atoi(seg_env) : -1;
-    const bool seg = L == RT_NOMADPLAINS && tune_seg_live > 0 &&
+    // (single frames only: batches have units enough, and a segment's lanes share one eye)
+    const bool seg = L == RT_NOMADPLAINS && tune_seg_live > 0 && m.n_frames == 1u &&
                      (seg_mode >= 0 ? seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
-    if (a.ao_samples > 0) (void)hipMemsetAsync(a.aocc, 0, (size_t)m.n_units * 64u * a.aa * sizeof(uint32_t), a.stream);
+    if (a.ao_samples > 0)
+        (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
     const int pipe = a.pipeline;
-    if (pipe != RT_PIPELINE_REFILL) hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.consts, cells, m, a.order);
+    if (pipe != RT_PIPELINE_REFILL) hipLaunchKernelGGL(k_order, dim3(m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
     // primary (+ shading in the fused kernel); hits it did not shade go to the global list
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
+        const RtConsts* k0 = a.frames_host.k[0];
         if (pipe == RT_PIPELINE_REFILL)
-            hipLaunchKernelGGL((k_march<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells, m,
+            hipLaunchKernelGGL((k_march<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.perm2d, a.grad, cells, m,
                                a.res, a.hitlist, a.queue, a.stats);
         else if (pipe == RT_PIPELINE_STAGED)
-            hipLaunchKernelGGL((k_primary<L, S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
+            hipLaunchKernelGGL((k_primary<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.perm2d, a.grad, cells,
                                m, a.order, a.res, a.hitlist, a.queue, a.stats);
         else if (seg)
-            hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               cells, m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+            hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
+                               m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
                                a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
         else
-            hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad,
-                               cells, m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+            hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
+                               m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
                                a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
-        hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
+        hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, a.shrec,
+        hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
                            a.fin, a.samples, a.aocc, a.long_cap, a.queue, a.stats);
-        hipLaunchKernelGGL((k_finish<S>), dim3(pblocks), blk, 0, a.stream, a.consts, a.perm2d, a.grad, m, a.res,
-                           a.samples, a.aocc, out8, out32, a.queue, a.stats);
+        hipLaunchKernelGGL((k_finish<S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
+                           a.samples, a.aocc, a.queue, a.stats);
     };
     if (a.stats) primary(std::true_type{});
     else primary(std::false_type{});
@@ -1621,36 +1746,51 @@ void rt_launch_camerarays(const RtLaunch& a, float4* out)
     if (++launches > 8) return;
 #endif
     switch (a.landscape) {
-    case RT_TESTING: launch_camerarays_l<RT_TESTING>(a, out); break;
-    case RT_SIMPLE: launch_camerarays_l<RT_SIMPLE>(a, out); break;
-    case RT_GREENROCKS: launch_camerarays_l<RT_GREENROCKS>(a, out); break;
-    default: launch_camerarays_l<RT_NOMADPLAINS>(a, out); break;
+    case RT_TESTING: launch_camerarays_l<RT_TESTING>(a, out, nullptr, 1u); break;
+    case RT_SIMPLE: launch_camerarays_l<RT_SIMPLE>(a, out, nullptr, 1u); break;
+    case RT_GREENROCKS: launch_camerarays_l<RT_GREENROCKS>(a, out, nullptr, 1u); break;
+    default: launch_camerarays_l<RT_NOMADPLAINS>(a, out, nullptr, 1u); break;
+    }
+}
+
+void rt_launch_camerarays_batch(const RtLaunch& a)
+{
+    switch (a.landscape) {
+    case RT_TESTING: launch_camerarays_l<RT_TESTING>(a, nullptr, a.frames, a.n_frames); break;
+    case RT_SIMPLE: launch_camerarays_l<RT_SIMPLE>(a, nullptr, a.frames, a.n_frames); break;
+    case RT_GREENROCKS: launch_camerarays_l<RT_GREENROCKS>(a, nullptr, a.frames, a.n_frames); break;
+    default: launch_camerarays_l<RT_NOMADPLAINS>(a, nullptr, a.frames, a.n_frames); break;
     }
 }
 
 void rt_launch_cell_depths(hipStream_t s, const float4* cam, float2* cells)
 {
-    hipLaunchKernelGGL(k_cell_depths, dim3(1), dim3(1024), 0, s, cam, cells);
+    hipLaunchKernelGGL(k_cell_depths, dim3(1), dim3(1024), 0, s, cam, cells, nullptr);
 }
 
-void rt_launch_tracescreen(const RtLaunch& a, const float2* cells, uint32_t* out8, float4* out32, uint32_t ox,
-                           uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first, uint32_t stride)
+void rt_launch_cell_depths_batch(const RtLaunch& a)
+{
+    hipLaunchKernelGGL(k_cell_depths, dim3(a.n_frames), dim3(1024), 0, a.stream, nullptr, nullptr, a.frames);
+}
+
+void rt_launch_tracescreen(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,
+                           uint32_t stride)
 {
     if (ex == 0 || ey == 0 || stride == 0) return;
     if (a.pipeline == RT_PIPELINE_MEGA) {
         switch (a.landscape) {
-        case RT_TESTING: launch_tracescreen_l<RT_TESTING>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-        case RT_SIMPLE: launch_tracescreen_l<RT_SIMPLE>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-        case RT_GREENROCKS: launch_tracescreen_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-        default: launch_tracescreen_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+        case RT_TESTING: launch_tracescreen_l<RT_TESTING>(a, ox, oy, ex, ey, first, stride); break;
+        case RT_SIMPLE: launch_tracescreen_l<RT_SIMPLE>(a, ox, oy, ex, ey, first, stride); break;
+        case RT_GREENROCKS: launch_tracescreen_l<RT_GREENROCKS>(a, ox, oy, ex, ey, first, stride); break;
+        default: launch_tracescreen_l<RT_NOMADPLAINS>(a, ox, oy, ex, ey, first, stride); break;
         }
         return;
     }
     switch (a.landscape) {
-    case RT_TESTING: launch_split_l<RT_TESTING>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    case RT_SIMPLE: launch_split_l<RT_SIMPLE>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    case RT_GREENROCKS: launch_split_l<RT_GREENROCKS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
-    default: launch_split_l<RT_NOMADPLAINS>(a, cells, out8, out32, ox, oy, ex, ey, first, stride); break;
+    case RT_TESTING: launch_split_l<RT_TESTING>(a, ox, oy, ex, ey, first, stride); break;
+    case RT_SIMPLE: launch_split_l<RT_SIMPLE>(a, ox, oy, ex, ey, first, stride); break;
+    case RT_GREENROCKS: launch_split_l<RT_GREENROCKS>(a, ox, oy, ex, ey, first, stride); break;
+    default: launch_split_l<RT_NOMADPLAINS>(a, ox, oy, ex, ey, first, stride); break;
     }
 }
 

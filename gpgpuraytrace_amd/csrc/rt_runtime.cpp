@@ -134,6 +134,12 @@ struct rt_device_s {
         hipGraphExec_t exec = nullptr;
     } graph_pre, graph_trace;
     unsigned long long graph_captures = 0, graph_launches = 0;
+    // the batch's frame table (rt_kernels.h FrameTable): device copy + the last uploaded contents
+    FrameTable* d_frames = nullptr;
+    FrameTable frames_last{};
+    bool frames_valid = false;
+    Staging frames_staging;
+    hipEvent_t sync_ev = nullptr; // orders this device's stream against a batch on another device
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -173,6 +179,7 @@ struct rt_texture_s {
     rt_device dev = nullptr;
     int dims = 0, fmt = 0, w = 0, h = 0;
     uint32_t* data = nullptr;
+    uint64_t hash = 0; // FNV-1a of the texels (frame batches check that they share the noise)
 };
 
 struct Shader;
@@ -440,7 +447,22 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.aocc = dev->aocc;
     a.ao_samples = s->ao;
     a.aa = s->aa;
+    a.frames = dev->d_frames;
+    a.frames_host = FrameTable{};
+    a.n_frames = 1;
     return a;
+}
+
+// the frame table the kernels read (uploaded only when its contents change)
+int upload_frames(rt_device dev, const FrameTable& ft)
+{
+    if (!dev->d_frames) HIP_TRY(hipMalloc(&dev->d_frames, sizeof(FrameTable)));
+    if (dev->frames_valid && memcmp(&ft, &dev->frames_last, sizeof(FrameTable)) == 0) return RT_OK;
+    const int rc = dev->frames_staging.upload(dev->stream, dev->d_frames, &ft, sizeof(FrameTable));
+    if (rc) return rc;
+    dev->frames_last = ft;
+    dev->frames_valid = true;
+    return RT_OK;
 }
 
 int check_texture(Shader* s)
@@ -457,9 +479,9 @@ int check_texture(Shader* s)
 // shading inputs of a long shadow ray (48 B) and an AO occlusion count (4 B); the
 // global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
 // (48 B each).
-int ensure_split_buffers(rt_device dev, int aa, int ao)
+int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
-    size_t need = rt_split_samples(dev->width, dev->height, aa);
+    size_t need = rt_split_samples(dev->width, dev->height, aa) * (size_t)n_frames;
     size_t long_need = need * (size_t)(1 + ao);
     if (need <= dev->samples_cap && long_need <= dev->long_cap) return RT_OK;
     need = std::max(need, dev->samples_cap);
@@ -486,7 +508,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao)
     HIP_TRY(hipMalloc(&dev->shrec, long_need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->aocc, need * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * RT_MAX_BATCH * sizeof(uint32_t)));
     dev->samples_cap = need;
     dev->long_cap = long_need;
     return RT_OK;
@@ -578,6 +600,8 @@ void rt_device_destroy(rt_device d)
     if (d->bgrx) (void)hipFree(d->bgrx);
     if (d->recorder) recorder_detach(d->recorder); // the recorder outlives its device: it stops capturing
     if (d->graph_pre.exec) (void)hipGraphExecDestroy(d->graph_pre.exec);
+    if (d->d_frames) (void)hipFree(d->d_frames);
+    if (d->sync_ev) (void)hipEventDestroy(d->sync_ev);
     if (d->graph_trace.exec) (void)hipGraphExecDestroy(d->graph_trace.exec);
     for (auto& pr : d->ev_pool) {
         (void)hipEventDestroy(pr.first);
@@ -740,6 +764,9 @@ int rt_texture_init(rt_texture t, int dims, int fmt, int w, int h, const void* d
     size_t bytes = (size_t)w * h * 4;
     HIP_TRY(hipMalloc(&t->data, bytes));
     HIP_TRY(hipMemcpy(t->data, data, bytes, hipMemcpyHostToDevice));
+    uint64_t hsh = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < bytes; ++i) hsh = (hsh ^ ((const uint8_t*)data)[i]) * 0x100000001b3ull;
+    t->hash = hsh;
     t->dims = dims;
     t->fmt = fmt;
     t->w = w;
@@ -902,7 +929,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     if (rc) return rc;
     rc = sync_shader(dev, s);
     if (rc) return rc;
-    if (s->kind == KIND_TRACESCREEN && (rc = ensure_split_buffers(dev, s->aa, s->ao))) return rc;
+    if (s->kind == KIND_TRACESCREEN && (rc = ensure_split_buffers(dev, s->aa, s->ao, 1))) return rc;
     RtLaunch a = make_launch(dev, s);
     if (dz == 0) return RT_OK;
     if (s->kind == KIND_CAMERARAYS) {
@@ -926,9 +953,16 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
         uint64_t ex = (uint64_t)dx * s->tx, ey = (uint64_t)dy * s->ty;
         ex = std::min<uint64_t>(ex, dev->width > (int)off[0] ? dev->width - off[0] : 0);
         ey = std::min<uint64_t>(ey, dev->height > (int)off[1] ? dev->height - off[1] : 0);
+        FrameTable ft{};
+        ft.k[0] = s->d_consts;
+        ft.cells[0] = (float2*)cd->dev_ptr;
+        ft.out8[0] = dev->fb8;
+        ft.out32[0] = dev->fb32;
+        if ((rc = upload_frames(dev, ft))) return rc;
+        a.frames = dev->d_frames;
+        a.frames_host = ft;
         KernelTimer kt(dev);
-        rt_launch_tracescreen(a, (const float2*)cd->dev_ptr, dev->fb8, dev->fb32, off[0], off[1], (uint32_t)ex,
-                              (uint32_t)ey, 0, 1);
+        rt_launch_tracescreen(a, off[0], off[1], (uint32_t)ex, (uint32_t)ey, 0, 1);
     }
     HIP_TRY(hipGetLastError());
     return RT_OK;
@@ -1002,16 +1036,17 @@ size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
 void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
 
 // ---- Terrain::render on the device -------------------------------------------
-static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count, bool feed);
+static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
+                                int shard_count, bool feed);
 
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
-    return terrain_render(cam, scr, shard_rank, shard_count, false);
+    return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false);
 }
 
 int rt_terrain_render_feed(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
-    return terrain_render(cam, scr, shard_rank, shard_count, true);
+    return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, true);
 }
 
 int rt_terrain_feed_wait(rt_compute cam, float* camera_results)
@@ -1036,7 +1071,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.hitlist,
                           (uint64_t)(uintptr_t)a.shrec, (uint64_t)a.long_cap, (uint64_t)(uintptr_t)a.fin,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
-                          (uint64_t)(uintptr_t)a.order};
+                          (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));
 }
 
@@ -1081,51 +1116,106 @@ int graph_run(rt_device dev, rt_device_s::FrameGraph& g, std::vector<uint64_t>&&
 } // namespace
 } // extern "C++"
 
-static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count, bool feed)
+namespace {
+// every shader of a batch traces frame 0's noise tables: they must hold the same bytes
+bool same_tables(const Shader* a, const Shader* b)
 {
-    if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
-    if (!cam->shader || !scr->shader) return fail(RT_ERR_STATE, "both computes need a current shader (swap)");
-    if (cam->shader->kind != KIND_CAMERARAYS || scr->shader->kind != KIND_TRACESCREEN)
-        return fail(RT_ERR_INVALID, "expected (camerarays, tracescreen)");
+    return a->textures[0]->hash == b->textures[0]->hash && a->cb[CB_NOISE] == b->cb[CB_NOISE];
+}
+
+void key_frames(std::vector<uint64_t>& k, const FrameTable& ft)
+{
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&ft);
+    k.insert(k.end(), w, w + sizeof(FrameTable) / sizeof(uint64_t));
+}
+} // namespace
+
+// Terrain::render (Terrain.cpp:105-136) for n frames at once: every frame's prepass and
+// setTargetDepths in one launch each, then one tracescreen over all frames' units
+// (frame-major), on frame 0's device stream and buffers.  Frames on other devices (a
+// FrameRing's slots) are ordered around the batch with events.
+static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
+                                int shard_count, bool feed)
+{
+    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
-    rt_device dev = cam->dev;
+    if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
     int rc;
-    if ((rc = check_texture(cam->shader)) || (rc = check_texture(scr->shader))) return rc;
-    if ((rc = sync_shader(dev, cam->shader)) || (rc = sync_shader(dev, scr->shader))) return rc;
-    if ((rc = ensure_split_buffers(dev, scr->shader->aa, scr->shader->ao))) return rc;
-    rt_array_s* cr = cam->shader->array("CameraResults");
-    rt_array_s* cd = scr->shader->array("CellDistance");
-    if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
-    float4* crp = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : dev->scratch_cam;
-    const RtLaunch la_cam = make_launch(dev, cam->shader), la_scr = make_launch(dev, scr->shader);
-    float2* cells = (float2*)cd->dev_ptr;
+    FrameTable ft{};
+    rt_device dev = nullptr;
+    const Shader* s0 = nullptr;
+    for (int f = 0; f < n; ++f) {
+        rt_compute cam = cams[f], scr = scrs[f];
+        if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
+        if (!cam->shader || !scr->shader) return fail(RT_ERR_STATE, "both computes need a current shader (swap)");
+        if (cam->shader->kind != KIND_CAMERARAYS || scr->shader->kind != KIND_TRACESCREEN)
+            return fail(RT_ERR_INVALID, "expected (camerarays, tracescreen)");
+        if ((rc = check_texture(cam->shader)) || (rc = check_texture(scr->shader))) return rc;
+        rt_device d = scr->dev;
+        const Shader* s = scr->shader;
+        if (f == 0) {
+            dev = d;
+            s0 = s;
+        } else if (d->ordinal != dev->ordinal || d->width != dev->width || d->height != dev->height ||
+                   s->landscape != s0->landscape || s->aa != s0->aa || s->ao != s0->ao ||
+                   s->max_steps != s0->max_steps || s->recording != s0->recording ||
+                   cam->shader->recording != cams[0]->shader->recording || !same_tables(s, s0) ||
+                   !same_tables(cam->shader, s0)) {
+            return fail(RT_ERR_INVALID, "frame %d: a batch needs one GPU, resolution, landscape, macro set and noise", f);
+        }
+        if ((rc = sync_shader(d, cam->shader)) || (rc = sync_shader(d, scr->shader))) return rc;
+        rt_array_s* cr = cam->shader->array("CameraResults");
+        rt_array_s* cd = scr->shader->array("CellDistance");
+        if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
+        ft.k[f] = scr->shader->d_consts;
+        ft.kcam[f] = cam->shader->d_consts;
+        ft.cam[f] = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : d->scratch_cam;
+        ft.cells[f] = (float2*)cd->dev_ptr;
+        ft.out8[f] = d->fb8;
+        ft.out32[f] = d->fb32;
+    }
+    // frames on other devices: their pending work (constant uploads, readbacks of the
+    // framebuffer) precedes the batch on its stream
+    bool others = false;
+    for (int f = 1; f < n; ++f) {
+        rt_device d = scrs[f]->dev;
+        if (d == dev) continue;
+        others = true;
+        if (!d->sync_ev) HIP_TRY(hipEventCreateWithFlags(&d->sync_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(d->sync_ev, d->stream));
+        HIP_TRY(hipStreamWaitEvent(dev->stream, d->sync_ev, 0));
+    }
+    if ((rc = ensure_split_buffers(dev, s0->aa, s0->ao, n))) return rc;
+    if ((rc = upload_frames(dev, ft))) return rc;
+    RtLaunch la_cam = make_launch(dev, cams[0]->shader), la_scr = make_launch(dev, scrs[0]->shader);
+    la_cam.frames_host = la_scr.frames_host = ft;
+    la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
     const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr;
+    auto pre = [&] {
+        rt_launch_camerarays_batch(la_cam);
+        rt_launch_cell_depths_batch(la_cam);
+    };
     if (graphs) {
-        // the constant uploads (sync_shader) stay outside: they precede the replay on this stream
+        // the constant / table uploads stay outside: they precede the replay on this stream
         std::vector<uint64_t> kp;
         key_launch(kp, la_cam);
-        kp.push_back((uint64_t)(uintptr_t)crp);
-        kp.push_back((uint64_t)(uintptr_t)cells);
-        if ((rc = graph_run(dev, dev->graph_pre, std::move(kp), [&] {
-                 rt_launch_camerarays(la_cam, crp);
-                 rt_launch_cell_depths(dev->stream, crp, cells);
-             })))
-            return rc;
+        key_frames(kp, ft);
+        if ((rc = graph_run(dev, dev->graph_pre, std::move(kp), pre))) return rc;
     } else {
-        rt_launch_camerarays(la_cam, crp);
+        pre();
     }
     if (feed) {
         // Flyby's view of this frame, on the host as soon as the prepass is done
+        rt_compute cam = cams[0];
         if (!cam->feed_host) HIP_TRY(hipHostMalloc(&cam->feed_host, 1024 * sizeof(float4)));
         if (!cam->feed_ev) HIP_TRY(hipEventCreateWithFlags(&cam->feed_ev, hipEventDisableTiming));
-        HIP_TRY(hipMemcpyAsync(cam->feed_host, crp, 1024 * sizeof(float4), hipMemcpyDeviceToHost, dev->stream));
+        HIP_TRY(hipMemcpyAsync(cam->feed_host, ft.cam[0], 1024 * sizeof(float4), hipMemcpyDeviceToHost, dev->stream));
         HIP_TRY(hipEventRecord(cam->feed_ev, dev->stream));
         cam->feed_pending = true;
     }
-    if (!graphs) rt_launch_cell_depths(dev->stream, crp, cells);
     auto trace = [&] {
-        rt_launch_tracescreen(la_scr, cells, dev->fb8, dev->fb32, 0, 0, (uint32_t)dev->width, (uint32_t)dev->height,
-                              (uint32_t)shard_rank, (uint32_t)shard_count);
+        rt_launch_tracescreen(la_scr, 0, 0, (uint32_t)dev->width, (uint32_t)dev->height, (uint32_t)shard_rank,
+                              (uint32_t)shard_count);
     };
     {
         KernelTimer kt(dev);
@@ -1133,9 +1223,9 @@ static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int sh
             std::vector<uint64_t> kt_key;
             key_launch(kt_key, la_scr);
             key_env(kt_key);
-            const uint64_t extra[] = {(uint64_t)(uintptr_t)cells, (uint64_t)(uintptr_t)dev->fb8,
-                                      (uint64_t)(uintptr_t)dev->fb32, (uint64_t)dev->width, (uint64_t)dev->height,
-                                      (uint64_t)shard_rank, (uint64_t)shard_count};
+            key_frames(kt_key, ft);
+            const uint64_t extra[] = {(uint64_t)dev->width, (uint64_t)dev->height, (uint64_t)shard_rank,
+                                      (uint64_t)shard_count};
             kt_key.insert(kt_key.end(), std::begin(extra), std::end(extra));
             if ((rc = graph_run(dev, dev->graph_trace, std::move(kt_key), trace))) return rc;
         } else {
@@ -1143,7 +1233,19 @@ static int terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int sh
         }
     }
     HIP_TRY(hipGetLastError());
+    if (others) {
+        // the other frames' devices see their frames complete in their own stream order
+        if (!dev->sync_ev) HIP_TRY(hipEventCreateWithFlags(&dev->sync_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(dev->sync_ev, dev->stream));
+        for (int f = 1; f < n; ++f)
+            if (scrs[f]->dev != dev) HIP_TRY(hipStreamWaitEvent(scrs[f]->dev->stream, dev->sync_ev, 0));
+    }
     return RT_OK;
+}
+
+int rt_terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count)
+{
+    return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false);
 }
 
 size_t rt_shard_bytes(rt_device d, int rank, int count)

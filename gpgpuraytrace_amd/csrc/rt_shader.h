@@ -130,9 +130,14 @@ __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py
 
 // ---------------------------------------------------------------------------
 // Per-frame state visible to device code (cbuffer contents + derived tables).
+// k: the launch's constant block (a kernel argument, so its loads are scalar); kf: the
+// block of the frame being traced, for the fields that change per frame (ViewInverse, the
+// eye-dependent sky terms; Eye and SunDirection are copied into eye / sun).  kf == k except
+// in frame batches.
 struct Ctx {
     NoiseView nz;
     const RtConsts* k;
+    const RtConsts* kf;
     f3 eye;
     f3 sun;
 };
@@ -549,9 +554,9 @@ __device__ __forceinline__ void get_pixel_ray(const Ctx& c, float px, float py, 
     const RtConsts* k = c.k;
     float sx = fma(px + 0.5f, k->rcp_w, -0.5f) * 2.0f;
     float sy = fma(py + 0.5f, k->rcp_h, -0.5f) * 2.0f;
-    sx = sx * k->proj22;
-    sy = sy * k->proj11;
-    const float* m = k->view_inverse;
+    sx = sx * c.kf->proj22;
+    sy = sy * c.kf->proj11;
+    const float* m = c.kf->view_inverse;
     float r0 = fma(1.0f, m[12], fma(1.0f, m[8], fma(sy, m[4], sx * m[0])));
     float r1 = fma(1.0f, m[13], fma(1.0f, m[9], fma(sy, m[5], sx * m[1])));
     float r2 = fma(1.0f, m[14], fma(1.0f, m[10], fma(sy, m[6], sx * m[2])));
@@ -597,10 +602,11 @@ __device__ __forceinline__ SkyColor get_rayleigh_mie(const Ctx& c, f3 org)
 {
     const RtConsts* k = c.k;
     f3 rd = mod_ray_dir(org);
-    float far = fma((1.0f - rd.y) * k->sky_dist_to_top, 2.0f, k->sky_dist_to_top);
-    f3 start = rtm::mk(k->sky_start[0], k->sky_start[1], k->sky_start[2]);
-    float fStartAngle = rtm::dot(rd, rtm::mk(k->sky_start_n[0], k->sky_start_n[1], k->sky_start_n[2]));
-    float fStartOffset = k->sky_depth0 * sky_scale(fStartAngle);
+    const RtConsts* kf = c.kf;
+    float far = fma((1.0f - rd.y) * kf->sky_dist_to_top, 2.0f, kf->sky_dist_to_top);
+    f3 start = rtm::mk(kf->sky_start[0], kf->sky_start[1], kf->sky_start[2]);
+    float fStartAngle = rtm::dot(rd, rtm::mk(kf->sky_start_n[0], kf->sky_start_n[1], kf->sky_start_n[2]));
+    float fStartOffset = kf->sky_depth0 * sky_scale(fStartAngle);
     float sampleLength = far * k->sky_rcp_samples;
     float scaledLength = sampleLength * k->sky_fscale;
     f3 sampleRay = rtm::scale(rd, sampleLength);

@@ -502,6 +502,19 @@ class Terrain:
         return self.camera_view
 
 
+def render_batch(terrains, shard_rank=0, shard_count=1):
+    """rt_terrain_render_batch: Terrain.render_device for up to 8 Terrains at once (one GPU,
+    one resolution, landscape, macro set and noise).  Each frame lands in its own Device's
+    framebuffer; the work is enqueued on the first terrain's device stream and the others'
+    streams wait for it."""
+    n = len(terrains)
+    for t in terrains:
+        t.update_shaders()
+    cams = (C.c_void_p * n)(*[t.camera_compute._h for t in terrains])
+    scrs = (C.c_void_p * n)(*[t.compute._h for t in terrains])
+    check(lib().rt_terrain_render_batch(cams, scrs, n, shard_rank, shard_count), "terrain_render_batch")
+
+
 def _cbuffer_matrix(m):
     """Bytes of XMMatrixTranspose(M) -- what the engine writes for a float4x4 cbuffer variable."""
     return np.ascontiguousarray(np.asarray(m, np.float32).T)
@@ -528,13 +541,15 @@ class FrameRing:
     leaves idle, instead of waiting for it.  Every frame is still computed in full and
     independently; a slot is reused only after its previous frame (i - depth) has completed on
     that slot's stream.  depth=1 is the reference's one-frame-at-a-time behaviour.
-    graph=True: each slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH)."""
+    graph=True: each slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH).
+    batch=B: a slot is B frames rendered by one rt_terrain_render_batch (B devices, the
+    batch on the first one's stream); render_batch() queues the next B frames."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 graph=False, **terrain_kw):
-        self.depth, self.frame = int(depth), 0
+                 graph=False, batch=1, **terrain_kw):
+        self.depth, self.frame, self.batch = int(depth), 0, int(batch)
         self.slots = []
-        for _ in range(self.depth):
+        for _ in range(self.depth * self.batch):
             dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph)
             if dev is None:
                 raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
@@ -546,10 +561,25 @@ class FrameRing:
                 ter.set_camera(camera)
             ter.set_time_of_day(time_of_day)
             ter.update_shaders()
+            if len(self.slots) % self.batch:  # a batch's devices share the first one's stream
+                dev.set_stream(self.slots[len(self.slots) - len(self.slots) % self.batch][0].stream())
             self.slots.append((dev, ter))
 
     def next_slot(self):
         return self.slots[self.frame % self.depth]
+
+    def render_batch(self, shard_rank=0, shard_count=1, present=True):
+        """Queue the next `batch` frames as one batch on the next slot group; returns their
+        Devices in frame order (each complete once its stream reaches this point)."""
+        g = (self.frame // self.batch) % self.depth
+        group = self.slots[g * self.batch:(g + 1) * self.batch]
+        render_batch([t for _, t in group], shard_rank, shard_count)
+        devs = [d for d, _ in group]
+        if present:
+            for d in devs:
+                d.present()
+        self.frame += self.batch
+        return devs
 
     def render(self, shard_rank=0, shard_count=1, camera=None, present=True):
         """Queue one frame on the next slot; returns its Device (the frame is complete once

@@ -168,6 +168,17 @@ int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank
  * copies it (1024 x float4: hit xyz, depth) to `camera_results`. */
 int rt_terrain_render_feed(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
 int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
+/* rt_terrain_render_batch: rt_terrain_render for n (1..8) frames at once -- frame i is
+ * (camera_cs[i], screen_cs[i]), each with its own constants (camera, sun), CameraResults,
+ * CellDistance and device framebuffer.  All frames must share one GPU, resolution,
+ * landscape, macro set and noise tables.  Every frame's prepass runs in one launch, and one
+ * tracescreen launch traces all frames' units frame-major, so one frame's last rays overlap
+ * the next frame's units instead of idling the GPU.  Enqueued on the stream of frame 0's
+ * device with frame 0's device buffers and counters; streams of frames on other devices
+ * wait for the batch.  No reference counterpart (the reference renders one frame per
+ * Terrain::render); each frame's pixels equal its rt_terrain_render frame bit for bit. */
+int rt_terrain_render_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
+                            int shard_count);
 /* Tile-cyclic shard transport: pack this rank's tiles from the framebuffer into a
  * contiguous device buffer (RGBA8, 32x32-pixel tiles in tile order), or unpack a rank's
  * packed tiles into the framebuffer.  Byte counts from rt_shard_bytes. */

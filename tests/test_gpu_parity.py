@@ -419,6 +419,106 @@ def test_frame_ring_graphs_bitexact():
     ring.destroy()
 
 
+# --- frame batches (rt_terrain_render_batch) ----------------------------------------------
+def _batch(specs, stats=False, graph=False, pipeline="split"):
+    """One (Device, Terrain) per spec, made as the single-frame tests make them."""
+    out = []
+    for spec in specs:
+        land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+        out.append(make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=stats, ao=ao, graph=graph,
+                        pipeline=pipeline))
+    return out
+
+
+def _check_frames(frames, specs):
+    gold = GI.load()
+    for (dev, _), spec in zip(frames, specs):
+        key = GI.frame_key(*spec)
+        assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"]), key
+        assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), key
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_batch_mixed_cameras_bitexact(n):
+    """n frames of two cameras in one batch (hits and long rays of different frames share
+    the kernel's shading batches and rings): every frame equals its golden frame, and the
+    batch's stats are the sum of the frames' oracle counts."""
+    from gpgpuraytrace_amd import engine as E
+    specs = [GI.FRAMES[i % 2] for i in range(n)]  # nomadplains 64x48 reset / lookdown
+    frames = _batch(specs, stats=True)
+    E.render_batch([t for _, t in frames])
+    _check_frames(frames, specs)
+    st = frames[0][0].stats()
+    gold = GI.load()
+    ref = sum(gold[GI.frame_key(*s) + "_stats"].astype(np.int64) for s in specs)
+    prepass = sum(gold[GI.frame_key(*s) + "_stats"][1] for s in specs)
+    assert (st["noise_calls"], st["primary_steps"], st["shadow_steps"], st["hits"], st["prepass_steps"]) == \
+        (ref[0], ref[2], ref[3], ref[5], prepass)
+    for d, _ in frames:
+        d.destroy()
+
+
+@pytest.mark.parametrize("idx", [2, 3, 4, 6, 7, 8, 9, 10], ids=lambda i: GI.frame_key(*GI.FRAMES[i]))
+def test_batch_every_landscape_and_macro_set(idx):
+    """Three frames of one spec per batch: AA 4, step cap, the other landscapes (greenrocks'
+    fog), AO 1/2/4."""
+    from gpgpuraytrace_amd import engine as E
+    specs = [GI.FRAMES[idx]] * 3
+    frames = _batch(specs)
+    E.render_batch([t for _, t in frames])
+    _check_frames(frames, specs)
+    for d, _ in frames:
+        d.destroy()
+
+
+def test_batch_shards_graphs_and_ring():
+    """Batches of 2 frames on 2 tile shards, replayed from graphs, assemble to the golden
+    frames; FrameRing(batch=3) over 2 slot groups."""
+    import torch
+
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]
+    ranks = [_batch(specs, graph=True) for _ in range(2)]
+    bufs = {}
+    for _ in range(2):  # second pass: graph replay
+        for r, frames in enumerate(ranks):
+            E.render_batch([t for _, t in frames], r, 2)
+            for f, (d, _) in enumerate(frames):
+                bufs[r, f] = torch.zeros(E.shard_bytes(d, r, 2), dtype=torch.uint8, device="cuda:0")
+                E.shard_pack(d, r, 2, bufs[r, f].data_ptr())
+                d.synchronize()
+        for f, (d, _) in enumerate(ranks[0]):
+            E.shard_unpack(d, 1, 2, bufs[1, f].data_ptr())
+        for (d, _), spec in zip(ranks[0], specs):  # the shard transport moves the RGBA8 frame
+            assert np.array_equal(d.readback(), GI.load()[GI.frame_key(*spec) + "_rgba8"])
+    assert ranks[0][0][0].graph_info() == (2, 4)
+    for frames in ranks:
+        for d, _ in frames:
+            d.destroy()
+    os.environ["RT_PIPELINE"] = "split"
+    cam = FixedCamera(GI.consts(64, 48, "lookdown"))
+    ring = G.FrameRing(64, 48, depth=2, batch=3, camera=cam)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cam.c["sun"])
+    for _ in range(3):
+        ring.render_batch()
+    ring.synchronize()
+    for dev, _ in ring.slots:
+        assert np.array_equal(dev.readback(), GI.load()[GI.frame_key(*GI.FRAMES[1]) + "_rgba8"])
+    ring.destroy()
+
+
+def test_batch_rejects_mixed_macro_sets():
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    frames = _batch([GI.FRAMES[0]]) + [make(GI.consts(64, 48, "reset"), max_steps=64)]
+    with pytest.raises(G.NativeError):
+        E.render_batch([t for _, t in frames])
+    for d, _ in frames:
+        d.destroy()
+
+
 # --- output path (SURVEY.md §8f row 1): GPU swizzle + recorder --------------------------
 @pytest.mark.parametrize("w,h", [(64, 48), (50, 36)])
 def test_bgrx_readback_bitexact(w, h):
