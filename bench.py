@@ -16,7 +16,7 @@ N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (str
 scaling: the frame is fixed), each rank packs its tiles and one RCCL gather to rank 0
 assembles the frame, which rank 0 unpacks into its framebuffer.
 
-Frames in flight (--frames-in-flight, default 3): the timed loop deals frames round-robin
+Frames in flight (--frames-in-flight, default 2): the timed loop deals frames round-robin
 over D complete frame contexts, each on its own HIP stream (engine.FrameRing), so frame
 i+1's prepass and primary phase fill the CUs that frame i's ray tail leaves idle.  Every
 frame is still computed in full; value / ms_per_step are the steady-state frame rate, and
@@ -72,11 +72,11 @@ def parse():
                     help="BASELINE.json config preset (resolution, step cap, AO rays); explicit flags override")
     ap.add_argument("--max-steps", type=int, default=None, help="primary-march cap (build extension); 0 = reference")
     ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
-    ap.add_argument("--frames-in-flight", type=int, default=3,
+    ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="frame contexts (HIP streams) kept in flight; 1 = one frame at a time (with --batch B: "
                          "batches of B frames in flight)")
-    ap.add_argument("--batch", type=int, default=1,
-                    help="frames per rt_terrain_render_batch launch sequence (1..8); the timed loop renders whole "
+    ap.add_argument("--batch", type=int, default=12,
+                    help="frames per rt_terrain_render_batch launch sequence (1..16); the timed loop renders whole "
                          "batches (steps rounded up to a multiple)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
@@ -174,7 +174,7 @@ def main():
 
     # --- timed: D frames in flight (FrameRing: one full frame context + HIP stream per slot) ---
     camera = G.Camera(W, H, euler=euler)
-    B = max(1, min(8, a.batch))
+    B = max(1, min(16, a.batch))
     ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     packed, gathered = {}, {}
@@ -253,7 +253,7 @@ def main():
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
-            key = f"{W}x{H}_{a.landscape}_{a.pose}_ms{a.max_steps}_ao{a.ao}"
+            key = f"{W}x{H}_{a.landscape}_{a.pose}_ms{a.max_steps}_ao{a.ao}_b{B}"
             traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -287,8 +287,8 @@ def main():
                 "frac": round(achieved / PEAK_FP32_VECTOR_TFLOPS, 4), "traffic": traffic,
                 "kernel": TRACESCREEN_KERNELS.get(os.environ.get("RT_PIPELINE", "split"), TRACESCREEN_KERNELS["split"]),
                 "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
-                "timing": "HIP events per launch on its stream, one frame in flight (the last "
-                          f"{kn} tracescreen launches of the run)",
+                "timing": "HIP events per launch on its stream, one batch in flight (the last "
+                          f"{kn} tracescreen launches of the run; one launch = {B} frames)",
                 "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per frame x {B} "
                              f"frame(s) per launch",
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "

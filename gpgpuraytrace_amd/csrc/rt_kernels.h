@@ -15,7 +15,7 @@ enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2, RT_P
 // one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
 // block (camera, sun), CameraResults, CellDistance and framebuffer; the kernels find them
 // through this table in device memory.  A single frame is a batch of one.
-#define RT_MAX_BATCH 8
+#define RT_MAX_BATCH 16
 struct FrameTable {
     const RtConsts* k[RT_MAX_BATCH];    // tracescreen's constant block
     const RtConsts* kcam[RT_MAX_BATCH]; // camerarays' constant block (its own cbuffers)

@@ -48,9 +48,10 @@ def main(src, dst):
     bench = open(os.path.join(src, "kt_bench.json")).read().strip().splitlines()[-1]
     with open(os.path.join(dst, "kernels.md"), "w") as f:
         f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`\n\n"
-                "All launches of the run.  The timed loop keeps 3 frames in flight, so those launches share the\n"
-                "GPU and each one spans longer than it would alone; the per-launch cost the roofline uses is the\n"
-                "bench's one-frame-in-flight pass, tabulated at the end from the same trace.\n\n")
+                "All launches of the run.  The timed loop keeps several batches of frames in flight, so those\n"
+                "launches share the GPU and each one spans longer than it would alone; the per-launch cost the\n"
+                "roofline uses is the bench's one-batch-in-flight pass, tabulated at the end from the same trace.\n"
+                "One tracescreen launch traces a whole batch (config.batch frames).\n\n")
         f.write("| kernel | calls | avg ms | total ms |\n|---|---:|---:|---:|\n")
         for r in rows:
             f.write(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e6:.4f} | "
@@ -80,7 +81,7 @@ def main(src, dst):
             if n.startswith(("k_finish", "k_tracescreen")) and cur is not None:
                 spans.append((t1 - cur) / 1e6)
         with open(os.path.join(dst, "kernels.md"), "a") as f:
-            f.write(f"\n## Roofline pass: the last {K} tracescreen launches (one frame in flight)\n\n")
+            f.write(f"\n## Roofline pass: the last {K} tracescreen launches (one batch in flight)\n\n")
             f.write("| kernel | calls | avg ms |\n|---|---:|---:|\n")
             for n in sorted(per, key=lambda n: -sum(per[n])):
                 f.write(f"| {n} | {len(per[n])} | {sum(per[n]) / len(per[n]):.4f} |\n")
@@ -91,7 +92,8 @@ def main(src, dst):
     m = pmc_means(src)
     with open(os.path.join(dst, "pmc.md"), "w") as f:
         f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group, "
-                "`bench.py --frames-in-flight 1`: the counters are chip-wide, so no frame may overlap)\n\n")
+                "`bench.py --frames-in-flight 1`: the counters are chip-wide, so no batch may overlap; "
+                "one launch = one batch of frames)\n\n")
         for k in sorted(m):
             f.write(f"## {k}\n\n")
             for c in sorted(m[k]):
@@ -107,7 +109,8 @@ def main(src, dst):
             wr += cs.get("TCC_EA0_WRREQ_sum", 0.0)
     b = json.loads(bench)
     cf = b["config"]
-    key = f"{cf['width']}x{cf['height']}_{cf['landscape']}_{cf['pose']}_ms{cf['max_steps']}_ao{cf.get('ao_samples', 0)}"
+    key = (f"{cf['width']}x{cf['height']}_{cf['landscape']}_{cf['pose']}_ms{cf['max_steps']}_ao{cf.get('ao_samples', 0)}"
+           f"_b{cf.get('batch', 1)}")
     tr[key] = {"hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
                "fetch_size_kib": fetch, "write_size_kib": write,
                "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
