@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=12,
                     help="frames per rt_terrain_render_batch launch sequence (1..16); the timed loop renders whole "
                          "batches (steps rounded up to a multiple)")
+    ap.add_argument("--split-prepass", type=int, default=1,
+                    help="N>1: each rank runs the prepass of B/N frames of a batch and one all-gather shares them "
+                         "(0 = every rank runs every frame's prepass)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
@@ -187,10 +190,29 @@ def main():
                 gathered[g] = [torch.zeros(B * maxb, dtype=torch.uint8, device=f"cuda:{local}") for _ in range(world)]
         group_streams = [torch.cuda.ExternalStream(ring.slots[g * B][0].stream(), device=f"cuda:{local}")
                          for g in range(ring.depth)]
+        # split prepass: rank r runs the prepass of frames [r*chunk, (r+1)*chunk) of each batch and
+        # one all-gather (its own communicator, so it never queues behind the frame gathers)
+        # hands every rank all B frames' CameraResults before its trace
+        chunk = -(-B // world)
+        pre_group = dist.new_group(backend="nccl") if a.split_prepass else None
+        cam_bufs = [torch.zeros(world * chunk * 1024 * 4, dtype=torch.float32, device=f"cuda:{local}")
+                    for _ in range(ring.depth)]
 
     def batch_step():
         g = (ring.frame // B) % ring.depth
-        devs = ring.render_batch(rank if world > 1 else 0, world, present=world == 1)
+        if world > 1 and a.split_prepass:
+            group = ring.slots[g * B:(g + 1) * B]
+            ters = [t for _, t in group]
+            devs = [d for d, _ in group]
+            first = rank * chunk
+            E.prepass_batch(ters, first, max(0, min(B - first, chunk)), cam_bufs[g].data_ptr())
+            with torch.cuda.stream(group_streams[g]):
+                mine = cam_bufs[g][rank * chunk * 4096:(rank + 1) * chunk * 4096]
+                dist.all_gather_into_tensor(cam_bufs[g], mine, group=pre_group)
+            E.trace_batch(ters, rank, world, cam_bufs[g].data_ptr())
+            ring.frame += B
+        else:
+            devs = ring.render_batch(rank if world > 1 else 0, world, present=world == 1)
         if world > 1:
             # one gather per batch rides on the batch's stream, so the other batches keep running
             with torch.cuda.stream(group_streams[g]):
@@ -275,7 +297,9 @@ def main():
                 "shadow_rays": hits, "ao_rays": hits * a.ao, "prepass_rays": 1024,
                 "hit_fraction": round(hits / (W * H), 4),
                 "noise3d_per_frame_tracescreen": shard_noise if world == 1 else None,
-                "parallelism": "single GPU" if world == 1 else f"tile-cyclic 32x32 shards x{world} + RCCL gather",
+                "parallelism": "single GPU" if world == 1 else (
+                    f"tile-cyclic 32x32 shards x{world} + RCCL gather per batch"
+                    + (" + prepass split over ranks (RCCL all-gather of CameraResults)" if a.split_prepass else "")),
                 "frames_in_flight": a.frames_in_flight * B,
                 "batch": B,
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph

@@ -82,6 +82,8 @@ SIGNATURES = {
     "rt_terrain_render": (_i, [_vp, _vp, _i, _i]),
     "rt_terrain_render_feed": (_i, [_vp, _vp, _i, _i]),
     "rt_terrain_render_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i]),
+    "rt_terrain_prepass_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
+    "rt_terrain_trace_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
     "rt_terrain_feed_wait": (_i, [_vp, _vp]),
     "rt_shard_bytes": (_sz, [_vp, _i, _i]),
     "rt_shard_pack": (_i, [_vp, _i, _i, _vp]),

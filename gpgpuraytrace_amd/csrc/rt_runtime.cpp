@@ -134,11 +134,13 @@ struct rt_device_s {
         hipGraphExec_t exec = nullptr;
     } graph_pre, graph_trace;
     unsigned long long graph_captures = 0, graph_launches = 0;
-    // the batch's frame table (rt_kernels.h FrameTable): device copy + the last uploaded contents
-    FrameTable* d_frames = nullptr;
-    FrameTable frames_last{};
-    bool frames_valid = false;
-    Staging frames_staging;
+    // frame tables (rt_kernels.h FrameTable): the batch's, and the split prepass's frame subset
+    struct DevTable {
+        FrameTable* d = nullptr;
+        FrameTable last{};
+        bool valid = false;
+        Staging staging;
+    } table, pre_table;
     hipEvent_t sync_ev = nullptr; // orders this device's stream against a batch on another device
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
@@ -447,21 +449,21 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.aocc = dev->aocc;
     a.ao_samples = s->ao;
     a.aa = s->aa;
-    a.frames = dev->d_frames;
+    a.frames = dev->table.d;
     a.frames_host = FrameTable{};
     a.n_frames = 1;
     return a;
 }
 
-// the frame table the kernels read (uploaded only when its contents change)
-int upload_frames(rt_device dev, const FrameTable& ft)
+// a frame table the kernels read (uploaded only when its contents change)
+int upload_frames(rt_device dev, rt_device_s::DevTable& t, const FrameTable& ft)
 {
-    if (!dev->d_frames) HIP_TRY(hipMalloc(&dev->d_frames, sizeof(FrameTable)));
-    if (dev->frames_valid && memcmp(&ft, &dev->frames_last, sizeof(FrameTable)) == 0) return RT_OK;
-    const int rc = dev->frames_staging.upload(dev->stream, dev->d_frames, &ft, sizeof(FrameTable));
+    if (!t.d) HIP_TRY(hipMalloc(&t.d, sizeof(FrameTable)));
+    if (t.valid && memcmp(&ft, &t.last, sizeof(FrameTable)) == 0) return RT_OK;
+    const int rc = t.staging.upload(dev->stream, t.d, &ft, sizeof(FrameTable));
     if (rc) return rc;
-    dev->frames_last = ft;
-    dev->frames_valid = true;
+    t.last = ft;
+    t.valid = true;
     return RT_OK;
 }
 
@@ -600,7 +602,8 @@ void rt_device_destroy(rt_device d)
     if (d->bgrx) (void)hipFree(d->bgrx);
     if (d->recorder) recorder_detach(d->recorder); // the recorder outlives its device: it stops capturing
     if (d->graph_pre.exec) (void)hipGraphExecDestroy(d->graph_pre.exec);
-    if (d->d_frames) (void)hipFree(d->d_frames);
+    if (d->table.d) (void)hipFree(d->table.d);
+    if (d->pre_table.d) (void)hipFree(d->pre_table.d);
     if (d->sync_ev) (void)hipEventDestroy(d->sync_ev);
     if (d->graph_trace.exec) (void)hipGraphExecDestroy(d->graph_trace.exec);
     for (auto& pr : d->ev_pool) {
@@ -958,8 +961,8 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
         ft.cells[0] = (float2*)cd->dev_ptr;
         ft.out8[0] = dev->fb8;
         ft.out32[0] = dev->fb32;
-        if ((rc = upload_frames(dev, ft))) return rc;
-        a.frames = dev->d_frames;
+        if ((rc = upload_frames(dev, dev->table, ft))) return rc;
+        a.frames = dev->table.d;
         a.frames_host = ft;
         KernelTimer kt(dev);
         rt_launch_tracescreen(a, off[0], off[1], (uint32_t)ex, (uint32_t)ey, 0, 1);
@@ -1036,8 +1039,10 @@ size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
 void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
 
 // ---- Terrain::render on the device -------------------------------------------
+enum { PH_PRE = 1, PH_TRACE = 2 };
 static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
-                                int shard_count, bool feed);
+                                int shard_count, bool feed, int phases = PH_PRE | PH_TRACE, int first = 0,
+                                int count = -1, float4* camera_out = nullptr, const float4* camera_in = nullptr);
 
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
@@ -1128,22 +1133,22 @@ void key_frames(std::vector<uint64_t>& k, const FrameTable& ft)
     const uint64_t* w = reinterpret_cast<const uint64_t*>(&ft);
     k.insert(k.end(), w, w + sizeof(FrameTable) / sizeof(uint64_t));
 }
-} // namespace
 
-// Terrain::render (Terrain.cpp:105-136) for n frames at once: every frame's prepass and
-// setTargetDepths in one launch each, then one tracescreen over all frames' units
-// (frame-major), on frame 0's device stream and buffers.  Frames on other devices (a
-// FrameRing's slots) are ordered around the batch with events.
-static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
-                                int shard_count, bool feed)
-{
-    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
-    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
-    if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
-    int rc;
+// A validated batch: its frame table, the device it runs on (frame 0's: stream, buffers,
+// counters) and whether frames live on other devices.
+struct Batch {
     FrameTable ft{};
     rt_device dev = nullptr;
     const Shader* s0 = nullptr;
+    bool others = false;
+};
+
+// Check the n (camerarays, tracescreen) pairs, upload their constants, build the frame table
+// and order the other frames' device streams before the batch.
+int batch_begin(const rt_compute* cams, const rt_compute* scrs, int n, Batch& b)
+{
+    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
+    int rc;
     for (int f = 0; f < n; ++f) {
         rt_compute cam = cams[f], scr = scrs[f];
         if (!cam || !scr || cam->dev != scr->dev) return fail(RT_ERR_INVALID, "computes must share a device");
@@ -1154,45 +1159,111 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
         rt_device d = scr->dev;
         const Shader* s = scr->shader;
         if (f == 0) {
-            dev = d;
-            s0 = s;
-        } else if (d->ordinal != dev->ordinal || d->width != dev->width || d->height != dev->height ||
-                   s->landscape != s0->landscape || s->aa != s0->aa || s->ao != s0->ao ||
-                   s->max_steps != s0->max_steps || s->recording != s0->recording ||
-                   cam->shader->recording != cams[0]->shader->recording || !same_tables(s, s0) ||
-                   !same_tables(cam->shader, s0)) {
+            b.dev = d;
+            b.s0 = s;
+        } else if (d->ordinal != b.dev->ordinal || d->width != b.dev->width || d->height != b.dev->height ||
+                   s->landscape != b.s0->landscape || s->aa != b.s0->aa || s->ao != b.s0->ao ||
+                   s->max_steps != b.s0->max_steps || s->recording != b.s0->recording ||
+                   cam->shader->recording != cams[0]->shader->recording || !same_tables(s, b.s0) ||
+                   !same_tables(cam->shader, b.s0)) {
             return fail(RT_ERR_INVALID, "frame %d: a batch needs one GPU, resolution, landscape, macro set and noise", f);
         }
         if ((rc = sync_shader(d, cam->shader)) || (rc = sync_shader(d, scr->shader))) return rc;
         rt_array_s* cr = cam->shader->array("CameraResults");
         rt_array_s* cd = scr->shader->array("CellDistance");
         if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
-        ft.k[f] = scr->shader->d_consts;
-        ft.kcam[f] = cam->shader->d_consts;
-        ft.cam[f] = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : d->scratch_cam;
-        ft.cells[f] = (float2*)cd->dev_ptr;
-        ft.out8[f] = d->fb8;
-        ft.out32[f] = d->fb32;
+        b.ft.k[f] = scr->shader->d_consts;
+        b.ft.kcam[f] = cam->shader->d_consts;
+        b.ft.cam[f] = (cr->dev_ptr && cr->elements >= 1024) ? (float4*)cr->dev_ptr : d->scratch_cam;
+        b.ft.cells[f] = (float2*)cd->dev_ptr;
+        b.ft.out8[f] = d->fb8;
+        b.ft.out32[f] = d->fb32;
     }
     // frames on other devices: their pending work (constant uploads, readbacks of the
     // framebuffer) precedes the batch on its stream
-    bool others = false;
     for (int f = 1; f < n; ++f) {
         rt_device d = scrs[f]->dev;
-        if (d == dev) continue;
-        others = true;
+        if (d == b.dev) continue;
+        b.others = true;
         if (!d->sync_ev) HIP_TRY(hipEventCreateWithFlags(&d->sync_ev, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(d->sync_ev, d->stream));
-        HIP_TRY(hipStreamWaitEvent(dev->stream, d->sync_ev, 0));
+        HIP_TRY(hipStreamWaitEvent(b.dev->stream, d->sync_ev, 0));
     }
-    if ((rc = ensure_split_buffers(dev, s0->aa, s0->ao, n))) return rc;
-    if ((rc = upload_frames(dev, ft))) return rc;
+    return RT_OK;
+}
+
+// the other frames' devices see their frames complete in their own stream order
+int batch_end(const rt_compute* scrs, int n, Batch& b)
+{
+    HIP_TRY(hipGetLastError());
+    if (!b.others) return RT_OK;
+    rt_device dev = b.dev;
+    if (!dev->sync_ev) HIP_TRY(hipEventCreateWithFlags(&dev->sync_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(dev->sync_ev, dev->stream));
+    for (int f = 1; f < n; ++f)
+        if (scrs[f]->dev != dev) HIP_TRY(hipStreamWaitEvent(scrs[f]->dev->stream, dev->sync_ev, 0));
+    return RT_OK;
+}
+
+} // namespace
+
+// Terrain::render (Terrain.cpp:105-136) for n frames at once: every frame's prepass and
+// setTargetDepths in one launch each, then one tracescreen over all frames' units
+// (frame-major), on frame 0's device stream and buffers.  Frames on other devices (a
+// FrameRing's slots) are ordered around the batch with events.  Phases: PRE = prepass,
+// TRACE = setTargetDepths + tracescreen; `first`/`count` select the prepass frames,
+// camera_out / camera_in redirect CameraResults through a contiguous device buffer
+// (n x 1024 float4) for the split prepass of rt_terrain_prepass_batch / rt_terrain_trace_batch.
+static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
+                                int shard_count, bool feed, int phases, int first, int count, float4* camera_out,
+                                const float4* camera_in)
+{
+    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
+    if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
+    int rc;
+    Batch b;
+    if ((rc = batch_begin(cams, scrs, n, b))) return rc;
+    rt_device dev = b.dev;
+    FrameTable& ft = b.ft;
+    if (count < 0) count = n;
+    if (first < 0 || count > n || first > n - count) return fail(RT_ERR_INVALID, "bad prepass frame range");
+    const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr && phases == (PH_PRE | PH_TRACE);
+    if (camera_in) {
+        // gathered prepass results: the table reads them, and each frame's CameraResults
+        // array receives its copy (Terrain::getCameraView stays valid)
+        for (int f = 0; f < n; ++f) {
+            const float4* src = camera_in + (size_t)f * 1024;
+            if (ft.cam[f] != scrs[f]->dev->scratch_cam)
+                HIP_TRY(hipMemcpyAsync(ft.cam[f], src, 1024 * sizeof(float4), hipMemcpyDeviceToDevice, dev->stream));
+            ft.cam[f] = const_cast<float4*>(src);
+        }
+    }
+    if ((rc = ensure_split_buffers(dev, b.s0->aa, b.s0->ao, n))) return rc;
     RtLaunch la_cam = make_launch(dev, cams[0]->shader), la_scr = make_launch(dev, scrs[0]->shader);
+    if (phases & PH_PRE) {
+        if (phases == PH_PRE) {
+            // the prepass of frames [first, first + count) only, on its own table
+            if (count == 0) return batch_end(scrs, n, b);
+            FrameTable sub{};
+            for (int i = 0; i < count; ++i) {
+                sub.k[i] = ft.k[first + i];
+                sub.kcam[i] = ft.kcam[first + i];
+                sub.cam[i] = camera_out ? camera_out + (size_t)(first + i) * 1024 : ft.cam[first + i];
+            }
+            if ((rc = upload_frames(dev, dev->pre_table, sub))) return rc;
+            la_cam.frames = dev->pre_table.d;
+            la_cam.frames_host = sub;
+            la_cam.n_frames = (uint32_t)count;
+            rt_launch_camerarays_batch(la_cam);
+            return batch_end(scrs, n, b);
+        }
+    }
+    if ((rc = upload_frames(dev, dev->table, ft))) return rc;
+    la_cam.frames = la_scr.frames = dev->table.d;
     la_cam.frames_host = la_scr.frames_host = ft;
     la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
-    const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr;
     auto pre = [&] {
-        rt_launch_camerarays_batch(la_cam);
+        if (phases & PH_PRE) rt_launch_camerarays_batch(la_cam);
         rt_launch_cell_depths_batch(la_cam);
     };
     if (graphs) {
@@ -1232,20 +1303,26 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             trace();
         }
     }
-    HIP_TRY(hipGetLastError());
-    if (others) {
-        // the other frames' devices see their frames complete in their own stream order
-        if (!dev->sync_ev) HIP_TRY(hipEventCreateWithFlags(&dev->sync_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(dev->sync_ev, dev->stream));
-        for (int f = 1; f < n; ++f)
-            if (scrs[f]->dev != dev) HIP_TRY(hipStreamWaitEvent(scrs[f]->dev->stream, dev->sync_ev, 0));
-    }
-    return RT_OK;
+    return batch_end(scrs, n, b);
 }
 
 int rt_terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count)
 {
     return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false);
+}
+
+int rt_terrain_prepass_batch(const rt_compute* cams, const rt_compute* scrs, int n, int first, int count,
+                             void* camera_out)
+{
+    return terrain_render_batch(cams, scrs, n, 0, 1, false, PH_PRE, first, count, (float4*)camera_out);
+}
+
+int rt_terrain_trace_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count,
+                           const void* camera_in)
+{
+    if (!camera_in) return fail(RT_ERR_INVALID, "camera_in: the batch's gathered CameraResults");
+    return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, PH_TRACE, 0, -1, nullptr,
+                                (const float4*)camera_in);
 }
 
 size_t rt_shard_bytes(rt_device d, int rank, int count)

@@ -515,6 +515,27 @@ def render_batch(terrains, shard_rank=0, shard_count=1):
     check(lib().rt_terrain_render_batch(cams, scrs, n, shard_rank, shard_count), "terrain_render_batch")
 
 
+def _batch_handles(terrains):
+    n = len(terrains)
+    for t in terrains:
+        t.update_shaders()
+    return n, (C.c_void_p * n)(*[t.camera_compute._h for t in terrains]), (C.c_void_p * n)(*[t.compute._h for t in terrains])
+
+
+def prepass_batch(terrains, first, count, camera_out_ptr):
+    """rt_terrain_prepass_batch: the prepass of frames [first, first + count) of the batch, frame
+    f's CameraResults to camera_out_ptr + f * 16 KiB (device memory)."""
+    n, cams, scrs = _batch_handles(terrains)
+    check(lib().rt_terrain_prepass_batch(cams, scrs, n, first, count, camera_out_ptr), "terrain_prepass_batch")
+
+
+def trace_batch(terrains, shard_rank, shard_count, camera_in_ptr):
+    """rt_terrain_trace_batch: setTargetDepths + tracescreen of the batch from gathered
+    CameraResults (frame f at camera_in_ptr + f * 16 KiB)."""
+    n, cams, scrs = _batch_handles(terrains)
+    check(lib().rt_terrain_trace_batch(cams, scrs, n, shard_rank, shard_count, camera_in_ptr), "terrain_trace_batch")
+
+
 def _cbuffer_matrix(m):
     """Bytes of XMMatrixTranspose(M) -- what the engine writes for a float4x4 cbuffer variable."""
     return np.ascontiguousarray(np.asarray(m, np.float32).T)

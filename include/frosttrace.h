@@ -179,6 +179,17 @@ int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
  * Terrain::render); each frame's pixels equal its rt_terrain_render frame bit for bit. */
 int rt_terrain_render_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
                             int shard_count);
+/* The same batch in two phases, for a prepass split across ranks (one process per GPU):
+ * rt_terrain_prepass_batch runs the camerarays prepass of frames [first, first + count) only
+ * and writes frame f's 1024 CameraResults to camera_out + f * 1024 float4 (a device buffer of
+ * n * 16 KiB); the ranks' shares are then exchanged with one all-gather of that buffer, and
+ * rt_terrain_trace_batch runs setTargetDepths + tracescreen of all n frames from camera_in
+ * (the gathered buffer), copying each frame's results into its CameraResults array too.
+ * The prepass is deterministic, so the frames equal rt_terrain_render_batch's bit for bit. */
+int rt_terrain_prepass_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int first, int count,
+                             void* camera_out);
+int rt_terrain_trace_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
+                           int shard_count, const void* camera_in);
 /* Tile-cyclic shard transport: pack this rank's tiles from the framebuffer into a
  * contiguous device buffer (RGBA8, 32x32-pixel tiles in tile order), or unpack a rank's
  * packed tiles into the framebuffer.  Byte counts from rt_shard_bytes. */

@@ -24,6 +24,10 @@ def main():
     ap.add_argument("--depth", type=int, default=2)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--ranks", default="all", help="'all' or 'first' (rank 0 only: quick)")
+    ap.add_argument("--split-prepass", type=int, default=0,
+                    help="1: rank r runs only its ceil(B/N) frames' prepass (bench.py --split-prepass; the "
+                         "all-gather is not simulated: the other frames' CameraResults come from a full prepass "
+                         "run once before timing)")
     a = ap.parse_args()
     import torch
     import gpgpuraytrace_amd as G
@@ -33,23 +37,40 @@ def main():
     for B in [int(x) for x in a.batches.split(",")]:
         ring = G.FrameRing(W, H, depth=a.depth, batch=B, camera=cam, time_of_day=0.3, max_steps=a.max_steps,
                            ao_samples=a.ao)
+        bufs = []
+        for g in range(a.depth):
+            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
+            bufs.append(torch.zeros(B * 1024 * 4, dtype=torch.float32, device="cuda:0"))
+            G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
+        torch.cuda.synchronize()
+
+        def step(r, n):
+            if not a.split_prepass or n == 1:
+                ring.render_batch(r, n, present=False)
+                return
+            g = (ring.frame // B) % ring.depth
+            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
+            chunk = -(-B // n)
+            G.engine.prepass_batch(ters, r * chunk, max(0, min(B - r * chunk, chunk)), bufs[g].data_ptr())
+            G.engine.trace_batch(ters, r, n, bufs[g].data_ptr())
+            ring.frame += B
         for n in [int(x) for x in a.ns.split(",")]:
             worst, per = 0.0, []
             for r in (range(n) if a.ranks == "all" else [0]):
                 for _ in range(2 * a.depth):
-                    ring.render_batch(r, n, present=False)
+                    step(r, n)
                 torch.cuda.synchronize()
                 nb = max(1, a.frames // B)
                 t0 = time.perf_counter()
                 for _ in range(nb):
-                    ring.render_batch(r, n, present=False)
+                    step(r, n)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / (nb * B) * 1e3
                 per.append(round(ms, 4))
                 worst = max(worst, ms)
             if base is None:
                 base = worst
-            print(json.dumps({"batch": B, "depth": a.depth, "n": n, "worst_frame_ms": round(worst, 4),
+            print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()
 

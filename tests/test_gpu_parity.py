@@ -509,6 +509,31 @@ def test_batch_shards_graphs_and_ring():
     ring.destroy()
 
 
+def test_batch_split_prepass_bitexact():
+    """rt_terrain_prepass_batch in three ranks' shares into one buffer (what the all-gather
+    produces), then rt_terrain_trace_batch from it: the golden frames, and every frame's
+    CameraResults array holds its golden prepass."""
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    specs = [GI.FRAMES[i % 2] for i in range(5)]
+    frames = _batch(specs, stats=True)
+    ters = [t for _, t in frames]
+    buf = torch.full((len(specs), 1024, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    for first, count in ((0, 2), (2, 2), (4, 1), (5, 0)):
+        E.prepass_batch(ters, first, count, buf.data_ptr())
+    E.trace_batch(ters, 0, 1, buf.data_ptr())
+    _check_frames(frames, specs)
+    gold = GI.load()
+    for (d, t), spec in zip(frames, specs):
+        t.get_camera_results()
+        assert np.array_equal(t.camera_view, gold[GI.frame_key(*spec) + "_camera_results"])
+    st = frames[0][0].stats()
+    assert st["prepass_steps"] == sum(gold[GI.frame_key(*s) + "_stats"][1] for s in specs)
+    for d, _ in frames:
+        d.destroy()
+
+
 def test_batch_rejects_mixed_macro_sets():
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
