@@ -534,6 +534,32 @@ def test_batch_split_prepass_bitexact():
         d.destroy()
 
 
+@pytest.mark.parametrize("ao,ms", [(1, 512), (0, 0)], ids=["c3", "ref"])
+def test_batch_1080p_equals_single_frames(ao, ms):
+    """Full-size frames (the bench's workload, overflow lists in use): a 3-frame batch mixing
+    the reset and look-down poses equals the same frames rendered one at a time, pixel for
+    pixel, and the batch's counts are the sum of theirs."""
+    from gpgpuraytrace_amd import engine as E
+    poses = ["reset", "lookdown", "reset"]
+    singles, ref_stats = [], []
+    for pose in poses:
+        dev, ter = make(GI.consts(1920, 1080, pose), max_steps=ms, ao=ao, stats=True)
+        ter.render_device()
+        singles.append((dev.readback_float(), dev.readback()))
+        ref_stats.append(dev.stats())
+        dev.destroy()
+    frames = [make(GI.consts(1920, 1080, pose), max_steps=ms, ao=ao, stats=True) for pose in poses]
+    E.render_batch([t for _, t in frames])
+    for (dev, _), (f32, f8) in zip(frames, singles):
+        assert bits_equal(dev.readback_float(), f32)
+        assert np.array_equal(dev.readback(), f8)
+    st = frames[0][0].stats()
+    for key in ("noise_calls", "primary_steps", "shadow_steps", "ao_steps", "hits", "prepass_steps"):
+        assert st[key] == sum(r[key] for r in ref_stats), key
+    for d, _ in frames:
+        d.destroy()
+
+
 def test_batch_rejects_mixed_macro_sets():
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
