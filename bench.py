@@ -85,6 +85,9 @@ def parse():
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true",
+                    help="after the timed loop rank 0 checks every assembled frame of the last batch against a "
+                         "whole-frame render on one device (RGBA8, bit for bit); adds config.verify")
     ap.add_argument("--cpu-row-step", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01", "traffic.json"),
@@ -134,9 +137,32 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on one GPU (RT_BENCH_SAME_GPU=1: every rank on cuda:0, with
+    # RT_DIST_BACKEND=gloo: collectives staged through host memory); the default is RCCL
+    backend = os.environ.get("RT_DIST_BACKEND", "nccl")
+    if os.environ.get("RT_BENCH_SAME_GPU") == "1":
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
     torch.cuda.set_device(local)
+
+    def all_gather(out, mine, group):
+        if backend == "nccl":
+            dist.all_gather_into_tensor(out, mine, group=group)
+            return
+        parts = [torch.empty(mine.numel(), dtype=mine.dtype) for _ in range(world)]
+        dist.all_gather(parts, mine.cpu(), group=group)
+        out.copy_(torch.cat(parts).to(out.device))
+
+    def gather(t, outs):
+        if backend == "nccl":
+            dist.gather(t, outs if rank == 0 else None, dst=0)
+            return
+        lst = [torch.empty(t.numel(), dtype=t.dtype) for _ in range(world)] if rank == 0 else None
+        dist.gather(t.cpu(), lst, dst=0)
+        if rank == 0:
+            for o, part in zip(outs, lst):
+                o.copy_(part.to(o.device))
 
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
@@ -194,7 +220,7 @@ def main():
         # one all-gather (its own communicator, so it never queues behind the frame gathers)
         # hands every rank all B frames' CameraResults before its trace
         chunk = -(-B // world)
-        pre_group = dist.new_group(backend="nccl") if a.split_prepass else None
+        pre_group = dist.new_group(backend=backend) if a.split_prepass else None
         cam_bufs = [torch.zeros(world * chunk * 1024 * 4, dtype=torch.float32, device=f"cuda:{local}")
                     for _ in range(ring.depth)]
 
@@ -208,7 +234,7 @@ def main():
             E.prepass_batch(ters, first, max(0, min(B - first, chunk)), cam_bufs[g].data_ptr())
             with torch.cuda.stream(group_streams[g]):
                 mine = cam_bufs[g][rank * chunk * 4096:(rank + 1) * chunk * 4096]
-                dist.all_gather_into_tensor(cam_bufs[g], mine, group=pre_group)
+                all_gather(cam_bufs[g], mine, pre_group)
             E.trace_batch(ters, rank, world, cam_bufs[g].data_ptr())
             ring.frame += B
         else:
@@ -219,7 +245,7 @@ def main():
                 # (a batch's devices share its stream: FrameRing)
                 for f, dev in enumerate(devs):
                     E.shard_pack(dev, rank, world, packed[g].data_ptr() + f * maxb)
-                dist.gather(packed[g], gathered[g] if rank == 0 else None, dst=0)
+                gather(packed[g], gathered[g] if rank == 0 else None)
                 if rank == 0:
                     for r in range(1, world):
                         for f, dev in enumerate(devs):
@@ -244,6 +270,16 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    verify = None
+    if a.verify and rank == 0:
+        # the last timed batch's frames, assembled from every rank's shards, against one whole frame
+        g_last = ((ring.frame // B) - 1) % ring.depth
+        vdev, vter = make(stats=False)
+        vter.render_device(0, 1)
+        want = vdev.readback()
+        vdev.destroy()
+        verify = all(np.array_equal(d.readback(), want) for d, _ in ring.slots[g_last * B:(g_last + 1) * B])
+
     # --- roofline pass: the same batches one at a time on slot group 0 (launches do not overlap),
     # HIP events around every tracescreen launch on the stream it runs on; also the latency ---
     group0 = ring.slots[:B]
@@ -263,7 +299,8 @@ def main():
     ring.set_profiling(False)
     k_avg_ms = kms / max(1, kn)  # one launch = a batch of B frames
     if world > 1:
-        t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed, latency_ms], dtype=torch.float64,
+                         device=f"cuda:{local}" if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, latency_ms = float(t[0].item()), float(t[1].item())
 
@@ -305,6 +342,8 @@ def main():
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
                               else "direct launches",
                 "frame_latency_ms": round(latency_ms, 4),  # one batch of B frames at a time
+                **({"verify": "frames equal a whole-frame render" if verify else "MISMATCH"}
+                   if verify is not None else {}),
             },
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_VECTOR_TFLOPS, "unit": "TFLOP/s",
