@@ -179,6 +179,26 @@ __device__ __forceinline__ int np_octaves(const Ctx& c, f3 p)
     return n;
 }
 
+// The four terrace subtractions of nomadplains/terrain.hlsl:30-37.  t = saturate((y - h) *
+// steep) is +0 wherever (y - 13) * steep <= 0 (steep == 0, or y <= 13 <= h), and then
+// fma(-(t*t), floorsize, s) == s bit for bit (s + -0 == s, also for s == +-0): a wave none of
+// whose samples has (y - 13) * steep > 0 skips all four.
+__device__ __forceinline__ float terraces(float s, float y, float steep)
+{
+    if (!__ballot((y - 13.0f) * steep > 0.0f)) return s;
+    const float floorsize = steep * 1.8f;
+    float t;
+    t = rtm::sat((y - 13.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((y - 16.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((y - 19.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    t = rtm::sat((y - 22.0f) * steep);
+    s = fma(-(t * t), floorsize, s);
+    return s;
+}
+
 // Media/nomadplains/shaders/terrain.hlsl:8-39
 __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 {
@@ -196,16 +216,7 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     }
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((noise3d(c.nz, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f) - 0.2f) * 6.0f) * 7.5f;
-    float floorsize = steep * 1.8f;
-    float t;
-    t = rtm::sat((p1.y - 13.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 16.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 19.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 22.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
+    s = terraces(s, p1.y, steep);
     s = fma(rtm::pow_nonneg(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
     return d + s;
 }
@@ -281,16 +292,7 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
     *octaves = (uint32_t)n_oct;
     s = rtm::pow_nonneg_flat(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
     float steep = rtm::sat((on[0] - 0.2f) * 6.0f) * 7.5f;
-    float floorsize = steep * 1.8f;
-    float t;
-    t = rtm::sat((p1.y - 13.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 16.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 19.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
-    t = rtm::sat((p1.y - 22.0f) * steep);
-    s = fma(-(t * t), floorsize, s);
+    s = terraces(s, p1.y, steep);
     // floor lift: pow(0, 1.5) == 0 exactly, so a wave whose bases are all 0 (every
     // sample above y = 25, the common case) skips the polynomial
     const float lb = rtm::sat((-p1.y + 10.0f) * 1.6f);
