@@ -32,6 +32,9 @@ using rtm::fma;
 //           v_perm_b32 addresses both loads (ds_read_b64 ... offset:32768); the b128
 //           loads are conflict-free however random the indices, the b64 loads 2-way.
 //           RT_GZ16=0: gz[i*32 + (s&31)] (8 B slots, conflict-free, own address).
+#ifndef RT_PAIR_SERIAL
+#define RT_PAIR_SERIAL 1
+#endif
 #ifndef RT_GZ16
 #define RT_GZ16 1
 #endif
@@ -73,15 +76,12 @@ __device__ __forceinline__ v2f gdot2(const float4& gxy, const float2& gz, float 
     return vfma(v2(gz.x, gz.y), zz, r);
 }
 
-// noise.hlsl:153-179 (live `#if 1` block); noise3d_raw does not count the call
-__device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, float py, float pz)
+// The lattice part of noise3d once the cell (Px, Py, Pz), the fractions (x, y, z), x - 1,
+// y - 1 and the fades (ux, uy, uz) are known: the perm2D texel, the eight gradient dots,
+// the trilinear lerp.
+__device__ __forceinline__ float noise3d_cell(const NoiseView& nz, int32_t Px, int32_t Py, int32_t Pz, float x, float y,
+                                              float x1, float y1, float z, float ux_, float uy_, float uz)
 {
-    float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
-    int32_t Px = (int32_t)fx, Py = (int32_t)fy, Pz = (int32_t)fz;
-    v2f xy = v2(px, py) - v2(fx, fy);
-    float z = pz - fz;
-    v2f uxy = fade2(xy);
-    float uz = fade(z);
     // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
     // texel (Px & 127, Py & 127) at byte ((Py & 127) << 9) | ((Px & 127) << 2): the low
     // term stays below 512, so add-then-mask needs no separate Py mask
@@ -106,20 +106,79 @@ __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, floa
     };
     const float4 a0 = gxy_at(0x0c0c0400u), a1 = gxy_at(0x0c0c0500u), b0 = gxy_at(0x0c0c0600u), b1 = gxy_at(0x0c0c0700u);
     const float2 za0 = gz_at(0x0c0c0400u), za1 = gz_at(0x0c0c0500u), zb0 = gz_at(0x0c0c0600u), zb1 = gz_at(0x0c0c0700u);
-    const float x = xy.x, y = xy.y;
-    const v2f xy1 = xy + v2(-1.0f, -1.0f);
-    const float x1 = xy1.x, y1 = xy1.y;
     const v2f zz = v2(z, z + -1.0f);
     v2f g00 = gdot2(a0, za0, x, y, zz);   // (g000, g001)
     v2f g10 = gdot2(b0, zb0, x1, y, zz);  // (g100, g101)
     v2f g01 = gdot2(a1, za1, x, y1, zz);  // (g010, g011)
     v2f g11 = gdot2(b1, zb1, x1, y1, zz); // (g110, g111)
     // lerp(a, b, t) = fma(t, b - a, a) element-wise: x, then y, then z
-    v2f ux = v2(uxy.x, uxy.x), uy = v2(uxy.y, uxy.y);
+    v2f ux = v2(ux_, ux_), uy = v2(uy_, uy_);
     v2f lx0 = vfma(ux, g10 - g00, g00);
     v2f lx1 = vfma(ux, g11 - g01, g01);
     v2f l = vfma(uy, lx1 - lx0, lx0); // (l0, l1)
     return fma(uz, l.y - l.x, l.x);
+}
+
+// noise.hlsl:153-179 (live `#if 1` block); noise3d_raw does not count the call
+__device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, float py, float pz)
+{
+    const float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
+    const v2f xy = v2(px, py) - v2(fx, fy);
+    const float z = pz - fz;
+    const v2f uxy = fade2(xy);
+    const v2f xy1 = xy + v2(-1.0f, -1.0f);
+    return noise3d_cell(nz, (int32_t)fx, (int32_t)fy, (int32_t)fz, xy.x, xy.y, xy1.x, xy1.y, z, uxy.x, uxy.y, fade(z));
+}
+
+// Two noise3d evaluations at once (elements .x and .y: two FBM octaves).  The floor fractions,
+// their fades and x - 1, y - 1 of the pair run in packed math (v_pk_*_f32), element-wise the
+// same IEEE operations as noise3d_raw, so each element is bit-identical to noise3d_raw of its
+// point; the pair halves the z work the single form does in scalar instructions.
+__device__ __forceinline__ v2f noise3d_pair(const NoiseView& nz, v2f px, v2f py, v2f pz)
+{
+    const v2f fx = v2(rtm::floor(px.x), rtm::floor(px.y));
+    const v2f fy = v2(rtm::floor(py.x), rtm::floor(py.y));
+    const v2f fz = v2(rtm::floor(pz.x), rtm::floor(pz.y));
+    const v2f x = px - fx, y = py - fy, z = pz - fz;
+    const v2f ux = fade2(x), uy = fade2(y), uz = fade2(z);
+    const v2f x1 = x + v2(-1.0f, -1.0f), y1 = y + v2(-1.0f, -1.0f);
+    int32_t Px = (int32_t)fx.y, Py = (int32_t)fy.y, Pz = (int32_t)fz.y;
+    float bx = x.y, by = y.y, bx1 = x1.y, by1 = y1.y, bz = z.y, bux = ux.y, buy = uy.y, buz = uz.y;
+    const float a = noise3d_cell(nz, (int32_t)fx.x, (int32_t)fy.x, (int32_t)fz.x, x.x, y.x, x1.x, y1.x, z.x, ux.x, uy.x,
+                                 uz.x);
+#if RT_PAIR_SERIAL
+    // the second cell's table loads start after the first cell's result (register pressure)
+    asm volatile("" : "+v"(Px), "+v"(Py), "+v"(Pz), "+v"(bx), "+v"(by), "+v"(bx1), "+v"(by1), "+v"(bz) : "v"(a));
+#endif
+    const float b = noise3d_cell(nz, Px, Py, Pz, bx, by, bx1, by1, bz, bux, buy, buz);
+    return v2(a, b);
+}
+
+// noise3d(px, py, 0) (nomadplains' steep noise, terrain.hlsl:26).  z = 0 makes Pz = 0 and
+// fade(z) = 0, so noise3d is the z-layer's bilinear lerp l0 (fma(+0, l1 - l0, l0) == l0), and
+// each z-layer gradient dot loses its z term (fma(g.z, +0, r) == r).  Both identities hold up
+// to the sign of a zero, and add/mul/fma inputs that differ only in zero signs give results
+// that differ only in zero signs: every nonzero value, the result included, is bit-identical to
+// noise3d_raw's.  The caller only forms sat((n - 0.2) * 6), where a zero's sign cannot show.
+__device__ __forceinline__ float noise3d_z0(const NoiseView& nz, float px, float py)
+{
+    const float fx = rtm::floor(px), fy = rtm::floor(py);
+    const v2f xy = v2(px, py) - v2(fx, fy);
+    const v2f uxy = fade2(xy);
+    const v2f xy1 = xy + v2(-1.0f, -1.0f);
+    const uint32_t Px = (uint32_t)(int32_t)fx, Py = (uint32_t)(int32_t)fy;
+    const uint32_t toff = ((Py << 9) + ((Px << 2) & 0x1fcu)) & 0xfffcu;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(nz.perm2d) + toff) & 0x7f7f7f7fu;
+    const char* gb = reinterpret_cast<const char*>(nz.gxy);
+    auto g_at = [&](uint32_t sel) {
+        return *reinterpret_cast<const float4*>(gb + __builtin_amdgcn_perm(w, nz.so16, sel));
+    };
+    const float4 a0 = g_at(0x0c0c0400u), a1 = g_at(0x0c0c0500u), b0 = g_at(0x0c0c0600u), b1 = g_at(0x0c0c0700u);
+    const float x = xy.x, y = xy.y, x1 = xy1.x, y1 = xy1.y;
+    const float g00 = fma(a0.z, y, a0.x * x), g10 = fma(b0.z, y, b0.x * x1);
+    const float g01 = fma(a1.z, y1, a1.x * x), g11 = fma(b1.z, y1, b1.x * x1);
+    const float lx0 = fma(uxy.x, g10 - g00, g00), lx1 = fma(uxy.x, g11 - g01, g01);
+    return fma(uxy.y, lx1 - lx0, lx0);
 }
 
 __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py, float pz)
@@ -199,7 +258,20 @@ __device__ __forceinline__ float terraces(float s, float y, float steep)
     return s;
 }
 
-// Media/nomadplains/shaders/terrain.hlsl:8-39
+// Media/nomadplains/shaders/terrain.hlsl:8-39.  RT_STEEP_Z0 (default): the steep noise,
+// noise3d(x, z, 0), by noise3d_z0 (+2% at C3 with the fog and floor-lift skips below).
+// RT_NP_PAIR / RT_COL_PAIR (A/B only): the FBM's octaves two at a time (noise3d_pair) while
+// some live lane needs both, the fma chain unchanged (octave N, then N + 1).  Bit-exact, but
+// 3.5% slower at C3: the pair's extra live values triple k_trace's scratch spills.
+#ifndef RT_NP_PAIR
+#define RT_NP_PAIR 0
+#endif
+#ifndef RT_STEEP_Z0
+#define RT_STEEP_Z0 1
+#endif
+#ifndef RT_COL_PAIR
+#define RT_COL_PAIR RT_NP_PAIR
+#endif
 __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 {
     float d = -p.y;
@@ -207,6 +279,25 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     float s = 0.0f;
     f3 q0 = rtm::scale(p1, 0.006f);
     const int n_oct = np_octaves(c, p);
+#if RT_NP_PAIR
+    #pragma unroll 1
+    for (int N = 1; N <= RT_NP_OCTAVES; N += 2) {
+        if (N > n_oct) break;
+        const bool two = N + 1 <= n_oct;
+        if (__ballot(two)) {
+            const int N1 = N < RT_NP_OCTAVES ? N + 1 : N; // == N + 1 wherever `two` holds
+            const v2f S = v2(c.k->np_scale[N], c.k->np_scale[N1]);
+            const v2f Sy = v2(c.k->np_scale_y[N], c.k->np_scale_y[N1]);
+            const v2f n = noise3d_pair(c.nz, v2(q0.x, q0.x) * S, v2(q0.y, q0.y) * Sy, v2(q0.z, q0.z) * S);
+            c.nz.calls += two ? 2u : 1u;
+            s = fma(n.x, c.k->np_rcp[N], s);
+            if (two) s = fma(n.y, c.k->np_rcp[N1], s);
+        } else {
+            const float S = c.k->np_scale[N];
+            s = fma(noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S), c.k->np_rcp[N], s);
+        }
+    }
+#else
     #pragma unroll 1
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
         if (N > n_oct) break;
@@ -214,10 +305,19 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
         float n = noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S);
         s = fma(n, c.k->np_rcp[N], s);
     }
+#endif
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
-    float steep = rtm::sat((noise3d(c.nz, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f) - 0.2f) * 6.0f) * 7.5f;
+#if RT_STEEP_Z0
+    c.nz.calls += 1u;
+    const float sn = noise3d_z0(c.nz, p1.x * 0.007138f, p1.z * 0.007138f);
+#else
+    const float sn = noise3d(c.nz, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f);
+#endif
+    float steep = rtm::sat((sn - 0.2f) * 6.0f) * 7.5f;
     s = terraces(s, p1.y, steep);
-    s = fma(rtm::pow_nonneg(rtm::sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
+    // floor lift: pow(0, 1.5) == 0 exactly, so a wave whose bases are all 0 skips the pow
+    const float lb = rtm::sat((-p1.y + 10.0f) * 1.6f);
+    s = fma(__ballot(lb != 0.0f) ? rtm::pow_nonneg(lb, 1.5f) : 0.0f, 19.0f, s);
     return d + s;
 }
 
@@ -479,14 +579,18 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
         fs.z = g.z * m.step;
         fs.w = g.w * m.step;
     }
+    // without fog fs is +0 and m.f stays +0 (+0 + +0 == +0 - +0 == +0): no updates
+    constexpr bool kFog = March<L, CALCFOG>::FOG;
     if (m.d > 0.0f) {
         if constexpr (SKIPREFINE) return;
         m.dist = m.dist - m.lastStep;
         m.step = m.step * 0.3f;
-        m.f.x = m.f.x - fs.x;
-        m.f.y = m.f.y - fs.y;
-        m.f.z = m.f.z - fs.z;
-        m.f.w = m.f.w - fs.w;
+        if constexpr (kFog) {
+            m.f.x = m.f.x - fs.x;
+            m.f.y = m.f.y - fs.y;
+            m.f.z = m.f.z - fs.z;
+            m.f.w = m.f.w - fs.w;
+        }
     } else {
         const float sx = rtm::abs(rtm::min(m.d + 5.0f, 0.0f));
         float stepmult;
@@ -497,10 +601,12 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
         m.step = m.step * k->step_factor;
         m.lastStep = m.step * stepmult;
         m.dist = m.dist + m.lastStep;
-        m.f.x = m.f.x + fs.x;
-        m.f.y = m.f.y + fs.y;
-        m.f.z = m.f.z + fs.z;
-        m.f.w = m.f.w + fs.w;
+        if constexpr (kFog) {
+            m.f.x = m.f.x + fs.x;
+            m.f.y = m.f.y + fs.y;
+            m.f.z = m.f.z + fs.z;
+            m.f.w = m.f.w + fs.w;
+        }
     }
 }
 
@@ -669,11 +775,22 @@ __device__ __forceinline__ ShadePre shade_pre(const Ctx& c, f3 p, f3 n, f3 d, fl
         float s = 0.0f;
         if constexpr (L == RT_NOMADPLAINS) {
             f3 q = rtm::mk(p.y * 0.5f, p.x * 0.01f, p.z * 0.01f);
+#if RT_COL_PAIR
+            #pragma unroll 1
+            for (int N = 1; N <= 20; N += 2) {
+                const v2f S = v2(c.k->col_scale[N], c.k->col_scale[N + 1]);
+                const v2f n = noise3d_pair(c.nz, v2(q.x, q.x) * S, v2(q.y, q.y) * S, v2(q.z, q.z) * S);
+                c.nz.calls += 2u;
+                s = fma(rtm::abs(n.x), c.k->col_rcp[N], s);
+                s = fma(rtm::abs(n.y), c.k->col_rcp[N + 1], s);
+            }
+#else
             #pragma unroll 1
             for (int N = 1; N <= 20; ++N) {
                 float S = c.k->col_scale[N];
                 s = fma(rtm::abs(noise3d(c.nz, q.x * S, q.y * S, q.z * S)), c.k->col_rcp[N], s);
             }
+#endif
             c0 = fma(-s, 0.5f, c0);
             c1 = fma(-s, 0.5f, c1);
             c2 = fma(-s, 0.5f, c2);
