@@ -1868,14 +1868,8 @@ __global__ void __launch_bounds__(256) k_debug_noise(const RtConsts* __restrict_
     if (i >= n) return;
     Ctx c = make_ctx(k, lds);
     f3 p = rtm::mk(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]);
-    // density 2: noise3d_z0(x, y) (z ignored); 3 / 4: element .x / .y of noise3d_pair with
-    // the neighbouring point (i ^ 1) in the other element
-    if (density >= 3) {
-        const int j = (i ^ 1) < n ? (i ^ 1) : i;
-        const f3 q = rtm::mk(xyz[3 * j], xyz[3 * j + 1], xyz[3 * j + 2]);
-        out[i] = density == 3 ? noise3d_pair(c.nz, v2(p.x, q.x), v2(p.y, q.y), v2(p.z, q.z)).x
-                              : noise3d_pair(c.nz, v2(q.x, p.x), v2(q.y, p.y), v2(q.z, p.z)).y;
-    } else if (density == 2) {
+    // density 2: noise3d_z0(x, y) (z ignored)
+    if (density == 2) {
         out[i] = noise3d_z0(c.nz, p.x, p.y);
     } else {
         out[i] = density ? get_density<L>(c, p) : noise3d(c.nz, p.x, p.y, p.z);

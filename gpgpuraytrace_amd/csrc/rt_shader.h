@@ -32,9 +32,6 @@ using rtm::fma;
 //           v_perm_b32 addresses both loads (ds_read_b64 ... offset:32768); the b128
 //           loads are conflict-free however random the indices, the b64 loads 2-way.
 //           RT_GZ16=0: gz[i*32 + (s&31)] (8 B slots, conflict-free, own address).
-#ifndef RT_PAIR_SERIAL
-#define RT_PAIR_SERIAL 1
-#endif
 #ifndef RT_GZ16
 #define RT_GZ16 1
 #endif
@@ -128,30 +125,6 @@ __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, floa
     const v2f uxy = fade2(xy);
     const v2f xy1 = xy + v2(-1.0f, -1.0f);
     return noise3d_cell(nz, (int32_t)fx, (int32_t)fy, (int32_t)fz, xy.x, xy.y, xy1.x, xy1.y, z, uxy.x, uxy.y, fade(z));
-}
-
-// Two noise3d evaluations at once (elements .x and .y: two FBM octaves).  The floor fractions,
-// their fades and x - 1, y - 1 of the pair run in packed math (v_pk_*_f32), element-wise the
-// same IEEE operations as noise3d_raw, so each element is bit-identical to noise3d_raw of its
-// point; the pair halves the z work the single form does in scalar instructions.
-__device__ __forceinline__ v2f noise3d_pair(const NoiseView& nz, v2f px, v2f py, v2f pz)
-{
-    const v2f fx = v2(rtm::floor(px.x), rtm::floor(px.y));
-    const v2f fy = v2(rtm::floor(py.x), rtm::floor(py.y));
-    const v2f fz = v2(rtm::floor(pz.x), rtm::floor(pz.y));
-    const v2f x = px - fx, y = py - fy, z = pz - fz;
-    const v2f ux = fade2(x), uy = fade2(y), uz = fade2(z);
-    const v2f x1 = x + v2(-1.0f, -1.0f), y1 = y + v2(-1.0f, -1.0f);
-    int32_t Px = (int32_t)fx.y, Py = (int32_t)fy.y, Pz = (int32_t)fz.y;
-    float bx = x.y, by = y.y, bx1 = x1.y, by1 = y1.y, bz = z.y, bux = ux.y, buy = uy.y, buz = uz.y;
-    const float a = noise3d_cell(nz, (int32_t)fx.x, (int32_t)fy.x, (int32_t)fz.x, x.x, y.x, x1.x, y1.x, z.x, ux.x, uy.x,
-                                 uz.x);
-#if RT_PAIR_SERIAL
-    // the second cell's table loads start after the first cell's result (register pressure)
-    asm volatile("" : "+v"(Px), "+v"(Py), "+v"(Pz), "+v"(bx), "+v"(by), "+v"(bx1), "+v"(by1), "+v"(bz) : "v"(a));
-#endif
-    const float b = noise3d_cell(nz, Px, Py, Pz, bx, by, bx1, by1, bz, bux, buy, buz);
-    return v2(a, b);
 }
 
 // noise3d(px, py, 0) (nomadplains' steep noise, terrain.hlsl:26).  z = 0 makes Pz = 0 and
@@ -258,19 +231,10 @@ __device__ __forceinline__ float terraces(float s, float y, float steep)
     return s;
 }
 
-// Media/nomadplains/shaders/terrain.hlsl:8-39.  RT_STEEP_Z0 (default): the steep noise,
-// noise3d(x, z, 0), by noise3d_z0 (+2% at C3 with the fog and floor-lift skips below).
-// RT_NP_PAIR / RT_COL_PAIR (A/B only): the FBM's octaves two at a time (noise3d_pair) while
-// some live lane needs both, the fma chain unchanged (octave N, then N + 1).  Bit-exact, but
-// 3.5% slower at C3: the pair's extra live values triple k_trace's scratch spills.
-#ifndef RT_NP_PAIR
-#define RT_NP_PAIR 0
-#endif
+// Media/nomadplains/shaders/terrain.hlsl:8-39.  The steep noise, noise3d(x, z, 0), is evaluated
+// by noise3d_z0 (RT_STEEP_Z0=0: by noise3d, for A/B runs).
 #ifndef RT_STEEP_Z0
 #define RT_STEEP_Z0 1
-#endif
-#ifndef RT_COL_PAIR
-#define RT_COL_PAIR RT_NP_PAIR
 #endif
 __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 {
@@ -279,25 +243,6 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     float s = 0.0f;
     f3 q0 = rtm::scale(p1, 0.006f);
     const int n_oct = np_octaves(c, p);
-#if RT_NP_PAIR
-    #pragma unroll 1
-    for (int N = 1; N <= RT_NP_OCTAVES; N += 2) {
-        if (N > n_oct) break;
-        const bool two = N + 1 <= n_oct;
-        if (__ballot(two)) {
-            const int N1 = N < RT_NP_OCTAVES ? N + 1 : N; // == N + 1 wherever `two` holds
-            const v2f S = v2(c.k->np_scale[N], c.k->np_scale[N1]);
-            const v2f Sy = v2(c.k->np_scale_y[N], c.k->np_scale_y[N1]);
-            const v2f n = noise3d_pair(c.nz, v2(q0.x, q0.x) * S, v2(q0.y, q0.y) * Sy, v2(q0.z, q0.z) * S);
-            c.nz.calls += two ? 2u : 1u;
-            s = fma(n.x, c.k->np_rcp[N], s);
-            if (two) s = fma(n.y, c.k->np_rcp[N1], s);
-        } else {
-            const float S = c.k->np_scale[N];
-            s = fma(noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S), c.k->np_rcp[N], s);
-        }
-    }
-#else
     #pragma unroll 1
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
         if (N > n_oct) break;
@@ -305,7 +250,6 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
         float n = noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S);
         s = fma(n, c.k->np_rcp[N], s);
     }
-#endif
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
 #if RT_STEEP_Z0
     c.nz.calls += 1u;
@@ -775,22 +719,11 @@ __device__ __forceinline__ ShadePre shade_pre(const Ctx& c, f3 p, f3 n, f3 d, fl
         float s = 0.0f;
         if constexpr (L == RT_NOMADPLAINS) {
             f3 q = rtm::mk(p.y * 0.5f, p.x * 0.01f, p.z * 0.01f);
-#if RT_COL_PAIR
-            #pragma unroll 1
-            for (int N = 1; N <= 20; N += 2) {
-                const v2f S = v2(c.k->col_scale[N], c.k->col_scale[N + 1]);
-                const v2f n = noise3d_pair(c.nz, v2(q.x, q.x) * S, v2(q.y, q.y) * S, v2(q.z, q.z) * S);
-                c.nz.calls += 2u;
-                s = fma(rtm::abs(n.x), c.k->col_rcp[N], s);
-                s = fma(rtm::abs(n.y), c.k->col_rcp[N + 1], s);
-            }
-#else
             #pragma unroll 1
             for (int N = 1; N <= 20; ++N) {
                 float S = c.k->col_scale[N];
                 s = fma(rtm::abs(noise3d(c.nz, q.x * S, q.y * S, q.z * S)), c.k->col_rcp[N], s);
             }
-#endif
             c0 = fma(-s, 0.5f, c0);
             c1 = fma(-s, 0.5f, c1);
             c2 = fma(-s, 0.5f, c2);
