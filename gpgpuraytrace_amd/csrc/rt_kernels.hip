@@ -13,6 +13,7 @@
 // until the slowest wave of its workgroup retires.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -124,8 +125,8 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
 // camerarays.hlsl:12-21 for nomadplains with one 32-lane group per prepass ray:
 // the prepass is 1024 sequential marches of ~350 steps, so it is bound by the
 // latency of one step, and spreading each step's 17 FBM octaves + steep noise over
-// a lane group (rts::density_nomadplains_seg<32>) shortens that chain ~4x.
-template <bool STATS, int BS>
+// a lane group (rts::density_nomadplains_seg<LPR>, LPR lanes per ray) shortens that chain ~4x.
+template <bool STATS, int BS, int LPR>
 __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restrict__ k,
                                                           const uint32_t* __restrict__ perm2d,
                                                           const float4* __restrict__ grad, float4* __restrict__ out,
@@ -135,12 +136,12 @@ __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restr
     if (ft) out = ft->cam[blockIdx.y];
     __shared__ uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad);
-    const int i = blockIdx.x * (blockDim.x >> 5) + (threadIdx.x >> 5);
+    const int i = blockIdx.x * (BS / LPR) + (int)(threadIdx.x / LPR);
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
     Ctx c = make_ctx(k, lds);
     if (ft) c = frame_ctx_cam(c, ft, blockIdx.y);
-    const uint32_t j = threadIdx.x & 31u, base = threadIdx.x & 32u;
-    const SegOctaves<32> g = seg_octaves<32>(c, j);
+    const uint32_t j = threadIdx.x & (LPR - 1u), base = threadIdx.x & 63u & ~(LPR - 1u);
+    const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
     int tx = i % RT_CAMERA_RES, ty = i / RT_CAMERA_RES;
     const float r31 = rtm::rcp(31.0f);
     uint32_t pxs = (uint32_t)(((float)tx * r31) * k->screen[0]);
@@ -153,7 +154,7 @@ __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restr
     while (march_live<L, false, true>(c, st, RT_CAMERA_FAR, 0)) {
         auto dens = [&](f3 q) {
             uint32_t used;
-            float d = density_nomadplains_seg<32>(c, g, q, j, base, &used);
+            float d = density_nomadplains_seg<LPR>(c, g, q, j, base, &used);
             noise += used + 1u;
             return d;
         };
@@ -382,6 +383,8 @@ struct UnitMap {
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_t lane, uint32_t W, uint32_t H,
                                            uint32_t* px, uint32_t* py)
 {
+    // 8x8 units (16x4 and 32x2 measured 1% and 3% slower at C3: rows near the horizon
+    // diverge more along x than an 8x8 block does along y)
     uint32_t T = (u >> 4) * m.tile_stride + m.tile_first, sub = u & 15u;
     uint32_t gx = (T % m.tiles32_x) * 32u + (sub & 3u) * 8u + (lane & 7u);
     uint32_t gy = (T / m.tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
@@ -1605,22 +1608,39 @@ template <int L>
 void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, uint32_t n)
 {
     if constexpr (L == RT_NOMADPLAINS) {
-        // one 32-lane group per ray.  A block holds the noise tables (one block per CU), so
+        // one LPR-lane group per ray.  A block holds the noise tables (one block per CU), so
         // a batch packs more rays per block to keep every frame's prepass in one dispatch
-        // round: 8 rays (256 threads) up to 2 frames, 16 up to 4, 32 beyond.
-        auto go = [&](auto bs_tag) {
-            constexpr int BS = decltype(bs_tag)::value;
-            dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / (BS / 32), n), block(BS);
+        // round: 8 rays of 32 lanes (256 threads) up to 2 frames, 16 up to 4, and beyond 64
+        // rays of 8 lanes (512 threads, <= 256 blocks for <= 16 frames).  Fewer lanes per ray
+        // lengthen a step (3 noise rounds instead of 1) but keep a 12-frame prepass in one
+        // round: 1.4 -> 0.7 ms per batch, +1.8% at C3 (32 rays of 32 lanes took two rounds).
+        // RT_PREPASS_CFG=<threads>,<lanes per ray> overrides (A/B runs).
+        auto go = [&](auto bs_tag, auto lpr_tag) {
+            constexpr int BS = decltype(bs_tag)::value, LPR = decltype(lpr_tag)::value;
+            dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / (BS / LPR), n), block(BS);
             if (a.stats)
-                hipLaunchKernelGGL((k_camerarays_group<true, BS>), grid, block, 0, a.stream, a.consts, a.perm2d,
+                hipLaunchKernelGGL((k_camerarays_group<true, BS, LPR>), grid, block, 0, a.stream, a.consts, a.perm2d,
                                    a.grad, out, a.stats, ft);
             else
-                hipLaunchKernelGGL((k_camerarays_group<false, BS>), grid, block, 0, a.stream, a.consts, a.perm2d,
-                                   a.grad, out, a.stats, ft);
+                hipLaunchKernelGGL((k_camerarays_group<false, BS, LPR>), grid, block, 0, a.stream, a.consts,
+                                   a.perm2d, a.grad, out, a.stats, ft);
         };
-        if (n <= 2) go(std::integral_constant<int, 256>{});
-        else if (n <= 4) go(std::integral_constant<int, 512>{});
-        else go(std::integral_constant<int, 1024>{});
+        using C1024 = std::integral_constant<int, 1024>;
+        using C512 = std::integral_constant<int, 512>;
+        using C256 = std::integral_constant<int, 256>;
+        using L32 = std::integral_constant<int, 32>;
+        static const char* cfg = std::getenv("RT_PREPASS_CFG");
+        int cbs = 0, clpr = 0;
+        if (cfg && std::sscanf(cfg, "%d,%d", &cbs, &clpr) == 2) {
+            if (cbs == 1024 && clpr == 32) return go(C1024{}, L32{});
+            if (cbs == 1024 && clpr == 16) return go(C1024{}, std::integral_constant<int, 16>{});
+            if (cbs == 1024 && clpr == 8) return go(C1024{}, std::integral_constant<int, 8>{});
+            if (cbs == 512 && clpr == 8) return go(C512{}, std::integral_constant<int, 8>{});
+            if (cbs == 256 && clpr == 4) return go(C256{}, std::integral_constant<int, 4>{});
+        }
+        if (n <= 2) go(C256{}, L32{});
+        else if (n <= 4) go(C512{}, L32{});
+        else go(C512{}, std::integral_constant<int, 8>{});
         return;
     }
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64, n), block(64);
