@@ -424,7 +424,7 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t t, 
 
 // Lanes idle before a wave refills them: amortises the refill's divergent
 // prologue against the idle lanes it leaves (k_march).
-constexpr uint32_t kRefillIdle = 8;
+constexpr uint32_t kRefillIdle = 4;
 
 template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
@@ -1044,7 +1044,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 constexpr uint32_t kHitRing = 512;
 constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
 constexpr uint32_t kLongBatch = 128; // queued long rays that make a wave switch to them
-constexpr uint32_t kCompactLive = 40; // live lanes below which a dry wave hands its rays back
+constexpr uint32_t kCompactLive = 56; // live lanes below which a dry wave hands its rays back
 
 struct TraceQueues {
     uint32_t lock;
