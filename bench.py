@@ -230,8 +230,8 @@ def main():
             group = ring.slots[g * B:(g + 1) * B]
             ters = [t for _, t in group]
             devs = [d for d, _ in group]
-            first = rank * chunk
-            E.prepass_batch(ters, first, max(0, min(B - first, chunk)), cam_bufs[g].data_ptr())
+            first = min(rank * chunk, B)  # ranks past the batch's last frame (B < world * chunk) run none
+            E.prepass_batch(ters, first, min(B - first, chunk), cam_bufs[g].data_ptr())
             with torch.cuda.stream(group_streams[g]):
                 mine = cam_bufs[g][rank * chunk * 4096:(rank + 1) * chunk * 4096]
                 all_gather(cam_bufs[g], mine, pre_group)

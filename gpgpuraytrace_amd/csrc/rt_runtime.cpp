@@ -1226,7 +1226,8 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     rt_device dev = b.dev;
     FrameTable& ft = b.ft;
     if (count < 0) count = n;
-    if (first < 0 || count > n || first > n - count) return fail(RT_ERR_INVALID, "bad prepass frame range");
+    // an empty range is valid anywhere: a rank past the last frame of a split prepass (B < N * chunk)
+    if (count > n || (count > 0 && (first < 0 || first > n - count))) return fail(RT_ERR_INVALID, "bad prepass frame range");
     const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr && phases == (PH_PRE | PH_TRACE);
     if (camera_in) {
         // gathered prepass results: the table reads them, and each frame's CameraResults

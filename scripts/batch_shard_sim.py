@@ -51,7 +51,7 @@ def main():
             g = (ring.frame // B) % ring.depth
             ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
             chunk = -(-B // n)
-            G.engine.prepass_batch(ters, r * chunk, max(0, min(B - r * chunk, chunk)), bufs[g].data_ptr())
+            G.engine.prepass_batch(ters, min(r * chunk, B), max(0, min(B - r * chunk, chunk)), bufs[g].data_ptr())
             G.engine.trace_batch(ters, r, n, bufs[g].data_ptr())
             ring.frame += B
         for n in [int(x) for x in a.ns.split(",")]:

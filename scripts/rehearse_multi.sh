@@ -4,10 +4,11 @@
 # equals a whole-frame render.  Timings are meaningless (ranks share one GPU); correctness is not.
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/reh
 export RT_BENCH_SAME_GPU=1 RT_DIST_BACKEND=gloo
-run() { local n=$1; shift
+PORT=29500
+run() { local n=$1; shift; PORT=$((PORT + 1))
   timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $((29500 + n)) bench.py --gpus $n --verify --no-cpu-baseline "$@" > gpurun_out/reh/n$n.json 2> gpurun_out/reh/n$n.err \
+    --master-port $PORT bench.py --gpus $n --verify --no-cpu-baseline "$@" > gpurun_out/reh/n$n.json 2> gpurun_out/reh/n$n.err \
     || { echo "n=$n failed"; tail -20 gpurun_out/reh/n$n.err; return 1; }
   tail -1 gpurun_out/reh/n$n.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['n_gpus'], d['config']['parallelism'], '->', d['config'].get('verify'))"
 }
-run 2 && run 4 && run 3 --split-prepass 0 --batch 5
+run 2 && run 4 && run 3 --split-prepass 0 --batch 5 && run 4 --batch 5  # 4 ranks x 2 frames: rank 3 has none

@@ -539,7 +539,8 @@ def test_batch_split_prepass_bitexact():
     frames = _batch(specs, stats=True)
     ters = [t for _, t in frames]
     buf = torch.full((len(specs), 1024, 4), float("nan"), dtype=torch.float32, device="cuda:0")
-    for first, count in ((0, 2), (2, 2), (4, 1), (5, 0)):
+    # (5, 0) and (6, 0): ranks past the last frame (bench.py at N = 8 with 12-frame batches)
+    for first, count in ((0, 2), (2, 2), (4, 1), (5, 0), (6, 0)):
         E.prepass_batch(ters, first, count, buf.data_ptr())
     E.trace_batch(ters, 0, 1, buf.data_ptr())
     _check_frames(frames, specs)
