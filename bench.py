@@ -191,6 +191,18 @@ def main():
     full = sdev.stats(reset=True)
     sdev.synchronize()
     shard_noise = full["noise_calls"] - pre["noise_calls"]
+    # a batch's frame f traces shard (rank + f) % world (per-frame rotation): its launch's noise count
+    B = max(1, min(16, a.batch))
+    per_shard = {rank % world if world > 1 else 0: shard_noise}
+    if world > 1 and B > 1:
+        for s in {(rank + f) % world for f in range(B)} - set(per_shard):
+            ster.camera_compute.run(2, 2, 1)
+            pre = sdev.stats(reset=True)
+            ster.render_device(s, world)
+            per_shard[s] = sdev.stats(reset=True)["noise_calls"] - pre["noise_calls"]
+        sdev.synchronize()
+    batch_noise = (sum(per_shard[(rank + f) % world] for f in range(B)) if world > 1 and B > 1
+                   else B * shard_noise)
     # whole-frame counts (all shards) for the ray total
     if world > 1:
         ster.render_device(0, 1)
@@ -203,7 +215,6 @@ def main():
 
     # --- timed: D frames in flight (FrameRing: one full frame context + HIP stream per slot) ---
     camera = G.Camera(W, H, euler=euler)
-    B = max(1, min(16, a.batch))
     ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     packed, gathered = {}, {}
@@ -244,12 +255,12 @@ def main():
             with torch.cuda.stream(group_streams[g]):
                 # (a batch's devices share its stream: FrameRing)
                 for f, dev in enumerate(devs):
-                    E.shard_pack(dev, rank, world, packed[g].data_ptr() + f * maxb)
+                    E.shard_pack(dev, (rank + f) % world, world, packed[g].data_ptr() + f * maxb)  # frame f: shard (rank + f) % world
                 gather(packed[g], gathered[g] if rank == 0 else None)
                 if rank == 0:
                     for r in range(1, world):
                         for f, dev in enumerate(devs):
-                            E.shard_unpack(dev, r, world, gathered[g][r].data_ptr() + f * maxb)
+                            E.shard_unpack(dev, (r + f) % world, world, gathered[g][r].data_ptr() + f * maxb)
             for dev in devs:
                 dev.present()
 
@@ -306,7 +317,7 @@ def main():
 
     ms_per_frame = elapsed / frames_timed * 1e3
     value = rays_per_frame * frames_timed / elapsed / 1e6
-    achieved = B * shard_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
+    achieved = batch_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
     traffic = None
     if os.path.exists(a.traffic_json):
         try:
@@ -352,8 +363,8 @@ def main():
                 "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
                 "timing": "HIP events per launch on its stream, one batch in flight (the last "
                           f"{kn} tracescreen launches of the run; one launch = {B} frames)",
-                "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {shard_noise} noise3d per frame x {B} "
-                             f"frame(s) per launch",
+                "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {batch_noise} noise3d per launch ({B} "
+                             f"frame(s); frame f traces shard (rank + f) % world)",
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "
                         "= FP32 dense matrix peak = 157.3 TFLOP/s",
             },

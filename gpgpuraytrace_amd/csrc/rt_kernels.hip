@@ -378,14 +378,16 @@ __global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict
 struct UnitMap {
     uint32_t off_x, off_y, ext_x, ext_y, tiles32_x, tile_first, tile_stride, n_units;
     uint32_t n_frames, frame_samples;
+    uint32_t frame_rot; // 1: frame f of a batch traces shard (tile_first + f) % tile_stride
 };
 
-__device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_t lane, uint32_t W, uint32_t H,
-                                           uint32_t* px, uint32_t* py)
+__device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
+                                           uint32_t H, uint32_t* px, uint32_t* py)
 {
+    const uint32_t first = m.frame_rot ? (m.tile_first + f) % m.tile_stride : m.tile_first;
     // 8x8 units (16x4 and 32x2 measured 1% and 3% slower at C3: rows near the horizon
     // diverge more along x than an 8x8 block does along y)
-    uint32_t T = (u >> 4) * m.tile_stride + m.tile_first, sub = u & 15u;
+    uint32_t T = (u >> 4) * m.tile_stride + first, sub = u & 15u;
     uint32_t gx = (T % m.tiles32_x) * 32u + (sub & 3u) * 8u + (lane & 7u);
     uint32_t gy = (T / m.tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
     *px = gx + m.off_x;
@@ -393,12 +395,12 @@ __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t u, uint32_
     return gx < m.ext_x && gy < m.ext_y && *px < W && *py < H;
 }
 
-__device__ __forceinline__ bool sample_pixel(const UnitMap& m, uint32_t t, uint32_t aa, uint32_t W, uint32_t H,
-                                             uint32_t* px, uint32_t* py, uint32_t* a)
+__device__ __forceinline__ bool sample_pixel(const UnitMap& m, uint32_t f, uint32_t t, uint32_t aa, uint32_t W,
+                                             uint32_t H, uint32_t* px, uint32_t* py, uint32_t* a)
 {
     uint32_t pix = t / aa;
     *a = t - pix * aa;
-    return unit_pixel(m, pix >> 6, pix & 63u, W, H, px, py);
+    return unit_pixel(m, f, pix >> 6, pix & 63u, W, H, px, py);
 }
 
 __device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane, uint32_t n = 1u)
@@ -496,7 +498,7 @@ __global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, 
                     if (mine) {
                         t = pool + (uint32_t)__popcll(idle & lt_mask);
                         uint32_t px, py, a;
-                        if (sample_pixel(m, t, aa, W, H, &px, &py, &a)) {
+                        if (sample_pixel(m, 0u, t, aa, W, H, &px, &py, &a)) {
                             // tracescreen.hlsl:53-62 plane + getPixelRay, tracing.hlsl:49-66 prologue
                             float pxf = (float)px, pyf = (float)py;
                             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
@@ -565,8 +567,8 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
             uint32_t px, py;
             uint32_t u = tile * 16u + (corner & 1u) * 3u + (corner >> 1) * 12u;
             uint32_t lane = (corner & 1u) * 7u + (corner >> 1) * 56u;
-            if (!unit_pixel(m, u, lane, W, H, &px, &py)) {
-                if (!unit_pixel(m, tile * 16u, 0u, W, H, &px, &py)) continue;
+            if (!unit_pixel(m, blockIdx.x, u, lane, W, H, &px, &py)) {
+                if (!unit_pixel(m, blockIdx.x, tile * 16u, 0u, W, H, &px, &py)) continue;
                 px = px + (corner & 1u) * 31u < W ? px + (corner & 1u) * 31u : W - 1u;
                 py = py + (corner >> 1) * 31u < H ? py + (corner >> 1) * 31u : H - 1u;
             }
@@ -622,7 +624,7 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
         if (q >= m.n_units) break;
         const uint32_t u = __builtin_amdgcn_readfirstlane(order[q >> 4]) * 16u + (q & 15u);
         uint32_t px, py;
-        const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
+        const bool valid = unit_pixel(m, 0u, u, lane, W, H, &px, &py);
         const float pxf = (float)px, pyf = (float)py;
         float plane_x = 0.0f;
         if (valid) {
@@ -782,7 +784,7 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     const float4 dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
     h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
     uint32_t px, py, a;
-    sample_pixel(m, tl, aa, W, H, &px, &py, &a);
+    sample_pixel(m, m.frame_rot ? (t - tl) / m.frame_samples : 0u, tl, aa, W, H, &px, &py, &a);
     h.px = px;
     h.py = py;
     h.a = a;
@@ -1356,7 +1358,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     auto do_unit = [&](uint32_t f, uint32_t u) {
         const Ctx cf = frame_ctx(c, ft, f);
         uint32_t px, py;
-        const bool valid = unit_pixel(m, u, lane, W, H, &px, &py);
+        const bool valid = unit_pixel(m, f, u, lane, W, H, &px, &py);
         const float pxf = (float)px, pyf = (float)py;
         float plane_x = 0.0f;
         if (valid) {
@@ -1512,7 +1514,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0
         uint32_t* out8 = ft->out8[f];
         float4* out32 = ft->out32[f];
         uint32_t px, py;
-        if (!unit_pixel(m, u, lane, W, H, &px, &py)) continue;
+        if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
             uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
@@ -1684,7 +1686,11 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     const float2* cells = a.frames_host.cells[0]; // single-frame primaries (staged, refill)
     UnitMap m;
     uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
-    if (first >= total) return;
+    // a batch rotates the shards over its frames (frame f traces shard (first + f) % stride), so
+    // each rank's share of a batch mixes the tile classes of every shard: the ranks' work evens
+    // out (the slowest of 8 ranks was 7% above the mean with a fixed deal at C3)
+    const uint32_t rot = a.n_frames > 1u && stride > 1u ? 1u : 0u;
+    if (!rot && first >= total) return;
     m.off_x = ox;
     m.off_y = oy;
     m.ext_x = ex;
@@ -1692,7 +1698,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.tiles32_x = tiles_x;
     m.tile_first = first;
     m.tile_stride = stride;
-    m.n_units = ((total - first + stride - 1) / stride) * 16u;
+    m.n_units = ((total - (rot ? 0u : first) + stride - 1) / stride) * 16u; // rot: the largest shard
+    m.frame_rot = rot;
     m.n_frames = a.n_frames;
     m.frame_samples = m.n_units * 64u * (uint32_t)a.aa;
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);

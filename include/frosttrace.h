@@ -176,7 +176,10 @@ int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
  * the next frame's units instead of idling the GPU.  Enqueued on the stream of frame 0's
  * device with frame 0's device buffers and counters; streams of frames on other devices
  * wait for the batch.  No reference counterpart (the reference renders one frame per
- * Terrain::render); each frame's pixels equal its rt_terrain_render frame bit for bit. */
+ * Terrain::render); each frame's pixels equal its rt_terrain_render frame bit for bit.
+ * Sharded (shard_count > 1, n > 1): frame i traces shard (shard_rank + i) % shard_count, a
+ * per-frame rotation that evens out the ranks' work; rt_shard_pack/unpack frame i with that
+ * shard index. */
 int rt_terrain_render_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
                             int shard_count);
 /* The same batch in two phases, for a prepass split across ranks (one process per GPU):

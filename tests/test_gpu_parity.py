@@ -504,11 +504,12 @@ def test_batch_shards_graphs_and_ring():
         for r, frames in enumerate(ranks):
             E.render_batch([t for _, t in frames], r, 2)
             for f, (d, _) in enumerate(frames):
-                bufs[r, f] = torch.zeros(E.shard_bytes(d, r, 2), dtype=torch.uint8, device="cuda:0")
-                E.shard_pack(d, r, 2, bufs[r, f].data_ptr())
+                # frame f of a batch traces shard (r + f) % 2 (the per-frame rotation)
+                bufs[r, f] = torch.zeros(E.shard_bytes(d, (r + f) % 2, 2), dtype=torch.uint8, device="cuda:0")
+                E.shard_pack(d, (r + f) % 2, 2, bufs[r, f].data_ptr())
                 d.synchronize()
         for f, (d, _) in enumerate(ranks[0]):
-            E.shard_unpack(d, 1, 2, bufs[1, f].data_ptr())
+            E.shard_unpack(d, (1 + f) % 2, 2, bufs[1, f].data_ptr())
         for (d, _), spec in zip(ranks[0], specs):  # the shard transport moves the RGBA8 frame
             assert np.array_equal(d.readback(), GI.load()[GI.frame_key(*spec) + "_rgba8"])
     assert ranks[0][0][0].graph_info() == (2, 4)
