@@ -18,6 +18,8 @@ RT_OK = 0
 RT_DEVICE_FLOAT_OUTPUT = 1
 RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
+RT_DEVICE_SEG_TAIL_OFF = 8
+RT_DEVICE_SEG_TAIL_ON = 16
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 

@@ -9,8 +9,6 @@
 enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2, RT_CTR_FINISH = 3, RT_CTR_SHADOW = 4, RT_CTR_LONG = 5 };
 #define RT_CTR_BYTES 64
 
-enum { RT_PIPELINE_SPLIT = 0, RT_PIPELINE_MEGA = 1, RT_PIPELINE_REFILL = 2, RT_PIPELINE_STAGED = 3 };
-
 // A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by
 // one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
 // block (camera, sun), CameraResults, CellDistance and framebuffer; the kernels find them
@@ -34,8 +32,8 @@ struct RtLaunch {
     RtStats* stats;           // nullptr = uninstrumented kernels
     uint32_t* queue;          // RT_CTR_BYTES of device work counters
     int num_cus;              // compute units (persistent grid size)
-    int pipeline;             // RT_PIPELINE_*
-    // split pipeline, rt_split_samples() entries each (sample t, see rt_kernels.hip)
+    int seg_mode;             // k_trace segment tail: -1 auto, 0 off, 1 on (RT_DEVICE_SEG_TAIL_*)
+    // per-sample buffers, rt_split_samples() entries per frame (sample t, see rt_kernels.hip)
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
     float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
     uint32_t* hitlist;        // compacted sample ids of primary hits
@@ -45,9 +43,9 @@ struct RtLaunch {
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension)
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
-    uint32_t* order;          // k_primary tile order (rt_split_samples/1024 entries per frame)
-    const FrameTable* frames; // device table of the batch's frames (split pipeline, prepass batch)
-    FrameTable frames_host;   // the same pointers on the host (single-frame pipelines)
+    uint32_t* order;          // k_order's tile order (rt_split_samples/1024 entries per frame)
+    const FrameTable* frames; // device table of the batch's frames
+    FrameTable frames_host;   // the same pointers on the host
     uint32_t n_frames;        // frames in the batch (1..RT_MAX_BATCH)
 };
 
@@ -57,8 +55,9 @@ void rt_launch_cell_depths(hipStream_t s, const float4* camera_results, float2* 
 void rt_launch_camerarays_batch(const RtLaunch& a);
 void rt_launch_cell_depths_batch(const RtLaunch& a);
 // Trace the region [off, off+ext) in 32x32-pixel tiles of every frame of a.frames (cells and
-// outputs from the table); tiles t (row-major over the region) with t % tile_stride ==
-// tile_first are traced (tile-cyclic sharding).
+// outputs from the table), tile-cyclic sharding: a single frame traces the tiles t (row-major
+// over the region) with t % tile_stride == tile_first; in a batch of n > 1 frames with
+// tile_stride > 1, frame f traces shard (tile_first + f) % tile_stride (per-frame rotation).
 void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, uint32_t ext_x, uint32_t ext_y,
                            uint32_t tile_first, uint32_t tile_stride);
 

@@ -4,13 +4,14 @@
 //   k_cell_depths  <- Graphics/Terrain.cpp:356-439 (setTargetDepths: host code in
 //                     the reference; on the device here so a frame needs no
 //                     GPU->CPU->GPU round trip)
-//   k_tracescreen  <- Media/common/shaders/tracescreen.hlsl:16-76
+//   k_order, k_trace, k_shade_pre, k_shadow, k_finish
+//                  <- Media/common/shaders/tracescreen.hlsl:16-76 (split pipeline below)
 //   k_shard_copy   -- tile-cyclic shard pack/unpack for the multi-GPU gather
 //
-// tracescreen is a persistent kernel: one 1024-thread workgroup per CU keeps the
-// noise tables (96 KiB) in LDS and every wave pulls 8x8-pixel work units from a
-// device-wide atomic queue, so a finished wave takes new work instead of idling
-// until the slowest wave of its workgroup retires.
+// k_trace is a persistent kernel: one 1024-thread workgroup per CU keeps the noise
+// tables (128 KiB) in LDS and every wave pulls 8x8-pixel work units from a device-wide
+// atomic queue, so a finished wave takes new work instead of idling until the slowest
+// wave of its workgroup retires.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -232,145 +233,13 @@ __global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__
     cells[i] = make_float2(dmin, dmax);
 }
 
-// ---------------------------------------------------------------------------
-// tracescreen.hlsl:16-48 traceSample
-template <int L>
-__device__ __forceinline__ f3 trace_sample(const Ctx& c, f3 pp, f3 pdir, f3 pdn, float plane_x, float plane_y,
-                                           float* psteps, float* ssteps, int* hit, uint32_t px, uint32_t py,
-                                           uint32_t a, float* ao_out, float* aosteps)
-{
-    *ao_out = 1.0f;
-    RayResult rr = trace_ray<L, true, false>(c, pp, plane_x, plane_y, 1.0f, pdir, c.k->max_steps);
-    *psteps += rr.steps;
-    float skyAmount = rr.pd.w * 0.0005f;
-    skyAmount = rtm::sat(skyAmount * skyAmount);
-    SkyColor scat = get_rayleigh_mie(c, pdn);
-    f3 color;
-    if (rr.density > 0.0f) {
-        *hit += 1;
-        f4 npd = {rr.pd.x, rr.pd.y, rr.pd.z, rr.density}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
-        f3 n = get_normal<L>(c, npd);
-        f3 hp = rtm::mk(rr.pd.x, rr.pd.y, rr.pd.z);
-        ShadePre sp = shade_pre<L>(c, hp, n, pdn, rr.pd.w);
-        RayResult sr = trace_ray<L, true, true>(c, hp, 0.4f, 100.0f, sp.precision, c.sun, 0);
-        *ssteps += sr.steps;
-        if (c.k->ao_samples > 0) { // AO extension (rt_shader.h ao_dir)
-            uint32_t occ = 0;
-            for (int kk = 0; kk < c.k->ao_samples; ++kk) {
-                RayResult ar = trace_ray<L, false, true>(c, hp, 0.4f, RT_AO_END, sp.precision,
-                                                         ao_dir(n, px, py, a, (uint32_t)kk), 0);
-                *aosteps += ar.steps;
-                occ += ar.density > 0.0f ? 1u : 0u;
-            }
-            *ao_out = ao_factor(occ, c.k->ao_samples);
-        }
-        color = shade_post(c, sp, sr.density, sr.fc.w);
-        color = rtm::mk(rtm::lerp(color.x, rr.fc.x, rr.fc.w), rtm::lerp(color.y, rr.fc.y, rr.fc.w),
-                        rtm::lerp(color.z, rr.fc.z, rr.fc.w));
-        color = rtm::mk(rtm::lerp(color.x, scat.rayleigh.x, skyAmount), rtm::lerp(color.y, scat.rayleigh.y, skyAmount),
-                        rtm::lerp(color.z, scat.rayleigh.z, skyAmount));
-    } else {
-        float space = get_space_color(c, pdn);
-        f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
-                         (scat.mie.z + scat.rayleigh.z) + space);
-        color = rtm::mk(rtm::lerp(sky.x, rr.fc.x, rr.fc.w), rtm::lerp(sky.y, rr.fc.y, rr.fc.w),
-                        rtm::lerp(sky.z, rr.fc.z, rr.fc.w));
-        color = rtm::mk(rtm::lerp(color.x, sky.x, skyAmount), rtm::lerp(color.y, sky.y, skyAmount),
-                        rtm::lerp(color.z, sky.z, skyAmount));
-    }
-    return color;
-}
-
-// tracescreen.hlsl:50-76 for one pixel (all AA samples)
-template <int L>
-__device__ __forceinline__ void shade_pixel(const Ctx& c, uint32_t px, uint32_t py, const float2* __restrict__ cells,
-                                            uint32_t* __restrict__ out8, float4* __restrict__ out32, float* psteps,
-                                            float* ssteps, int* hits, float* aosteps)
-{
-    const RtConsts* k = c.k;
-    float pxf = (float)px, pyf = (float)py;
-    float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-    uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
-    float plane_x = cells[cell].x, plane_y = RT_CAMERA_FAR;
-    float col0 = 0.0f, col1 = 0.0f, col2 = 0.0f;
-    const int aa = k->aa_samples;
-    for (int a = 0; a < aa; ++a) {
-        f3 p, dir;
-        get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
-        f3 pdn = rtm::normalize(dir);
-        float ao;
-        f3 s = trace_sample<L>(c, p, dir, pdn, plane_x, plane_y, psteps, ssteps, hits, px, py, (uint32_t)a, &ao,
-                               aosteps);
-        if (k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
-            col0 = col0 + rtm::sat(s.x) * ao;
-            col1 = col1 + rtm::sat(s.y) * ao;
-            col2 = col2 + rtm::sat(s.z) * ao;
-        } else {
-            col0 = col0 + rtm::sat(s.x);
-            col1 = col1 + rtm::sat(s.y);
-            col2 = col2 + rtm::sat(s.z);
-        }
-    }
-    float ia = rtm::rcp((float)aa);
-    col0 = col0 * ia;
-    col1 = col1 * ia;
-    col2 = col2 * ia;
-    size_t o = (size_t)py * (size_t)k->width + px;
-    out8[o] = unorm8(col0) | (unorm8(col1) << 8) | (unorm8(col2) << 16) | 0xff000000u;
-    if (out32) out32[o] = make_float4(col0, col1, col2, 1.0f);
-}
-
-// Persistent screen trace.  Work unit u (0..n_units): 32x32 shard tile
-// T = (u/16)*tile_stride + tile_first (row-major over the region, tiles32_x per
-// row), 8x8 sub-tile u%16; lane l traces pixel (l&7, l>>3) of the sub-tile.
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_tracescreen(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                      const float4* __restrict__ grad, const float2* __restrict__ cells,
-                                                      uint32_t* __restrict__ out8, float4* __restrict__ out32,
-                                                      uint32_t off_x, uint32_t off_y, uint32_t ext_x, uint32_t ext_y,
-                                                      uint32_t tiles32_x, uint32_t tile_first, uint32_t tile_stride,
-                                                      uint32_t n_units, uint32_t* __restrict__ queue, RtStats* stats)
-{
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
-    const uint32_t lane = threadIdx.x & 63u;
-    Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
-    float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
-    int hits = 0;
-    for (;;) {
-        uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(queue, 1u);
-        u = __builtin_amdgcn_readfirstlane(u);
-        if (u >= n_units) break;
-        uint32_t T = (u >> 4) * tile_stride + tile_first, sub = u & 15u;
-        uint32_t gx = (T % tiles32_x) * 32u + (sub & 3u) * 8u + (lane & 7u);
-        uint32_t gy = (T / tiles32_x) * 32u + (sub >> 2) * 8u + (lane >> 3);
-        if (gx < ext_x && gy < ext_y) {
-            uint32_t px = gx + off_x, py = gy + off_y;
-            if (px < W && py < H) shade_pixel<L>(c, px, py, cells, out8, out32, &psteps, &ssteps, &hits, &aosteps);
-        }
-    }
-    if constexpr (STATS) {
-        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
-        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
-        atomicAdd(&stats->hits, (unsigned long long)hits);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
-    }
-}
-
 // ===========================================================================
-// Split (wavefront) screen pipeline: the same tracescreen.hlsl:16-76 frame in
-// three passes so every kernel body stays small and lanes stay busy.
-//   P k_march  : primary march (tracing.hlsl:47-105) with lane refill -- each lane
-//                owns one ray and takes the next sample the moment its ray leaves
-//                the loop, so a wave's lanes stay full until the sample queue
-//                drains.  Writes the RayResult of every sample; hits are appended
-//                to a compacted list (staged per wave in LDS, one atomic per 64).
-//   S k_shade_pre + k_shadow: normal, colour, sky and the first shadow step over
-//                the hit list, then the long shadow rays with lane refill.
-//   R k_finish : sky colour of the misses + in-order AA average + UNORM8.
+// Screen pipeline: tracescreen.hlsl:16-76 over a batch of frames in four launches.
+//   k_order     : longest-first 32x32 tile order per frame (scheduling only).
+//   k_trace     : persistent; primary march (tracing.hlsl:47-105) per 8x8 unit, the hit
+//                 shading + first shadow step, the long shadow / AO rays (LDS rings).
+//   k_shade_pre + k_shadow: drain what did not fit k_trace's rings (empty = instant exit).
+//   k_finish    : sky colour of the misses + in-order AA average + UNORM8.
 // Sample t = (u*64 + j)*AA + a: AA sample a of lane-slot j of 8x8 unit u.
 // A batch of n_frames frames: unit g of the launch is unit g % n_units of frame g / n_units
 // (frame-major, so a frame's tail overlaps the next frame's units), and sample ids are
@@ -424,118 +293,7 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t t, 
     res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
 }
 
-// Lanes idle before a wave refills them: amortises the refill's divergent
-// prologue against the idle lanes it leaves (k_march).
-constexpr uint32_t kRefillIdle = 4;
-
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_march(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                const float4* __restrict__ grad, const float2* __restrict__ cells,
-                                                UnitMap m, float4* __restrict__ res, uint32_t* __restrict__ hitlist,
-                                                uint32_t* __restrict__ counters, RtStats* stats)
-{
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
-    __shared__ uint32_t s_stage[16][128];
-    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
-    load_noise_lds(lds, perm2d, grad);
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
-    const uint32_t n_samples = m.n_units * 64u * aa;
-    const int max_steps = k->max_steps;
-    March<L, true> st;
-    st.d = 0.0f;
-    st.iters = 0;
-    bool live = false;
-    uint32_t t = 0;
-    uint32_t pool = 0, pool_left = 0, staged = 0; // wave-uniform
-    bool drained = false;
-    float psteps = 0.0f;
-    uint32_t nhits = 0;
-    for (;;) {
-        // 1. retire rays that left the loop (tracing.hlsl:68 condition false)
-        bool fin = live && !march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
-        bool hit = fin && st.d > 0.0f;
-        if (fin) {
-            store_ray(res, t, march_result(st));
-            live = false;
-            if constexpr (STATS) psteps += (float)st.iters;
-        }
-        uint64_t hb = __ballot(hit);
-        if (hb) {
-            if (hit) s_stage[wv][staged + (uint32_t)__popcll(hb & lt_mask)] = t;
-            staged += (uint32_t)__popcll(hb);
-            if constexpr (STATS) nhits += hit ? 1u : 0u;
-            if (staged >= 64u) {
-                __builtin_amdgcn_wave_barrier();
-                uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, 64u);
-                uint32_t first = s_stage[wv][lane], second = s_stage[wv][64u + lane];
-                hitlist[b + lane] = first;
-                staged -= 64u;
-                if (lane < staged) s_stage[wv][lane] = second;
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        // 2. hand idle lanes new samples from the wave's pool (64 ids per queue atomic)
-        if (!drained) {
-            uint64_t idle = __ballot(!live);
-            if ((uint32_t)__popcll(idle) >= kRefillIdle) {
-                while (idle) {
-                    if (pool_left == 0u) {
-                        uint32_t b = wave_fetch(&counters[RT_CTR_PRIMARY], lane, 64u);
-                        if (b >= n_samples) {
-                            drained = true;
-                            break;
-                        }
-                        pool = b;
-                        pool_left = (n_samples - b) < 64u ? (n_samples - b) : 64u;
-                    }
-                    uint32_t nidle = (uint32_t)__popcll(idle);
-                    uint32_t take = nidle < pool_left ? nidle : pool_left;
-                    bool mine = ((idle >> lane) & 1ull) && (uint32_t)__popcll(idle & lt_mask) < take;
-                    if (mine) {
-                        t = pool + (uint32_t)__popcll(idle & lt_mask);
-                        uint32_t px, py, a;
-                        if (sample_pixel(m, 0u, t, aa, W, H, &px, &py, &a)) {
-                            // tracescreen.hlsl:53-62 plane + getPixelRay, tracing.hlsl:49-66 prologue
-                            float pxf = (float)px, pyf = (float)py;
-                            float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-                            uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
-                            f3 p, dir;
-                            get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
-                            march_begin(c, st, p, s_plane[cell], 1.0f, dir);
-                            if (march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps)) live = true;
-                            else store_ray(res, t, march_result(st)); // empty march: a miss at the near plane
-                        }
-                    }
-                    idle &= ~__ballot(mine);
-                    pool += take;
-                    pool_left -= take;
-                }
-            }
-        }
-        // 3. one march step on every live lane
-        if (__ballot(live) == 0ull) {
-            if (drained) break;
-            continue;
-        }
-        if (live) march_step<L, true, false>(c, st);
-    }
-    if (staged) {
-        __builtin_amdgcn_wave_barrier();
-        uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, staged);
-        if (lane < staged) hitlist[b + lane] = s_stage[wv][lane];
-    }
-    if constexpr (STATS) {
-        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
-        atomicAdd(&stats->hits, (unsigned long long)nhits);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
-    }
-}
-
-// Longest-first tile order for k_primary.  A frame's critical path is its few
+// Longest-first tile order for k_trace.  A frame's critical path is its few
 // grazing units (hundreds of march steps near the horizon); in screen order they
 // start half-way through the queue and finish long after the rest.  The prepass
 // cells already say where they are: a tile whose cells' depth bracket
@@ -593,86 +351,6 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
     for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) order[atomicAdd(&s_hist[bucket(t)], 1u)] = t;
 }
 
-// Tile-ordered primary march: each wave takes one 8x8 unit at a time (neighbouring
-// pixels march to similar distances, so their FBM octave counts agree and few
-// lanes idle inside noise loops).  The march loop is the wave's own; a wave still
-// on its unit after kPrioSteps[i] iterations raises its issue priority so the few
-// grazing, many-hundred-step units (the kernel's critical path) are not starved
-// by the SIMD's short-unit waves (MI355X_MICROARCH.md: VALU issue is arbitrated
-// by priority, then age).
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
-                                                  const float4* __restrict__ grad, const float2* __restrict__ cells,
-                                                  UnitMap m, const uint32_t* __restrict__ order,
-                                                  float4* __restrict__ res, uint32_t* __restrict__ hitlist,
-                                                  uint32_t* __restrict__ counters, RtStats* stats)
-{
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    __shared__ float s_plane[RT_CAMERA_RES * RT_CAMERA_RES];
-    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) s_plane[i] = cells[i].x;
-    load_noise_lds(lds, perm2d, grad);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    Ctx c = make_ctx(k, lds);
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
-    const int max_steps = k->max_steps;
-    float psteps = 0.0f;
-    uint32_t nhits = 0;
-    const uint32_t n_static = gridDim.x * (blockDim.x >> 6); // first unit dealt statically (k_trace)
-    for (bool first = true;; first = false) {
-        const uint32_t q = first ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
-        if (q >= m.n_units) break;
-        const uint32_t u = __builtin_amdgcn_readfirstlane(order[q >> 4]) * 16u + (q & 15u);
-        uint32_t px, py;
-        const bool valid = unit_pixel(m, 0u, u, lane, W, H, &px, &py);
-        const float pxf = (float)px, pyf = (float)py;
-        float plane_x = 0.0f;
-        if (valid) {
-            float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-            plane_x = s_plane[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))];
-        }
-        for (uint32_t a = 0; a < aa; ++a) {
-            const uint32_t t = (u * 64u + lane) * aa + a;
-            March<L, true> st;
-            st.d = 0.0f;
-            bool lv = false;
-            if (valid) {
-                f3 p, dir;
-                get_pixel_ray(c, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], &p, &dir);
-                march_begin(c, st, p, plane_x, 1.0f, dir);
-                lv = true;
-            }
-            __builtin_amdgcn_s_setprio(0);
-            for (uint32_t it = 0;; ++it) {
-                lv = lv && march_live<L, true, false>(c, st, RT_CAMERA_FAR, max_steps);
-                if (__ballot(lv) == 0ull) break;
-                if (lv) march_step<L, true, false>(c, st);
-                if (it == 96u) __builtin_amdgcn_s_setprio(1);
-                else if (it == 224u) __builtin_amdgcn_s_setprio(2);
-                else if (it == 384u) __builtin_amdgcn_s_setprio(3);
-            }
-            const bool hit = valid && st.d > 0.0f;
-            if (valid) {
-                RayResult rr = march_result(st);
-                store_ray(res, t, rr);
-                if constexpr (STATS) psteps += rr.steps;
-            }
-            const uint64_t hb = __ballot(hit);
-            if (hb) {
-                uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, (uint32_t)__popcll(hb));
-                if (hit) hitlist[b + (uint32_t)__popcll(hb & lt_mask)] = t;
-                if constexpr (STATS) nhits += hit ? 1u : 0u;
-            }
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if constexpr (STATS) {
-        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
-        atomicAdd(&stats->hits, (unsigned long long)nhits);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
-    }
-}
-
 // Shading (tracescreen.hlsl:28-35, nomadplains/color.hlsl:8-72).  Per hit, the
 // uniform work -- getNormal (3 densities), getColor up to the shadow ray (20-octave
 // albedo FBM), the Rayleigh/Mie sky -- and the FIRST shadow-march step
@@ -683,6 +361,10 @@ __global__ void __launch_bounds__(1024) k_primary(const RtConsts* __restrict__ k
 // brightness, fcolord, rayleigh rgb and skyAmount) and its march state to a
 // 3-float4 record (long_pack).
 constexpr uint32_t kShadowRec = 3;
+
+// Lanes idle before a long-ray wave refills them: amortises the refill's divergent
+// prologue against the idle lanes it leaves.
+constexpr uint32_t kRefillIdle = 4;
 
 // color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
 __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, float4 fog, float4 ray,
@@ -886,7 +568,7 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
                                                     float4* __restrict__ shrec, uint32_t long_cap,
                                                     uint32_t* __restrict__ counters, RtStats* stats)
 {
-    // hits the primary pass did not shade itself (all of them for k_primary / k_march)
+    // hits k_trace could not queue on its CU (hit ring full)
     const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
     if (n_hits == 0u) return; // everything was shaded inside k_trace
     __shared__ uint32_t lds[kNoiseLdsWords];
@@ -1354,7 +1036,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         }
     };
 
-    // ---- one 8x8 primary unit (as k_primary) ----
+    // ---- one 8x8 primary unit ----
     auto do_unit = [&](uint32_t f, uint32_t u) {
         const Ctx cf = frame_ctx(c, ft, f);
         uint32_t px, py;
@@ -1616,7 +1298,6 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
         // rays of 8 lanes (512 threads, <= 256 blocks for <= 16 frames).  Fewer lanes per ray
         // lengthen a step (3 noise rounds instead of 1) but keep a 12-frame prepass in one
         // round: 1.4 -> 0.7 ms per batch, +1.8% at C3 (32 rays of 32 lanes took two rounds).
-        // RT_PREPASS_CFG=<threads>,<lanes per ray> overrides (A/B runs).
         auto go = [&](auto bs_tag, auto lpr_tag) {
             constexpr int BS = decltype(bs_tag)::value, LPR = decltype(lpr_tag)::value;
             dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / (BS / LPR), n), block(BS);
@@ -1627,19 +1308,9 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
                 hipLaunchKernelGGL((k_camerarays_group<false, BS, LPR>), grid, block, 0, a.stream, a.consts,
                                    a.perm2d, a.grad, out, a.stats, ft);
         };
-        using C1024 = std::integral_constant<int, 1024>;
         using C512 = std::integral_constant<int, 512>;
         using C256 = std::integral_constant<int, 256>;
         using L32 = std::integral_constant<int, 32>;
-        static const char* cfg = std::getenv("RT_PREPASS_CFG");
-        int cbs = 0, clpr = 0;
-        if (cfg && std::sscanf(cfg, "%d,%d", &cbs, &clpr) == 2) {
-            if (cbs == 1024 && clpr == 32) return go(C1024{}, L32{});
-            if (cbs == 1024 && clpr == 16) return go(C1024{}, std::integral_constant<int, 16>{});
-            if (cbs == 1024 && clpr == 8) return go(C1024{}, std::integral_constant<int, 8>{});
-            if (cbs == 512 && clpr == 8) return go(C512{}, std::integral_constant<int, 8>{});
-            if (cbs == 256 && clpr == 4) return go(C256{}, std::integral_constant<int, 4>{});
-        }
         if (n <= 2) go(C256{}, L32{});
         else if (n <= 4) go(C512{}, L32{});
         else go(C512{}, std::integral_constant<int, 8>{});
@@ -1655,40 +1326,17 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
 }
 
 template <int L>
-void launch_tracescreen_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,
-                          uint32_t stride)
-{
-    // single-frame pipeline: frame 0 of the table
-    const float2* cells = a.frames_host.cells[0];
-    uint32_t* out8 = a.frames_host.out8[0];
-    float4* out32 = a.frames_host.out32[0];
-    uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
-    if (first >= total) return;
-    uint32_t n_tiles = (total - first + stride - 1) / stride;
-    uint32_t n_units = n_tiles * 16u;
-    uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
-    uint32_t need = (n_units + 15u) / 16u; // 16 waves per block
-    if (need < blocks) blocks = need;
-    (void)hipMemsetAsync(a.queue, 0, sizeof(uint32_t), a.stream);
-    dim3 grid(blocks), block(1024);
-    if (a.stats)
-        hipLaunchKernelGGL((k_tracescreen<L, true>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, cells, out8,
-                           out32, ox, oy, ex, ey, tiles_x, first, stride, n_units, a.queue, a.stats);
-    else
-        hipLaunchKernelGGL((k_tracescreen<L, false>), grid, block, 0, a.stream, a.consts, a.perm2d, a.grad, cells,
-                           out8, out32, ox, oy, ex, ey, tiles_x, first, stride, n_units, a.queue, a.stats);
-}
-
-template <int L>
 void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,
                     uint32_t stride)
 {
-    const float2* cells = a.frames_host.cells[0]; // single-frame primaries (staged, refill)
     UnitMap m;
     uint32_t tiles_x = (ex + 31) / 32, tiles_y = (ey + 31) / 32, total = tiles_x * tiles_y;
     // a batch rotates the shards over its frames (frame f traces shard (first + f) % stride), so
-    // each rank's share of a batch mixes the tile classes of every shard: the ranks' work evens
-    // out (the slowest of 8 ranks was 7% above the mean with a fixed deal at C3)
+    // each rank's share of a batch mixes the tile classes of every shard.  Measured at C3 with
+    // 12-frame batches (one-GPU shard simulation): the slowest of 4 ranks
+    // went from 4-7% above the mean to 3.49x/4 scaling; N=2 and N=8 within noise.  n_units is
+    // the largest shard's; the trailing units of a smaller shard map past the tile range and
+    // unit_pixel rejects every lane of them.
     const uint32_t rot = a.n_frames > 1u && stride > 1u ? 1u : 0u;
     if (!rot && first >= total) return;
     m.off_x = ox;
@@ -1706,53 +1354,27 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     dim3 blk(1024);
-    // scheduler knobs of k_trace (RT_LONG_BATCH / RT_REFILL_IDLE override for experiments)
-    static const uint32_t tune_long_batch = [] {
-        const char* e = getenv("RT_LONG_BATCH");
-        return e ? (uint32_t)atoi(e) : kLongBatch;
-    }();
-    static const uint32_t tune_refill_idle = [] {
-        const char* e = getenv("RT_REFILL_IDLE");
-        return e ? (uint32_t)atoi(e) : kRefillIdle;
-    }();
-    static const uint32_t tune_compact_live = [] {
-        const char* e = getenv("RT_COMPACT_LIVE");
-        return e ? (uint32_t)atoi(e) : kCompactLive;
-    }();
-    static const uint32_t tune_seg_live = [] {
-        const char* e = getenv("RT_SEG_LIVE");
-        const uint32_t v = e ? (uint32_t)atoi(e) : kSegLive;
-        return v < kSegLive ? v : kSegLive; // seg_finish packs at most 16 rays (4 lanes each)
-    }();
     // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
-    const char* seg_env = getenv("RT_SEG"); // RT_SEG=0/1 forces it off/on (read per launch: tests flip it)
-    const int seg_mode = seg_env ? atoi(seg_env) : -1;
-    // (single frames only: batches have units enough, and a segment's lanes share one eye)
-    const bool seg = L == RT_NOMADPLAINS && tune_seg_live > 0 && m.n_frames == 1u &&
-                     (seg_mode >= 0 ? seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
+    // (single frames only: batches have units enough, and a segment's lanes share one eye);
+    // a.seg_mode (device flags RT_DEVICE_SEG_TAIL_*) forces it off or on
+    const bool seg = L == RT_NOMADPLAINS && m.n_frames == 1u &&
+                     (a.seg_mode >= 0 ? a.seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
         (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
-    const int pipe = a.pipeline;
-    if (pipe != RT_PIPELINE_REFILL) hipLaunchKernelGGL(k_order, dim3(m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
-    // primary (+ shading in the fused kernel); hits it did not shade go to the global list
+    hipLaunchKernelGGL(k_order, dim3(m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
+    // primary + shading + long rays; what did not fit the CU's rings goes to the global lists
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        if (pipe == RT_PIPELINE_REFILL)
-            hipLaunchKernelGGL((k_march<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.perm2d, a.grad, cells, m,
-                               a.res, a.hitlist, a.queue, a.stats);
-        else if (pipe == RT_PIPELINE_STAGED)
-            hipLaunchKernelGGL((k_primary<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.perm2d, a.grad, cells,
-                               m, a.order, a.res, a.hitlist, a.queue, a.stats);
-        else if (seg)
+        if (seg)
             hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
                                m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
-                               a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
+                               a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
         else
             hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
                                m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
-                               a.queue, a.stats, tune_long_batch, tune_refill_idle, tune_compact_live, tune_seg_live);
+                               a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
@@ -1808,15 +1430,6 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t
                            uint32_t stride)
 {
     if (ex == 0 || ey == 0 || stride == 0) return;
-    if (a.pipeline == RT_PIPELINE_MEGA) {
-        switch (a.landscape) {
-        case RT_TESTING: launch_tracescreen_l<RT_TESTING>(a, ox, oy, ex, ey, first, stride); break;
-        case RT_SIMPLE: launch_tracescreen_l<RT_SIMPLE>(a, ox, oy, ex, ey, first, stride); break;
-        case RT_GREENROCKS: launch_tracescreen_l<RT_GREENROCKS>(a, ox, oy, ex, ey, first, stride); break;
-        default: launch_tracescreen_l<RT_NOMADPLAINS>(a, ox, oy, ex, ey, first, stride); break;
-        }
-        return;
-    }
     switch (a.landscape) {
     case RT_TESTING: launch_split_l<RT_TESTING>(a, ox, oy, ex, ey, first, stride); break;
     case RT_SIMPLE: launch_split_l<RT_SIMPLE>(a, ox, oy, ex, ey, first, stride); break;

@@ -113,8 +113,8 @@ struct rt_device_s {
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
-    int pipeline = RT_PIPELINE_SPLIT; // RT_PIPELINE env: "mega" = single kernel, "refill" / "staged" = unfused primary
-    float4* samples = nullptr;     // split pipeline buffers, sized for samples_cap samples
+    int seg_mode = -1;             // k_trace segment tail: -1 auto, 0 off, 1 on (RT_DEVICE_SEG_TAIL_*)
+    float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
     float4* res = nullptr;
     uint32_t* hitlist = nullptr;
     uint32_t* order = nullptr;
@@ -438,7 +438,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.stats = (dev->flags & RT_DEVICE_STATS) ? dev->stats : nullptr;
     a.queue = dev->queue;
     a.num_cus = dev->num_cus;
-    a.pipeline = dev->pipeline;
+    a.seg_mode = dev->seg_mode;
     a.samples = dev->samples;
     a.res = dev->res;
     a.hitlist = dev->hitlist;
@@ -476,7 +476,7 @@ int check_texture(Shader* s)
     return RT_OK;
 }
 
-// Split-pipeline buffers: per AA sample of every whole 32x32 tile, one shaded
+// Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded
 // colour (16 B), one primary RayResult (48 B), one hit-list slot (4 B), the
 // shading inputs of a long shadow ray (48 B) and an AO occlusion count (4 B); the
 // global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
@@ -564,14 +564,10 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
     HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
-    if (const char* p = getenv("RT_PIPELINE"))
-        d->pipeline = strcmp(p, "mega") == 0     ? RT_PIPELINE_MEGA
-                      : strcmp(p, "refill") == 0 ? RT_PIPELINE_REFILL
-                      : strcmp(p, "staged") == 0 ? RT_PIPELINE_STAGED
-                                                 : RT_PIPELINE_SPLIT;
+    if ((flags & RT_DEVICE_SEG_TAIL_OFF) && (flags & RT_DEVICE_SEG_TAIL_ON))
+        return fail(RT_ERR_INVALID, "RT_DEVICE_SEG_TAIL_OFF and RT_DEVICE_SEG_TAIL_ON are exclusive");
+    d->seg_mode = (flags & RT_DEVICE_SEG_TAIL_OFF) ? 0 : (flags & RT_DEVICE_SEG_TAIL_ON) ? 1 : -1;
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
-    if (const char* g = getenv("RT_GRID_CUS")) // persistent-grid cap (experiments: CU share per frame in flight)
-        if (atoi(g) > 0 && atoi(g) < d->num_cus) d->num_cus = atoi(g);
     *out = d.release();
     return RT_OK;
 }
@@ -1066,24 +1062,17 @@ int rt_terrain_feed_wait(rt_compute cam, float* camera_results)
 
 extern "C++" {
 namespace {
-// every value a captured launch bakes in: pointers, sizes, modes, and the environment
-// switches the launch code reads per call
+// every value a captured launch bakes in: pointers, sizes and modes
 void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
 {
     const uint64_t v[] = {(uint64_t)(uintptr_t)a.stream, (uint64_t)a.landscape, (uint64_t)(uintptr_t)a.consts,
                           (uint64_t)(uintptr_t)a.perm2d, (uint64_t)(uintptr_t)a.grad, (uint64_t)(uintptr_t)a.stats,
-                          (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)a.pipeline,
+                          (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(a.seg_mode + 1),
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.hitlist,
                           (uint64_t)(uintptr_t)a.shrec, (uint64_t)a.long_cap, (uint64_t)(uintptr_t)a.fin,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));
-}
-
-void key_env(std::vector<uint64_t>& k)
-{
-    const char* seg = getenv("RT_SEG"); // read per tracescreen launch (launch_split_l)
-    k.push_back(seg ? (uint64_t)(1 + atoi(seg)) : 0);
 }
 
 // Replay g (capturing `launches` on dev->stream first when its key changed).  Stream
@@ -1294,7 +1283,6 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
         if (graphs) {
             std::vector<uint64_t> kt_key;
             key_launch(kt_key, la_scr);
-            key_env(kt_key);
             key_frames(kt_key, ft);
             const uint64_t extra[] = {(uint64_t)dev->width, (uint64_t)dev->height, (uint64_t)shard_rank,
                                       (uint64_t)shard_count};

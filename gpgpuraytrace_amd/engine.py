@@ -157,10 +157,13 @@ class Compute:
 class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
-    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False):
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, seg_tail=None):
+        """seg_tail: None = the trace kernel picks its tail form per launch; False / True force
+        it off / on (RT_DEVICE_SEG_TAIL_OFF / _ON; same bits either way)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
-                      | (_native.RT_DEVICE_GRAPH if graph else 0))
+                      | (_native.RT_DEVICE_GRAPH if graph else 0)
+                      | {None: 0, False: _native.RT_DEVICE_SEG_TAIL_OFF, True: _native.RT_DEVICE_SEG_TAIL_ON}[seg_tail])
         self._h = None
 
     def create(self):
@@ -589,11 +592,19 @@ class FrameRing:
     def next_slot(self):
         return self.slots[self.frame % self.depth]
 
-    def render_batch(self, shard_rank=0, shard_count=1, present=True):
-        """Queue the next `batch` frames as one batch on the next slot group; returns their
-        Devices in frame order (each complete once its stream reaches this point)."""
+    def group(self, frames=None):
+        """The next slot group (its first `frames` slots, default all `batch`)."""
         g = (self.frame // self.batch) % self.depth
-        group = self.slots[g * self.batch:(g + 1) * self.batch]
+        n = self.batch if frames is None else int(frames)
+        if not 1 <= n <= self.batch:
+            raise ValueError("frames must be 1..batch")
+        return self.slots[g * self.batch:g * self.batch + n]
+
+    def render_batch(self, shard_rank=0, shard_count=1, present=True, frames=None):
+        """Queue the next `batch` frames (or the first `frames` of them: a partial batch) as one
+        batch on the next slot group; returns their Devices in frame order (each complete once
+        its stream reaches this point)."""
+        group = self.group(frames)
         render_batch([t for _, t in group], shard_rank, shard_count)
         devs = [d for d, _ in group]
         if present:

@@ -1,14 +1,29 @@
 """Frame sharding across GPUs (one process per GPU, torch.distributed over RCCL).
 
-The reference renders on one D3D11 adapter.  Here a frame is split tile-cyclically:
-32x32-pixel tiles in row-major order, tile t belongs to rank t % world.  Every rank
-recomputes the 1024-ray prepass (tiny, deterministic) so no collective precedes the
-trace; afterwards each rank packs its tiles (1024 pixels per tile, RGBA8) and ONE
-gather assembles the frame on rank 0.  Cyclic dealing balances the ~10x cost spread
+The reference renders on one D3D11 adapter (Terrain.cpp:105-136 dispatches the frame's
+tiles on it).  Here a frame is split tile-cyclically: 32x32-pixel tiles in row-major order;
+shard s of N is the tiles t with t % N == s.  Cyclic dealing balances the ~10x cost spread
 between sky and terrain tiles.
 
-The mapping here is the same one the HIP kernels use (rt_kernels.h rt_shard_tiles,
-k_shard_copy); the host functions are used by the CPU (gloo) tests.
+bench.py renders BATCHES of B frames (rt_terrain_render_batch) and rotates the shards over a
+batch: frame f of rank r's batch traces shard (r + f) % N, so every rank's batch mixes every
+shard's tile classes.  BatchPlan holds that bookkeeping and run_batch() is the one sequence of
+steps every rank runs per batch; bench.py drives it with device ops (HIP kernels, RCCL) and
+tests/test_dist.py with host ops (numpy, gloo), so the CPU tests exercise the same code:
+
+  1. prepass: split (default): rank r runs the camerarays prepass of frames
+     [r*chunk, (r+1)*chunk) of the batch, chunk = ceil(B/N) (ranks past the last frame run an
+     empty range), and an all-gather hands every rank all B frames' CameraResults (16 KiB per
+     frame).  This is a SECOND collective per batch: SURVEY.md section 8e planned per-rank
+     prepass recompute instead; the split removes an N-fold repeat of latency-bound prepass
+     rays.  Unsplit: every rank runs every frame's prepass.
+  2. trace: each rank traces its shard of every frame (setTargetDepths + tracescreen).
+  3. pack: frame f's shard (r + f) % N goes to packed[f * max_bytes : ...] (k_shard_copy;
+     1024 RGBA8 pixels per tile, tiles in ascending order).
+  4. ONE gather of the packed buffers to rank 0, which unpacks rank src's frame f as shard
+     (src + f) % N from gathered[src][f * max_bytes : ...].
+
+The tile mapping is the one the HIP kernels use (rt_kernels.h rt_shard_tiles, k_shard_copy).
 """
 import numpy as np
 
@@ -68,3 +83,108 @@ def gather_frame(dist, packed, width, height, rank, world, unpack):
         for r in range(1, world):
             unpack(r, bufs[r])
     return bufs
+
+
+def frame_shard(rank, f, world):
+    """The shard frame f of a batch traces on `rank` (per-frame rotation; rt_kernels.h
+    rt_launch_tracescreen).  A single frame (f = 0) traces shard `rank`."""
+    return (rank + f) % world if world > 1 else 0
+
+
+class BatchPlan:
+    """Bookkeeping of one B-frame batch on `world` ranks (see the module docstring)."""
+
+    CAMERA_FLOATS = 1024 * 4  # CameraResults of one frame: float4[1024]
+
+    def __init__(self, width, height, batch, world, split_prepass=True):
+        if not 1 <= batch <= 16:
+            raise ValueError("batch must be 1..16 frames (RT_MAX_BATCH)")
+        self.width, self.height, self.batch, self.world = int(width), int(height), int(batch), int(world)
+        self.split_prepass = bool(split_prepass) and self.world > 1
+        self.chunk = -(-self.batch // self.world)
+        self.max_bytes = max(shard_bytes(self.width, self.height, r, self.world) for r in range(self.world))
+
+    def shard(self, rank, f):
+        return frame_shard(rank, f, self.world)
+
+    def prepass_range(self, rank):
+        """(first, count) of the frames whose prepass `rank` runs (count may be 0)."""
+        first = min(rank * self.chunk, self.batch)
+        return first, max(0, min(self.batch - first, self.chunk))
+
+    def camera_slice(self, rank):
+        """rank's part of the all-gathered CameraResults buffer (world * chunk frames), in floats."""
+        n = self.chunk * self.CAMERA_FLOATS
+        return slice(rank * n, (rank + 1) * n)
+
+    def camera_floats(self):
+        return self.world * self.chunk * self.CAMERA_FLOATS
+
+    def packed_bytes(self):
+        return self.batch * self.max_bytes
+
+    def pack_offset(self, f):
+        return f * self.max_bytes
+
+    def packs(self, rank, frames=None):
+        """[(f, shard, byte offset)] this rank packs, frame order."""
+        n = self.batch if frames is None else frames
+        return [(f, self.shard(rank, f), self.pack_offset(f)) for f in range(n)]
+
+    def unpacks(self, frames=None):
+        """[(src rank, f, shard, byte offset in src's gathered buffer)] rank 0 unpacks."""
+        n = self.batch if frames is None else frames
+        return [(src, f, self.shard(src, f), self.pack_offset(f)) for src in range(1, self.world) for f in range(n)]
+
+
+def run_batch(plan, rank, ops, frames=None):
+    """One batch on this rank.  `ops` supplies the actions (bench.py: HIP + RCCL; tests: numpy
+    + gloo): prepass(first, count), all_gather_cameras(), trace(), render() (prepass + trace of
+    every frame, the unsplit path), pack(f, shard, offset), gather(), unpack(src, f, shard,
+    offset), present().  `frames` < plan.batch renders a partial batch (its first frames)."""
+    n = plan.batch if frames is None else int(frames)
+    if plan.split_prepass:
+        first, count = plan.prepass_range(rank)
+        count = max(0, min(count, n - first))
+        ops.prepass(first, count)
+        ops.all_gather_cameras()
+        ops.trace()
+    else:
+        ops.render()
+    if plan.world > 1:
+        for f, shard, off in plan.packs(rank, n):
+            ops.pack(f, shard, off)
+        ops.gather()
+        if rank == 0:
+            for src, f, shard, off in plan.unpacks(n):
+                ops.unpack(src, f, shard, off)
+    ops.present()
+
+
+class Collectives:
+    """The two collectives of run_batch over torch.distributed: device-memory RCCL
+    (backend "nccl") or host-staged gloo (rehearsals on one GPU, CPU tests)."""
+
+    def __init__(self, dist, backend, rank, world):
+        self.dist, self.backend, self.rank, self.world = dist, backend, rank, world
+
+    def all_gather(self, out, mine, group=None):
+        if self.backend == "nccl":
+            self.dist.all_gather_into_tensor(out, mine, group=group)
+            return
+        import torch
+        parts = [torch.empty(mine.numel(), dtype=mine.dtype) for _ in range(self.world)]
+        self.dist.all_gather(parts, mine.cpu(), group=group)
+        out.copy_(torch.cat(parts).to(out.device))
+
+    def gather(self, t, outs):
+        """t from every rank into outs[src] on rank 0 (outs ignored elsewhere)."""
+        if self.backend == "nccl":
+            self.dist.gather(t, outs if self.rank == 0 else None, dst=0)
+            return
+        import torch
+        lst = [torch.empty(t.numel(), dtype=t.dtype) for _ in range(self.world)] if self.rank == 0 else None
+        self.dist.gather(t.cpu(), lst, dst=0)
+        if self.rank == 0:
+            for o, part in zip(outs, lst):
+                o.copy_(part.to(o.device))

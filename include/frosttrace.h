@@ -41,11 +41,21 @@ enum {
 /* DeviceDirect3D.cpp:113-126 swap-chain format R8G8B8A8_UNORM is always
  * produced; RT_DEVICE_FLOAT_OUTPUT additionally keeps the pre-quantisation
  * float4 colour (texOut's float4 value, tracescreen.hlsl:75) for parity. */
-enum { RT_DEVICE_FLOAT_OUTPUT = 1u, RT_DEVICE_STATS = 2u, RT_DEVICE_GRAPH = 4u };
+enum {
+    RT_DEVICE_FLOAT_OUTPUT = 1u,
+    RT_DEVICE_STATS = 2u,
+    RT_DEVICE_GRAPH = 4u,
+    RT_DEVICE_SEG_TAIL_OFF = 8u,
+    RT_DEVICE_SEG_TAIL_ON = 16u
+};
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
  * every frame; a changed launch argument (shader swap, buffers, shard, stats) re-captures.
- * No reference counterpart (the D3D frame loop re-records its dispatches every frame). */
+ * No reference counterpart (the D3D frame loop re-records its dispatches every frame).
+ * RT_DEVICE_SEG_TAIL_OFF / _ON: force the trace kernel's octave-parallel tail form off or on
+ * (default: chosen per launch, on when a single frame's shard has fewer than 2 work units per
+ * wave of the grid).  Both forms produce the same bits; the flags exist for the parity tests
+ * and A/B timing.  Setting both fails with RT_ERR_INVALID. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };

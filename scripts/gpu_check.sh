@@ -1,8 +1,12 @@
 #!/bin/bash
-# GPU round trip: parity tests, a short bench, and a kernel-trace profile.
-cd /tmp && export TMPDIR=/tmp
-cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/check; mkdir -p $O
-timeout -k 10 400 python3 -m pytest tests -m gpu -x -q > $O/pytest.log 2>&1; rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/bench.log 2>&1 && tail -1 $O/bench.log && \
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $O/kt.log 2>&1 && echo kt ok
+# One GPU call: the -m gpu tests, the default bench line (with CPU baseline, parity, companions),
+# then the N>1 rehearsal (bench.py's multi-rank path on one GPU through gloo).
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  > gpurun_out/check_tests.log 2>&1 || { tail -30 gpurun_out/check_tests.log; exit 1; }
+tail -2 gpurun_out/check_tests.log
+timeout -k 10 400 python3 bench.py > gpurun_out/check_bench.json 2> gpurun_out/check_bench.err \
+  || { tail -20 gpurun_out/check_bench.err; exit 1; }
+tail -c 3000 gpurun_out/check_bench.json
+[ -n "$NOREH" ] && exit 0
+bash scripts/rehearse_multi.sh

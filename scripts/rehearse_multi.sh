@@ -7,8 +7,8 @@ export RT_BENCH_SAME_GPU=1 RT_DIST_BACKEND=gloo
 PORT=29500
 run() { local n=$1; shift; PORT=$((PORT + 1))
   timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $PORT bench.py --gpus $n --verify --no-cpu-baseline "$@" > gpurun_out/reh/n$n.json 2> gpurun_out/reh/n$n.err \
-    || { echo "n=$n failed"; tail -20 gpurun_out/reh/n$n.err; return 1; }
-  tail -1 gpurun_out/reh/n$n.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['n_gpus'], d['config']['parallelism'], '->', d['config'].get('verify'))"
+    --master-port $PORT bench.py --gpus $n --verify --no-cpu-baseline "$@" > gpurun_out/reh/$PORT.json 2> gpurun_out/reh/$PORT.err \
+    || { echo "n=$n failed"; tail -20 gpurun_out/reh/$PORT.err; return 1; }
+  tail -1 gpurun_out/reh/$PORT.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['n_gpus'], d['config']['parallelism'], '->', d['config'].get('verify'))"
 }
-run 2 && run 4 && run 3 --split-prepass 0 --batch 5 && run 4 --batch 5  # 4 ranks x 2 frames: rank 3 has none
+run 2 --no-companions && run 3 --no-companions --steps 10 && run 3 --split-prepass 0 --batch 5 --steps 5 --no-companions && run 4 --batch 5 --steps 5 --no-companions  # 4 ranks x 2 frames: rank 3 has none

@@ -166,3 +166,20 @@ def render(nz, fr):
                           rgba8.ctypes.data_as(C.POINTER(C.c_uint8)), _fp(steps), C.byref(st))
     return {"camera_results": cr.reshape(1024, 4), "cell_distance": cd.reshape(1024, 2), "rgba32f": rgba,
             "rgba8": rgba8, "primary_steps": steps, "stats": st.as_dict()}
+
+
+def render_rows(nz, fr):
+    """Prepass + setTargetDepths + tracescreen on fr's rows (row_begin::row_step) only.
+    Returns (rgba32f, rgba8, camera_results, cell_distance, stats); rows outside the sample
+    stay zero."""
+    W, H = fr.width, fr.height
+    cr = np.zeros(1024 * 4, np.float32)
+    cd = np.zeros(1024 * 2, np.float32)
+    rgba = np.zeros((H, W, 4), np.float32)
+    rgba8 = np.zeros((H, W, 4), np.uint8)
+    st = Stats()
+    lib().ro_camerarays(C.byref(nz), C.byref(fr), _fp(cr), C.byref(st))
+    lib().ro_set_target_depths(_fp(cr), _fp(cd))
+    lib().ro_tracescreen(C.byref(nz), C.byref(fr), _fp(cd), _fp(rgba), rgba8.ctypes.data_as(C.POINTER(C.c_uint8)),
+                         None, C.byref(st))
+    return rgba, rgba8, cr.reshape(1024, 4), cd.reshape(1024, 2), st.as_dict()

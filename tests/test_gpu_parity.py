@@ -2,7 +2,6 @@
 golden fixtures.  Bar: bit-exact float32 colours and UNORM8 pixels, identical
 step / noise3d counts.  Run on the GPU box with `pytest -m gpu`."""
 import ctypes as C
-import os
 
 import numpy as np
 import pytest
@@ -31,11 +30,10 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         pipeline="split", ao=0, graph=False):
+         seg_tail=None, ao=0, graph=False):
     import gpgpuraytrace_amd as G
-    os.environ["RT_PIPELINE"] = pipeline
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
-                                    stats=stats, graph=graph)
+                                    stats=stats, graph=graph, seg_tail=seg_tail)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -170,18 +168,16 @@ def test_density_bitexact(land):
 
 
 # --- whole frames vs the golden oracle frames ----------------------------------------------
-@pytest.mark.parametrize("pipeline", ["split", "split-noseg", "staged", "mega", "refill"])
+@pytest.mark.parametrize("tail", ["auto", "noseg", "seg"])
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
-def test_frame_bitexact_device_path(spec, pipeline, monkeypatch):
-    """split: the fused k_trace; at these sizes (few units per wave) it runs the segment tail,
-    split-noseg forces the plain form the large single-GPU frames use (RT_SEG=0)."""
-    if pipeline == "split-noseg":
-        monkeypatch.setenv("RT_SEG", "0")
-        pipeline = "split"
+def test_frame_bitexact_device_path(spec, tail):
+    """auto: k_trace picks its tail form (at these sizes, few units per wave: the segment
+    tail); noseg forces the plain form the large single-GPU frames use, seg the segment tail."""
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True, pipeline=pipeline, ao=ao)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True,
+                    seg_tail={"auto": None, "noseg": False, "seg": True}[tail], ao=ao)
     ter.render_device()
     dev.present()
     img, img8 = dev.readback_float(), dev.readback()
@@ -271,6 +267,61 @@ def test_1080p_full_frame_rows_and_properties(pose):
     dev.destroy()
 
 
+# BASELINE.json GPU configs at their full sizes (configs[1], [2], [4]): the product path vs the
+# oracle on a row sample (rows r0::step; the oracle renders only those rows).  C3 is the
+# bench's headline workload, C5 the 4K / 1024-step / 4-AO one.
+BASELINE_CONFIGS = {  # name: (W, H, max_steps, ao, row_step)
+    "c2": (1280, 720, 256, 0, 8),
+    "c3": (1920, 1080, 512, 1, 8),
+    "c5": (3840, 2160, 1024, 4, 36),
+}
+
+
+def _config_rows(name, pose, r0):
+    w, h, ms, ao, step = BASELINE_CONFIGS[name]
+    consts = _consts_1080p_like(w, h, pose)
+    fr = O.make_frame(consts, max_steps=ms, ao=ao, rows=(r0, h, step))
+    return consts, O.render_rows(O.noise_tables(), fr), slice(r0, h, step)
+
+
+@pytest.mark.parametrize("pose", ["reset", "lookdown"])
+@pytest.mark.parametrize("name", sorted(BASELINE_CONFIGS))
+def test_baseline_config_rows_bitexact(name, pose):
+    """rt_terrain_render (the device path: prepass -> device setTargetDepths -> k_trace) at the
+    config's full size, step cap and AO count: float32 colour and UNORM8 bit-exact against the
+    oracle on the row sample, the whole CameraResults / CellDistance exact, every pixel written."""
+    w, h, ms, ao, step = BASELINE_CONFIGS[name]
+    consts, (ref, ref8, cr, cd, _), rows = _config_rows(name, pose, 5)
+    dev, ter = make(consts, max_steps=ms, ao=ao)
+    ter.render_device()
+    img, img8 = dev.readback_float(), dev.readback()
+    assert bits_equal(img[rows], ref[rows])
+    assert np.array_equal(img8[rows], ref8[rows])
+    assert np.array_equal(_device_cells(ter), cd)
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, cr)
+    assert np.all(img8[..., 3] == 255) and np.all(img[..., 3] == 1.0)
+    dev.destroy()
+
+
+@pytest.mark.parametrize("name", ["c2", "c3"])
+def test_baseline_config_batch_rows_bitexact(name):
+    """The bench's entry point: one rt_terrain_render_batch of 4 frames (reset, look-down,
+    reset, look-down) at the config's size; every frame equals the oracle on its row sample."""
+    from gpgpuraytrace_amd import engine as E
+    w, h, ms, ao, step = BASELINE_CONFIGS[name]
+    poses = ["reset", "lookdown", "reset", "lookdown"]
+    refs = {p: _config_rows(name, p, 3) for p in ("reset", "lookdown")}
+    frames = [make(refs[p][0], max_steps=ms, ao=ao) for p in poses]
+    E.render_batch([t for _, t in frames])
+    for (dev, _), p in zip(frames, poses):
+        _, (ref, ref8, _, _, _), rows = refs[p]
+        assert bits_equal(dev.readback_float()[rows], ref[rows])
+        assert np.array_equal(dev.readback()[rows], ref8[rows])
+    for d, _ in frames:
+        d.destroy()
+
+
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_shards_assemble_to_full_frame(world):
     import torch
@@ -342,7 +393,6 @@ def test_frame_ring_in_flight_bitexact():
     every frame while the other slots' frames are still running; each slot's last frame equals
     the golden frame of its camera."""
     import gpgpuraytrace_amd as G
-    os.environ["RT_PIPELINE"] = "split"
     gold = GI.load()
     specs = [GI.FRAMES[0], GI.FRAMES[1]]  # nomadplains 64x48, reset / lookdown
     cams = []
@@ -421,7 +471,6 @@ def test_graph_constants_shards_and_swap():
 
 def test_frame_ring_graphs_bitexact():
     import gpgpuraytrace_amd as G
-    os.environ["RT_PIPELINE"] = "split"
     gold = GI.load()
     spec = GI.FRAMES[1]
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
@@ -439,13 +488,12 @@ def test_frame_ring_graphs_bitexact():
 
 
 # --- frame batches (rt_terrain_render_batch) ----------------------------------------------
-def _batch(specs, stats=False, graph=False, pipeline="split"):
+def _batch(specs, stats=False, graph=False):
     """One (Device, Terrain) per spec, made as the single-frame tests make them."""
     out = []
     for spec in specs:
         land, pose, w, h, aa, ms, ao = GI.unpack(spec)
-        out.append(make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=stats, ao=ao, graph=graph,
-                        pipeline=pipeline))
+        out.append(make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=stats, ao=ao, graph=graph))
     return out
 
 
@@ -516,7 +564,6 @@ def test_batch_shards_graphs_and_ring():
     for frames in ranks:
         for d, _ in frames:
             d.destroy()
-    os.environ["RT_PIPELINE"] = "split"
     cam = FixedCamera(GI.consts(64, 48, "lookdown"))
     ring = G.FrameRing(64, 48, depth=2, batch=3, camera=cam)
     for _, ter in ring.slots:
@@ -527,6 +574,56 @@ def test_batch_shards_graphs_and_ring():
     for dev, _ in ring.slots:
         assert np.array_equal(dev.readback(), GI.load()[GI.frame_key(*GI.FRAMES[1]) + "_rgba8"])
     ring.destroy()
+
+
+@pytest.mark.parametrize("w,h,world,split", [(64, 48, 3, True), (64, 48, 3, False), (50, 36, 3, True),
+                                             (64, 48, 2, True)])
+def test_batch_ragged_rotated_shards_bitexact(w, h, world, split):
+    """bench.py's N>1 batch on one GPU, following parallel.BatchPlan: 3-frame batches whose tile
+    count is not a multiple of N (64x48 and 50x36: 4 tiles, shards of 2/1/1), so rotated frames
+    trace shards smaller than the launch's unit count and the trailing units map past the tile
+    range.  Each rank runs its prepass range (split) into its slice of a shared CameraResults
+    buffer (what the all-gather produces) and traces from it, or renders the whole batch
+    (unsplit); packs frame f's shard (r + f) % N at the plan's offsets; rank 0 unpacks every
+    other rank's frames.  Every assembled frame equals its golden frame."""
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    specs = [("nomadplains", "reset", w, h, 1, 0), ("nomadplains", "lookdown", w, h, 1, 0),
+             ("nomadplains", "reset", w, h, 1, 0)]
+    gold = GI.load()
+    have = all(GI.frame_key(*s) + "_rgba8" in gold for s in specs)
+    consts = {p: GI.consts(w, h, p) if have else _consts_1080p_like(w, h, p) for p in ("reset", "lookdown")}
+    # 50x36 has no golden frame: the oracle renders the reference frames here
+    want = {p: gold[GI.frame_key("nomadplains", p, w, h, 1, 0) + "_rgba8"] if have
+            else O.render(O.noise_tables(), O.make_frame(consts[p]))["rgba8"] for p in consts}
+    plan = P.BatchPlan(w, h, len(specs), world, split_prepass=split)
+    ranks = [[make(consts[s[1]]) for s in specs] for _ in range(world)]
+    cams = torch.full((plan.camera_floats(),), float("nan"), dtype=torch.float32, device="cuda:0")
+    if split:
+        for r, frames in enumerate(ranks):
+            first, count = plan.prepass_range(r)
+            # frame f's CameraResults land at f * 16 KiB: rank r's frames fill its plan.camera_slice(r)
+            E.prepass_batch([t for _, t in frames], first, count, cams.data_ptr())
+    packed = [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    for r, frames in enumerate(ranks):
+        ters = [t for _, t in frames]
+        if split:
+            E.trace_batch(ters, r, world, cams.data_ptr())
+        else:
+            E.render_batch(ters, r, world)
+        for f, shard, off in plan.packs(r):
+            E.shard_pack(frames[f][0], shard, world, packed[r].data_ptr() + off)
+        for d, _ in frames:
+            d.synchronize()
+    for src, f, shard, off in plan.unpacks():
+        E.shard_unpack(ranks[0][f][0], shard, world, packed[src].data_ptr() + off)
+    for (d, _), s in zip(ranks[0], specs):
+        assert np.array_equal(d.readback(), want[s[1]]), s
+    for frames in ranks:
+        for d, _ in frames:
+            d.destroy()
 
 
 def test_batch_split_prepass_bitexact():
@@ -668,7 +765,6 @@ def test_fly_through_device_feed_matches_oracle_feed():
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import camera as CAM
     from gpgpuraytrace_amd.flyby import Flyby, fly_through
-    os.environ["RT_PIPELINE"] = "split"
     W, H, frames, dt = 64, 48, 6, 1.0 / 25.0
     cam = CAM.Camera(W, H)
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H)
