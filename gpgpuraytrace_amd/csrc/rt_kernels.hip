@@ -26,37 +26,45 @@ using rtm::f3;
 
 namespace {
 
-// LDS image: paired lane-private gradients gxy (32 KiB) + gz (32 KiB), then the
-// perm2D lattice (64 KiB); see rts::NoiseView.
-constexpr int kGxyWords = 128 * 16 * 4;
-constexpr int kGzWords = 128 * 32 * 2;
-constexpr int kGradWords = kGxyWords + kGzWords;
+// LDS image (rts::NoiseView): perm2D texels at offset 0 (64 KiB), the paired lane-private
+// gradients gxy at kLdsGxy (32 KiB) and gz at kLdsGz (32 KiB, 8 of every 16 B used), then the
+// octave constants (NoiseView::oct / colt): nomadplains FBM (S, 0.35 S, 1/S, 0) for
+// N = 0..RT_NP_OCTAVES + 2 and colour FBM (S, 1/S) for N = 0..RT_COL_OCTAVES + 2 (the entries past
+// the last octave are padding).  A kernel declares it as its ONLY static LDS array, so it sits
+// at LDS address 0 and the texel address needs no base (other LDS a kernel needs is carved after it).
 constexpr int kPermWords = 128 * 128;
-constexpr int kNoiseLdsWords = kGradWords + kPermWords;
+constexpr int kNpOct = RT_NP_OCTAVES + 3, kColOct = RT_COL_OCTAVES + 3;
+constexpr int kOctWords = (kNpOct * 4 + kColOct * 2 + 3) / 4 * 4;
+constexpr int kOctBase = (int)kLdsGz / 4 + (int)(kLdsGz - kLdsGxy) / 4; // words
+constexpr int kNoiseLdsWords = kOctBase + kOctWords;
+static_assert(kNoiseLdsWords % 4 == 0, "LDS carved after the noise image stays 16-byte aligned");
+static_assert(kLdsGxy == (uint32_t)kPermWords * 4u, "gxy follows the perm2D texels");
 
 __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __restrict__ perm2d,
-                                               const float4* __restrict__ grad)
+                                               const float4* __restrict__ grad, const RtConsts* __restrict__ k)
 {
-    float4* gxy = reinterpret_cast<float4*>(lds);
+    {
+        float4* oct = reinterpret_cast<float4*>(lds + kOctBase);
+        float2* colt = reinterpret_cast<float2*>(oct + kNpOct);
+        const int i = threadIdx.x;
+        if (i < kNpOct) {
+            const int n = i <= RT_NP_OCTAVES ? i : RT_NP_OCTAVES;
+            oct[i] = make_float4(k->np_scale[n], k->np_scale_y[n], k->np_rcp[n], 0.0f);
+        }
+        if (i < kColOct) {
+            const int n = i <= RT_COL_OCTAVES ? i : RT_COL_OCTAVES;
+            colt[i] = make_float2(k->col_scale[n], k->col_rcp[n]);
+        }
+    }
+    float4* gxy = reinterpret_cast<float4*>(lds + kLdsGxy / 4);
+    float4* gz = reinterpret_cast<float4*>(lds + kLdsGz / 4); // gxy's slot layout, 8 of 16 B used
     for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) {
         int e = i >> 4;
         float4 g0 = grad[e], g1 = grad[(e + 1) & 127];
         gxy[i] = make_float4(g0.x, g1.x, g0.y, g1.y);
+        gz[i] = make_float4(g0.z, g1.z, 0.0f, 0.0f);
     }
-#if RT_GZ16
-    float4* gz = reinterpret_cast<float4*>(lds + kGxyWords); // gxy's slot layout, 8 of 16 B used
-    for (int i = threadIdx.x; i < 128 * 16; i += blockDim.x) {
-        int e = i >> 4;
-        gz[i] = make_float4(grad[e].z, grad[(e + 1) & 127].z, 0.0f, 0.0f);
-    }
-#else
-    float2* gz = reinterpret_cast<float2*>(lds + kGxyWords);
-    for (int i = threadIdx.x; i < 128 * 32; i += blockDim.x) {
-        int e = i >> 5;
-        gz[i] = make_float2(grad[e].z, grad[(e + 1) & 127].z);
-    }
-#endif
-    uint4* p = reinterpret_cast<uint4*>(lds + kGradWords);
+    uint4* p = reinterpret_cast<uint4*>(lds);
     const uint4* src = reinterpret_cast<const uint4*>(perm2d);
     for (int i = threadIdx.x; i < kPermWords / 4; i += blockDim.x) p[i] = src[i];
     __syncthreads();
@@ -65,11 +73,10 @@ __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __
 __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
 {
     Ctx c;
-    c.nz.gxy = reinterpret_cast<const float4*>(lds);
-    c.nz.gz = reinterpret_cast<const float2*>(lds + kGxyWords);
-    c.nz.perm2d = lds + kGradWords;
-    c.nz.so16 = (threadIdx.x & 15u) * 16u;
-    c.nz.so32 = (threadIdx.x & 31u) * 8u;
+    c.nz.img = reinterpret_cast<const char*>(lds);
+    c.nz.oct = reinterpret_cast<const float4*>(lds + kOctBase);
+    c.nz.colt = reinterpret_cast<const float2*>(c.nz.oct + kNpOct);
+    c.nz.so16 = kLdsGxy | ((threadIdx.x & 15u) * 16u);
     c.nz.calls = 0;
     c.k = k;
     c.kf = k;
@@ -102,8 +109,8 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
                                                    RtStats* stats, const FrameTable* __restrict__ ft)
 {
     if (ft) out = ft->cam[blockIdx.y];
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return;
     Ctx c = make_ctx(k, lds);
@@ -135,8 +142,8 @@ __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restr
 {
     constexpr int L = RT_NOMADPLAINS;
     if (ft) out = ft->cam[blockIdx.y];
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k);
     const int i = blockIdx.x * (BS / LPR) + (int)(threadIdx.x / LPR);
     if (i >= RT_CAMERA_RES * RT_CAMERA_RES) return; // whole groups leave together
     Ctx c = make_ctx(k, lds);
@@ -571,8 +578,8 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
     // hits k_trace could not queue on its CU (hit ring full)
     const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
     if (n_hits == 0u) return; // everything was shaded inside k_trace
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
@@ -640,10 +647,10 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 {
     const uint32_t n_long = min(__builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]), long_cap);
     if (n_long == 0u) return; // every long shadow ray was marched inside k_trace
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    __shared__ FrameRays s_fr;
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords + sizeof(FrameRays) / 4];
+    FrameRays& s_fr = *reinterpret_cast<FrameRays*>(lds + kNoiseLdsWords);
     frame_rays_load(s_fr, ft, m.n_frames);
-    load_noise_lds(lds, perm2d, grad);
+    load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds); // c.eye: the lane's ray's frame (set on refill)
@@ -891,9 +898,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
                                                 uint32_t compact_live, uint32_t seg_live)
 {
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    __shared__ FrameRays s_fr;
-    __shared__ TraceQueues q;
+    // one LDS array (the noise image at address 0, then the frame table and the rings)
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords + (sizeof(FrameRays) + sizeof(TraceQueues)) / 4];
+    FrameRays& s_fr = *reinterpret_cast<FrameRays*>(lds + kNoiseLdsWords);
+    TraceQueues& q = *reinterpret_cast<TraceQueues*>(lds + kNoiseLdsWords + sizeof(FrameRays) / 4);
     frame_rays_load(s_fr, ft, m.n_frames);
     if (threadIdx.x == 0) {
         q.lock = 0;
@@ -902,7 +910,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         q.active = 0;
         q.drained = 0;
     }
-    load_noise_lds(lds, perm2d, grad);
+    load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds); // k: frame-invariant constants (per-frame ones: frame_ctx / s_fr)
@@ -1182,8 +1190,8 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0
                                                  const uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                  RtStats* stats)
 {
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k0);
     const uint32_t lane = threadIdx.x & 63u;
     Ctx c0x = make_ctx(k0, lds);
     const uint32_t W = (uint32_t)k0->width, H = (uint32_t)k0->height, aa = (uint32_t)k0->aa_samples;
@@ -1502,8 +1510,8 @@ __global__ void __launch_bounds__(256) k_debug_noise(const RtConsts* __restrict_
                                                      const float4* __restrict__ grad, const float* __restrict__ xyz,
                                                      float* __restrict__ out, int n, int density)
 {
-    __shared__ uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad);
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k);
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     Ctx c = make_ctx(k, lds);

@@ -17,32 +17,30 @@ using rtm::f3;
 using rtm::fma;
 
 // ---------------------------------------------------------------------------
-// Noise lattice view (both tables live in LDS for the kernel's lifetime).
-//   perm2d: texPerm2D texels (R8G8B8A8_UINT), texel (x,y) at x + y*128 (64 KiB).
-//   gxy/gz: CBNoise.permGradients re-laid as PAIRS.  The z+1 corners of noise3d
-//           (noise.hlsl:166-168, Pu + ONE_PIXEL) index gradient (i+1)&127 where the
-//           z corners index i, so entry i holds gradients i and i+1 side by side:
-//             gxy[i] = (g[i].x, g[i+1].x, g[i].y, g[i+1].y)   16 B
-//             gz[i]  = (g[i].z, g[i+1].z)                      8 B
-//           One pair of loads yields both z-layers of a lattice column in register
-//           pairs that v_pk_fma_f32 consumes as they land (no shuffles), and only
-//           the four z-layer indices need extracting.  Entries are lane-private:
-//           entry i for lane slot s at gxy[i*16 + (s&15)] (16 B) and, RT_GZ16, gz at
-//           the same byte offset in the next 32 KiB (8 of the slot's 16 B used), so one
-//           v_perm_b32 addresses both loads (ds_read_b64 ... offset:32768); the b128
-//           loads are conflict-free however random the indices, the b64 loads 2-way.
-//           RT_GZ16=0: gz[i*32 + (s&31)] (8 B slots, conflict-free, own address).
-#ifndef RT_GZ16
-#define RT_GZ16 1
-#endif
+// Noise lattice view: one LDS image for the kernel's lifetime (rt_kernels.hip load_noise_lds):
+//   byte 0      perm2D texels (R8G8B8A8_UINT), texel (x,y) at (x + y*128) * 4 (64 KiB).  At image
+//               offset 0 the texel address is the masked lattice offset itself (no base add).
+//   kLdsGxy     gxy: CBNoise.permGradients re-laid as PAIRS.  The z+1 corners of noise3d
+//               (noise.hlsl:166-168, Pu + ONE_PIXEL) index gradient (i+1)&127 where the z corners
+//               index i, so entry i holds gradients i and i+1 side by side:
+//                 gxy[i] = (g[i].x, g[i+1].x, g[i].y, g[i+1].y)   16 B
+//                 gz[i]  = (g[i].z, g[i+1].z)                      8 B (of a 16-B slot)
+//               One pair of loads yields both z-layers of a lattice column in register pairs that
+//               v_pk_fma_f32 consumes as they land (no shuffles), and only the four z-layer
+//               indices need extracting.  Entries are lane-private: entry i for lane slot s at
+//               kLdsGxy + i*256 + (s&15)*16, so one v_perm_b32 builds the whole address
+//               (base byte from so16, index byte from the texel, slot byte from so16); the b128
+//               loads are conflict-free however random the indices, the b64 loads 2-way.
+//   kLdsGz      gz at the same slot layout (ds_read_b64 ... offset:32768 from the gxy address).
+//   then        the octave tables (oct, colt).
+constexpr uint32_t kLdsGxy = 0x10000u, kLdsGz = 0x18000u;
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 struct NoiseView {
-    const uint32_t* perm2d;
-    const float4* gxy;
-    const float2* gz;
-    uint32_t so16;  // (lane & 15) * 16: this lane's byte slot in a gxy entry row
-    uint32_t so32;  // (lane & 31) * 8:  this lane's byte slot in a gz entry row (RT_GZ16=0)
+    const char* img;    // the LDS image (perm2D texels at its offset 0)
+    const float4* oct;  // nomadplains FBM octave N: (S, 0.35 S, 1/S, 0), N = 0 .. RT_NP_OCTAVES + 2
+    const float2* colt; // colour FBM octave N: (S, 1/S), N = 0 .. RT_COL_OCTAVES + 1
+    uint32_t so16;  // kLdsGxy | (lane & 15) * 16: byte 2 = the gxy plane's base >> 16, byte 0 = the lane's slot
     mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
 };
 
@@ -73,36 +71,25 @@ __device__ __forceinline__ v2f gdot2(const float4& gxy, const float2& gz, float 
     return vfma(v2(gz.x, gz.y), zz, r);
 }
 
-// The lattice part of noise3d once the cell (Px, Py, Pz), the fractions (x, y, z), x - 1,
-// y - 1 and the fades (ux, uy, uz) are known: the perm2D texel, the eight gradient dots,
+// The lattice part of noise3d once the cell is known: the perm2D texel t of (Px, Py), Z = Pz & 127,
+// the fractions (x, y, z), x - 1, y - 1 and the fades (ux, uy, uz): the eight gradient dots and
 // the trilinear lerp.
-__device__ __forceinline__ float noise3d_cell(const NoiseView& nz, int32_t Px, int32_t Py, int32_t Pz, float x, float y,
-                                              float x1, float y1, float z, float ux_, float uy_, float uz)
+__device__ __forceinline__ float noise3d_lattice(const NoiseView& nz, uint32_t t, uint32_t Z, float x, float y,
+                                                 float x1, float y1, float z, float ux_, float uy_, float uz)
 {
-    // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
-    // texel (Px & 127, Py & 127) at byte ((Py & 127) << 9) | ((Px & 127) << 2): the low
-    // term stays below 512, so add-then-mask needs no separate Py mask
-    const uint32_t Z = (uint32_t)Pz & 127u;
-    const uint32_t toff = (((uint32_t)Py << 9) + (((uint32_t)Px << 2) & 0x1fcu)) & 0xfffcu;
-    uint32_t t = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(nz.perm2d) + toff);
     // Pu = texel + Pu.z per channel (bytes <= 127+127: no carry), % 128
     uint32_t w = (t + Z * 0x01010101u) & 0x7f7f7f7fu; // AA, AB, BA, BB column indices at z
     // entry i of either plane starts at byte i*256: one v_perm_b32 per corner builds
-    // (index byte << 8) | lane slot ({w, slot} byte pick: 4+k = byte k of w, 0 = slot, 12 = 0)
-    const char* gb = reinterpret_cast<const char*>(nz.gxy);
-    const char* zb = reinterpret_cast<const char*>(nz.gz);
+    // base | (index byte << 8) | lane slot ({w, so16} byte pick: 4+k = byte k of w, 0 / 2 = bytes
+    // 0 / 2 of so16, 12 = 0); gz is the same address + 32768 (the load's offset field)
     auto gxy_at = [&](uint32_t sel) {
-        return *reinterpret_cast<const float4*>(gb + __builtin_amdgcn_perm(w, nz.so16, sel));
+        return *reinterpret_cast<const float4*>(nz.img + __builtin_amdgcn_perm(w, nz.so16, sel));
     };
     auto gz_at = [&](uint32_t sel) {
-#if RT_GZ16
-        return *reinterpret_cast<const float2*>(zb + __builtin_amdgcn_perm(w, nz.so16, sel));
-#else
-        return *reinterpret_cast<const float2*>(zb + __builtin_amdgcn_perm(w, nz.so32, sel));
-#endif
+        return *reinterpret_cast<const float2*>(nz.img + (kLdsGz - kLdsGxy) + __builtin_amdgcn_perm(w, nz.so16, sel));
     };
-    const float4 a0 = gxy_at(0x0c0c0400u), a1 = gxy_at(0x0c0c0500u), b0 = gxy_at(0x0c0c0600u), b1 = gxy_at(0x0c0c0700u);
-    const float2 za0 = gz_at(0x0c0c0400u), za1 = gz_at(0x0c0c0500u), zb0 = gz_at(0x0c0c0600u), zb1 = gz_at(0x0c0c0700u);
+    const float4 a0 = gxy_at(0x0c020400u), a1 = gxy_at(0x0c020500u), b0 = gxy_at(0x0c020600u), b1 = gxy_at(0x0c020700u);
+    const float2 za0 = gz_at(0x0c020400u), za1 = gz_at(0x0c020500u), zb0 = gz_at(0x0c020600u), zb1 = gz_at(0x0c020700u);
     const v2f zz = v2(z, z + -1.0f);
     v2f g00 = gdot2(a0, za0, x, y, zz);   // (g000, g001)
     v2f g10 = gdot2(b0, zb0, x1, y, zz);  // (g100, g101)
@@ -116,15 +103,77 @@ __device__ __forceinline__ float noise3d_cell(const NoiseView& nz, int32_t Px, i
     return fma(uz, l.y - l.x, l.x);
 }
 
+// The first half of noise3d (noise.hlsl:153-164): the cell of p and its perm2D texel.  Split from
+// the lattice half so an FBM loop can fetch octave N+1's texel while octave N's gradient loads
+// are in flight (noise_fbm below).
+struct NoiseCell {
+    v2f xy;     // fractions x, y
+    float z;    // fraction z
+    uint32_t Z; // Pz & 127
+    uint32_t t; // perm2D texel of (Px & 127, Py & 127)
+};
+
+// FAST: the integer half without v_cvt_i32_f32 and with one shift.  gfx950 issues v_cvt_*,
+// v_floor, shifts, v_perm and the 3-operand integer ops at half the rate of FP32 add / mul / fma
+// and v_and / v_add_u32 (scripts/ubench_issue.hip), so the lattice integers come from the
+// float floor values by the magic-number add: for an integer f with |f| < 2^22, the bits of
+// f + 1.5 * 2^23 hold (2^22 + f) in their low 23 bits, so bits & 127 == f & 127, and those of
+// fma(f, 4, 1.5 * 2^23) hold ((f & 127) << 2) under the mask 0x1fc when |4 f| < 2^22.  The caller
+// guarantees |coordinate| < kFastCellRange = 2^20 (floor keeps it).  Same bits as the general path.
+constexpr float kFastCellRange = 1048576.0f;
+constexpr float kMagic = 12582912.0f; // 1.5 * 2^23
+
+// Byte offset of perm2D texel (floor x & 127, floor y & 127) in the LDS image (see FAST below).
+template <bool FAST>
+__device__ __forceinline__ uint32_t texel_offset(float fx, float fy)
+{
+    if constexpr (FAST) {
+        const uint32_t mx4 = rtm::bits(fma(fx, 4.0f, kMagic)), my = rtm::bits(fy + kMagic);
+        // ((my << 9) | x4) & 0xfffc: one v_lshl_or_b32 (the compiler's lshl + and_or is two
+        // half-rate ops); a pure register op, so the asm needs no wait bookkeeping
+        uint32_t t;
+        asm("v_lshl_or_b32 %0, %1, 9, %2" : "=v"(t) : "v"(my), "v"(mx4 & 0x1fcu));
+        return t & 0xfffcu;
+    } else {
+        // texel (Px & 127, Py & 127) at byte ((Py & 127) << 9) | ((Px & 127) << 2): the low
+        // term stays below 512, so add-then-mask needs no separate Py mask
+        const uint32_t Px = (uint32_t)(int32_t)fx, Py = (uint32_t)(int32_t)fy;
+        return ((Py << 9) + ((Px << 2) & 0x1fcu)) & 0xfffcu;
+    }
+}
+
+// Pz & 127 (the z-layer index)
+template <bool FAST>
+__device__ __forceinline__ uint32_t layer_index(float fz)
+{
+    if constexpr (FAST) return rtm::bits(fz + kMagic) & 127u;
+    else return (uint32_t)(int32_t)fz & 127u;
+}
+
+template <bool FAST = false>
+__device__ __forceinline__ NoiseCell noise3d_cell(const NoiseView& nz, float px, float py, float pz)
+{
+    NoiseCell c;
+    const float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
+    c.xy = v2(px, py) - v2(fx, fy);
+    c.z = pz - fz;
+    // P & 127 == the HLSL negative-safe modulo (noise.hlsl:159-164)
+    c.Z = layer_index<FAST>(fz);
+    c.t = *reinterpret_cast<const uint32_t*>(nz.img + texel_offset<FAST>(fx, fy));
+    return c;
+}
+
+__device__ __forceinline__ float noise3d_finish(const NoiseView& nz, const NoiseCell& c)
+{
+    const v2f uxy = fade2(c.xy);
+    const v2f xy1 = c.xy + v2(-1.0f, -1.0f);
+    return noise3d_lattice(nz, c.t, c.Z, c.xy.x, c.xy.y, xy1.x, xy1.y, c.z, uxy.x, uxy.y, fade(c.z));
+}
+
 // noise.hlsl:153-179 (live `#if 1` block); noise3d_raw does not count the call
 __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, float py, float pz)
 {
-    const float fx = rtm::floor(px), fy = rtm::floor(py), fz = rtm::floor(pz);
-    const v2f xy = v2(px, py) - v2(fx, fy);
-    const float z = pz - fz;
-    const v2f uxy = fade2(xy);
-    const v2f xy1 = xy + v2(-1.0f, -1.0f);
-    return noise3d_cell(nz, (int32_t)fx, (int32_t)fy, (int32_t)fz, xy.x, xy.y, xy1.x, xy1.y, z, uxy.x, uxy.y, fade(z));
+    return noise3d_finish(nz, noise3d_cell(nz, px, py, pz));
 }
 
 // noise3d(px, py, 0) (nomadplains' steep noise, terrain.hlsl:26).  z = 0 makes Pz = 0 and
@@ -133,20 +182,18 @@ __device__ __forceinline__ float noise3d_raw(const NoiseView& nz, float px, floa
 // to the sign of a zero, and add/mul/fma inputs that differ only in zero signs give results
 // that differ only in zero signs: every nonzero value, the result included, is bit-identical to
 // noise3d_raw's.  The caller only forms sat((n - 0.2) * 6), where a zero's sign cannot show.
+template <bool FAST = false>
 __device__ __forceinline__ float noise3d_z0(const NoiseView& nz, float px, float py)
 {
     const float fx = rtm::floor(px), fy = rtm::floor(py);
     const v2f xy = v2(px, py) - v2(fx, fy);
     const v2f uxy = fade2(xy);
     const v2f xy1 = xy + v2(-1.0f, -1.0f);
-    const uint32_t Px = (uint32_t)(int32_t)fx, Py = (uint32_t)(int32_t)fy;
-    const uint32_t toff = ((Py << 9) + ((Px << 2) & 0x1fcu)) & 0xfffcu;
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(nz.perm2d) + toff) & 0x7f7f7f7fu;
-    const char* gb = reinterpret_cast<const char*>(nz.gxy);
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(nz.img + texel_offset<FAST>(fx, fy)) & 0x7f7f7f7fu;
     auto g_at = [&](uint32_t sel) {
-        return *reinterpret_cast<const float4*>(gb + __builtin_amdgcn_perm(w, nz.so16, sel));
+        return *reinterpret_cast<const float4*>(nz.img + __builtin_amdgcn_perm(w, nz.so16, sel));
     };
-    const float4 a0 = g_at(0x0c0c0400u), a1 = g_at(0x0c0c0500u), b0 = g_at(0x0c0c0600u), b1 = g_at(0x0c0c0700u);
+    const float4 a0 = g_at(0x0c020400u), a1 = g_at(0x0c020500u), b0 = g_at(0x0c020600u), b1 = g_at(0x0c020700u);
     const float x = xy.x, y = xy.y, x1 = xy1.x, y1 = xy1.y;
     const float g00 = fma(a0.z, y, a0.x * x), g10 = fma(b0.z, y, b0.x * x1);
     const float g01 = fma(a1.z, y1, a1.x * x), g11 = fma(b1.z, y1, b1.x * x1);
@@ -231,11 +278,24 @@ __device__ __forceinline__ float terraces(float s, float y, float steep)
     return s;
 }
 
+// nomadplains' FBM (terrain.hlsl:16-24): sum over N = 1 .. n_oct of noise3d(q0 * (S, 0.35 S, S)) / S,
+// in octave order (the octave constants come from the LDS image: no scalar loads in the loop).
+template <bool FAST>
+__device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
+{
+    float s = 0.0f;
+    #pragma unroll 1
+    for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
+        if (N > n_oct) break;
+        const float4 oc = c.nz.oct[N];
+        c.nz.calls += 1;
+        s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * oc.x, q0.y * oc.y, q0.z * oc.x)), oc.z, s);
+    }
+    return s;
+}
+
 // Media/nomadplains/shaders/terrain.hlsl:8-39.  The steep noise, noise3d(x, z, 0), is evaluated
-// by noise3d_z0 (RT_STEEP_Z0=0: by noise3d, for A/B runs).
-#ifndef RT_STEEP_Z0
-#define RT_STEEP_Z0 1
-#endif
+// by noise3d_z0.
 __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 {
     float d = -p.y;
@@ -243,20 +303,17 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     float s = 0.0f;
     f3 q0 = rtm::scale(p1, 0.006f);
     const int n_oct = np_octaves(c, p);
-    #pragma unroll 1
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
-        if (N > n_oct) break;
-        float S = c.k->np_scale[N];
-        float n = noise3d(c.nz, q0.x * S, q0.y * c.k->np_scale_y[N], q0.z * S);
-        s = fma(n, c.k->np_rcp[N], s);
-    }
+    // The octave cells take the short integer path (noise3d_cell<true>) when every lattice
+    // coordinate of the wave's noises stays below 2^20 in magnitude: |q0| * S_n < 2^20 for the
+    // lane's last octave n (S grows with N; the steep noise's coordinates are 1.19 |q0| < S_1 |q0|).
+    // Wave-uniform, so the sample runs one of two copies.
+    const float qm = rtm::max(rtm::max(rtm::abs(q0.x), rtm::abs(q0.y)), rtm::abs(q0.z));
+    const bool fast = !__ballot(!(qm * c.nz.oct[n_oct].x < kFastCellRange));
+    s = fast ? np_fbm<true>(c, q0, n_oct) : np_fbm<false>(c, q0, n_oct);
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
-#if RT_STEEP_Z0
     c.nz.calls += 1u;
-    const float sn = noise3d_z0(c.nz, p1.x * 0.007138f, p1.z * 0.007138f);
-#else
-    const float sn = noise3d(c.nz, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f);
-#endif
+    const float sn = fast ? noise3d_z0<true>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f)
+                          : noise3d_z0<false>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f);
     float steep = rtm::sat((sn - 0.2f) * 6.0f) * 7.5f;
     s = terraces(s, p1.y, steep);
     // floor lift: pow(0, 1.5) == 0 exactly, so a wave whose bases are all 0 skips the pow
