@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Generate the committed golden fixtures (run in the build container).
 
-1. noise_reference_glibc_seed300.npz -- the tables produced by the REFERENCE's own
+1. noise_reference_{glibc,msvc}_seed300.npz -- the tables produced by the REFERENCE's own
    gpuraytrace/Graphics/Noise.cpp (Noise::generate(false), seed 300), compiled in place
-   from /root/reference by oracle/Makefile (`make -C oracle ref`) and run here (glibc
-   rand).  Data only: perm2D bytes + gradient floats.
+   from /root/reference by oracle/Makefile (`make -C oracle ref`) and run here: with glibc's
+   rand, and with the MSVC CRT rand/srand interposed (oracle/msvc_rand.cpp; the tables the
+   reference builds on Windows).  Data only: perm2D bytes + gradient floats.
 2. scene_constants.npz -- frame constants (matrices as the shader sees them) of the
    fixed benchmark scene, so kernel parity never depends on the camera maths.
 3. oracle_frames.npz -- small frames rendered by the C oracle (oracle/rt_oracle.c):
@@ -38,6 +39,9 @@ FRAMES = [  # (landscape, pose, W, H, aa, max_steps[, ao_samples])
     ("nomadplains", "reset", 64, 48, 1, 0, 1),
     ("nomadplains", "lookdown", 48, 32, 1, 512, 4),
     ("greenrocks", "reset", 48, 32, 2, 0, 2),
+    # AA_SAMPLES 8 and 16 (antialiasing.hlsl, D3D11 standard sample patterns)
+    ("nomadplains", "reset", 32, 24, 8, 0),
+    ("nomadplains", "lookdown", 24, 16, 16, 0, 1),
 ]
 
 
@@ -55,16 +59,15 @@ def consts_for(w, h, pose):
 
 
 def main():
-    ref_bin = os.path.join(ROOT, "oracle", "_ref", "ref_noise_dump")
-    if not os.path.exists(ref_bin):
-        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
-    raw = subprocess.run([ref_bin], capture_output=True, check=True).stdout
-    np.savez_compressed(os.path.join(HERE, "noise_reference_glibc_seed300.npz"),
-                        perm2d=np.frombuffer(raw[:65536], np.uint8), grad=np.frombuffer(raw[65536:], np.float32))
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    for crt, exe in (("glibc", "ref_noise_dump"), ("msvc", "ref_noise_dump_msvc")):
+        raw = subprocess.run([os.path.join(ROOT, "oracle", "_ref", exe)], capture_output=True, check=True).stdout
+        np.savez_compressed(os.path.join(HERE, f"noise_reference_{crt}_seed300.npz"),
+                            perm2d=np.frombuffer(raw[:65536], np.uint8), grad=np.frombuffer(raw[65536:], np.float32))
 
     sc = {}
     for pose in POSES:
-        for (w, h) in ((64, 48), (48, 32), (256, 256), (1920, 1080)):
+        for (w, h) in ((64, 48), (48, 32), (32, 24), (24, 16), (256, 256), (1920, 1080)):
             c = consts_for(w, h, pose)
             for k in ("eye", "view_inverse", "projection", "sun"):
                 sc[f"{pose}_{w}x{h}_{k}"] = np.asarray(c[k], np.float32)

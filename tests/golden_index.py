@@ -20,6 +20,9 @@ FRAMES = [  # (landscape, pose, W, H, aa, max_steps[, ao_samples]) -- keep in sy
     ("nomadplains", "reset", 64, 48, 1, 0, 1),
     ("nomadplains", "lookdown", 48, 32, 1, 512, 4),
     ("greenrocks", "reset", 48, 32, 2, 0, 2),
+    # AA_SAMPLES 8 and 16 (antialiasing.hlsl, D3D11 standard sample patterns)
+    ("nomadplains", "reset", 32, 24, 8, 0),
+    ("nomadplains", "lookdown", 24, 16, 16, 0, 1),
 ]
 
 _cache = {}

@@ -525,9 +525,9 @@ def test_batch_mixed_cameras_bitexact(n):
         d.destroy()
 
 
-@pytest.mark.parametrize("idx", [2, 3, 4, 6, 7, 8, 9, 10], ids=lambda i: GI.frame_key(*GI.FRAMES[i]))
+@pytest.mark.parametrize("idx", [2, 3, 4, 6, 7, 8, 9, 10, 11, 12], ids=lambda i: GI.frame_key(*GI.FRAMES[i]))
 def test_batch_every_landscape_and_macro_set(idx):
-    """Three frames of one spec per batch: AA 4, step cap, the other landscapes (greenrocks'
+    """Three frames of one spec per batch: AA 4/8/16, step cap, the other landscapes (greenrocks'
     fog), AO 1/2/4."""
     from gpgpuraytrace_amd import engine as E
     specs = [GI.FRAMES[idx]] * 3

@@ -51,6 +51,19 @@ def test_product_noise_generator_matches_oracle(kind, seed):
     assert np.array_equal(n.permutations1D, np.frombuffer(bytes(o.grad), np.float32))
 
 
+@pytest.mark.parametrize("crt,kind", [("msvc", 0), ("glibc", 1)])
+def test_product_noise_generator_matches_reference_build(crt, kind):
+    """The product's table generator (rt_noise.cpp) against the reference's own Noise.cpp built
+    here with each CRT's rand (tests/golden/noise_reference_<crt>_seed300.npz, make_golden.py)."""
+    import gpgpuraytrace_amd as G
+    ref = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                               f"noise_reference_{crt}_seed300.npz"))
+    n = G.Noise()
+    n.generate(seed=300, rand_kind=kind)
+    assert np.array_equal(n.permutations2D, ref["perm2d"])
+    assert np.array_equal(n.permutations1D, ref["grad"])
+
+
 @pytest.mark.parametrize("seed", [0, 7])
 def test_product_host_set_target_depths_matches_oracle(seed):
     import gpgpuraytrace_amd as G

@@ -32,18 +32,29 @@ def test_noise_tables_match_reference_build():
     assert np.array_equal(g, ref["grad"])
 
 
-def test_noise_tables_reference_binary_if_present():
-    exe = os.path.join(O.ORACLE_DIR, "_ref", "ref_noise_dump")
+def test_noise_tables_match_reference_build_msvc():
+    """MSVC CRT rand (the reference's platform): bit-identical to the reference's own Noise.cpp
+    built here with the MSVC rand/srand interposed (oracle/msvc_rand.cpp;
+    tests/golden/noise_reference_msvc_seed300.npz, made by oracle/_ref/ref_noise_dump_msvc)."""
+    ref = np.load(os.path.join(GOLDEN, "noise_reference_msvc_seed300.npz"))
+    p2, g = tables(O.noise_tables(300, O.RAND_MSVC))
+    assert np.array_equal(p2, ref["perm2d"])
+    assert np.array_equal(g, ref["grad"])
+
+
+@pytest.mark.parametrize("exe,kind", [("ref_noise_dump", O.RAND_GLIBC), ("ref_noise_dump_msvc", O.RAND_MSVC)])
+def test_noise_tables_reference_binary_if_present(exe, kind):
+    exe = os.path.join(O.ORACLE_DIR, "_ref", exe)
     if not os.path.exists(exe):
         pytest.skip("oracle/_ref not built (no /root/reference here)")
     import subprocess
     raw = subprocess.run([exe], capture_output=True, check=True).stdout
-    p2, g = tables(O.noise_tables(300, O.RAND_GLIBC))
+    p2, g = tables(O.noise_tables(300, kind))
     assert raw[:65536] == p2.tobytes() and raw[65536:] == g.tobytes()
 
 
 def test_noise_tables_msvc_golden():
-    """MSVC CRT rand (the reference's platform): SURVEY.md §8c measured values."""
+    """MSVC CRT rand: SURVEY.md §8c measured values."""
     p2, g = tables(O.noise_tables(300, O.RAND_MSVC))
     assert list(p2[:8]) == [25, 53, 121, 90, 121, 90, 7, 19]
     assert fnv1a32(p2) == 0x6067CD85
