@@ -2,6 +2,7 @@
 golden fixtures.  Bar: bit-exact float32 colours and UNORM8 pixels, identical
 step / noise3d counts.  Run on the GPU box with `pytest -m gpu`."""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -216,6 +217,44 @@ def test_frame_bitexact_reference_call_sequence(spec):
     assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])
     assert np.array_equal(ter.camera_view, gold[key + "_camera_results"])
     dev.destroy()
+
+
+DRIVER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_build",
+                      "terrain_driver")
+
+
+@pytest.mark.parametrize("mode", ["ref", "device"])
+@pytest.mark.parametrize("spec", [GI.FRAMES[0], GI.FRAMES[1], GI.FRAMES[4], GI.FRAMES[9]],
+                         ids=["np_reset", "np_down", "testing", "np_down_ms512_ao4"])
+def test_cpp_adapter_terrain_sequence(spec, mode, tmp_path):
+    """The C++ adapter (integration/hip_adapter.cpp: DeviceHIP, ComputeHIP, ShaderVariableHIP,
+    ShaderArrayHIP, TextureHIP) driven through the reference's own interfaces by
+    integration/terrain_driver.cpp, which replays Terrain::create / reload / updateShaders /
+    render (Terrain.cpp:55-206: run(2,2,1) -> CameraResults map/unmap -> setTargetDepths ->
+    CellDistance write -> per tile ThreadOffset write + run + flush -> present) or the one-call
+    device path; the RGBA8 readback and CameraResults equal the golden frame's."""
+    assert os.path.exists(DRIVER), "integration/_build/terrain_driver not built (make -C integration, needs " \
+                                   "the reference headers: __graft_entry__.build() in the build container)"
+    import subprocess
+    gold = GI.load()
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    key = GI.frame_key(*spec)
+    c = GI.consts(w, h, pose)
+    cin, cout = tmp_path / "consts.bin", tmp_path / "out.bin"
+    with open(cin, "wb") as f:  # the cbuffer bytes Terrain writes (XMMatrixTranspose of the matrices)
+        f.write(np.array([w, h], np.int32).tobytes())
+        f.write(np.ascontiguousarray(np.asarray(c["view_inverse"], np.float32).T).tobytes())
+        f.write(np.asarray(c["eye"], np.float32).tobytes())
+        f.write(np.ascontiguousarray(np.asarray(c["projection"], np.float32).T).tobytes())
+        f.write(np.asarray(c["sun"], np.float32).tobytes())
+    r = subprocess.run([DRIVER, str(cin), str(cout), land, str(aa), str(ms), str(ao), mode],
+                       capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    raw = np.fromfile(cout, np.uint8)
+    img8 = raw[:w * h * 4].reshape(h, w, 4)
+    cam = raw[w * h * 4:].view(np.float32).reshape(1024, 4)
+    assert np.array_equal(img8, gold[key + "_rgba8"])
+    assert np.array_equal(cam, gold[key + "_camera_results"])
 
 
 def test_tiled_dispatch_1280x720_rows():
