@@ -205,7 +205,7 @@ def main():
         """Instrumented frames (untimed): noise3d of each shard this rank traces in a batch, the
         whole frame's hits and rays, and (keep_frame) the whole frame's pixels."""
         sdev, ster = make(stats=True, max_steps=max_steps, ao=ao, float_output=keep_frame)
-        per_shard, whole, img = {}, None, None
+        per_shard, waves, whole, img = {}, {}, None, None
         for s in sorted({P.frame_shard(rank, f, world) for f in range(B)} | {0}):
             ster.update_shaders()
             ster.camera_compute.run(2, 2, 1)
@@ -213,6 +213,7 @@ def main():
             ster.render_device(s, world)
             st = sdev.stats(reset=True)
             per_shard[s] = st["noise_calls"] - pre["noise_calls"]
+            waves[s] = st["noise_wave_iters"] - pre["noise_wave_iters"]
             if world == 1:
                 whole = st
         if world > 1:
@@ -223,7 +224,9 @@ def main():
         sdev.destroy()
         batch_noise = sum(per_shard[P.frame_shard(rank, f, world)] for f in range(B))
         hits = whole["hits"]
-        return {"batch_noise": batch_noise, "shard_noise": per_shard[P.frame_shard(rank, 0, world)], "hits": hits,
+        s0 = P.frame_shard(rank, 0, world)
+        return {"batch_noise": batch_noise, "shard_noise": per_shard[s0], "hits": hits,
+                "noise_lane_util": per_shard[s0] / (64.0 * waves[s0]) if waves[s0] else None,
                 "rays": W * H + hits + hits * ao + 1024, "img": img}
 
     want_cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
@@ -416,6 +419,8 @@ def main():
                 "primary_plus_shadow_mrays": round((W * H + hits + 1024) * a.steps / elapsed / 1e6, 3),
                 "hit_fraction": round(hits / (W * H), 4),
                 "noise3d_per_frame_tracescreen": counts["shard_noise"] if world == 1 else None,
+                # noise3d lane-calls / (64 x wave iterations of them): SIMD lane utilisation of the noise work
+                "noise_lane_utilisation": round(counts["noise_lane_util"], 4) if counts["noise_lane_util"] else None,
                 "parallelism": "single GPU" if world == 1 else (
                     f"tile-cyclic 32x32 shards x{world} (rotated per frame) + RCCL gather per batch"
                     + (" + prepass split over ranks (RCCL all-gather of CameraResults)" if plan.split_prepass

@@ -27,7 +27,7 @@ RT_FORMAT_R8G8B8A8_UINT = 3
 class RtStats(C.Structure):
     _fields_ = [("primary_steps", C.c_ulonglong), ("shadow_steps", C.c_ulonglong),
                 ("prepass_steps", C.c_ulonglong), ("hits", C.c_ulonglong), ("noise_calls", C.c_ulonglong),
-                ("ao_steps", C.c_ulonglong)]
+                ("ao_steps", C.c_ulonglong), ("noise_wave_iters", C.c_ulonglong)]
 
 
 class NativeError(RuntimeError):

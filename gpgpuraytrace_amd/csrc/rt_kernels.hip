@@ -85,6 +85,13 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     return c;
 }
 
+// STATS kernels: a lane's noise count (NoiseView::calls) into the frame statistics
+__device__ __forceinline__ void stats_noise(RtStats* stats, uint64_t calls)
+{
+    atomicAdd(&stats->noise_calls, (unsigned long long)(calls & 0xffffffffull));
+    if (calls >> 32) atomicAdd(&stats->noise_waves, (unsigned long long)(calls >> 32));
+}
+
 __device__ __forceinline__ float uniform_f(float x)
 {
     return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
@@ -126,7 +133,7 @@ __global__ void __launch_bounds__(64) k_camerarays(const RtConsts* __restrict__ 
     out[i] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
     if constexpr (STATS) {
         atomicAdd(&stats->prepass_steps, (unsigned long long)rr.steps);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+        stats_noise(stats, c.nz.calls);
     }
 }
 
@@ -629,7 +636,7 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
     }
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+        stats_noise(stats, c.nz.calls);
     }
 }
 
@@ -713,7 +720,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     if constexpr (STATS) {
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
         atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+        stats_noise(stats, c.nz.calls);
     }
 }
 
@@ -860,7 +867,7 @@ template <bool SKIPREFINE>
 __device__ __forceinline__ void seg_finish(const Ctx& c, March<RT_NOMADPLAINS, true>& st, bool live, float enddist,
                                            int max_steps, uint32_t lane)
 {
-    const uint32_t calls0 = c.nz.calls;
+    const uint64_t calls0 = c.nz.calls;
     uint32_t own = 0; // noise3d of this lane's own ray (STATS)
     __builtin_amdgcn_s_setprio(3);
     for (;;) {
@@ -1174,7 +1181,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
         atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
         atomicAdd(&stats->hits, (unsigned long long)nhits);
-        atomicAdd(&stats->noise_calls, (unsigned long long)c.nz.calls);
+        stats_noise(stats, c.nz.calls);
     }
 }
 
@@ -1246,7 +1253,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0
         if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
         c0x.nz.calls = c.nz.calls;
     }
-    if constexpr (STATS) atomicAdd(&stats->noise_calls, (unsigned long long)c0x.nz.calls);
+    if constexpr (STATS) stats_noise(stats, c0x.nz.calls);
 }
 
 // Tile-cyclic shard transport: one 256-thread block per 32x32 tile.

@@ -706,6 +706,7 @@ int rt_device_stats(rt_device d, rt_stats* out, int reset)
     out->hits = h.hits;
     out->noise_calls = h.noise_calls;
     out->ao_steps = h.ao_steps;
+    out->noise_wave_iters = h.noise_waves;
     if (reset) HIP_TRY(hipMemsetAsync(d->stats, 0, sizeof(RtStats), d->stream));
     return RT_OK;
 }

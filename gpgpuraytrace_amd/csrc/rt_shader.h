@@ -41,8 +41,17 @@ struct NoiseView {
     const float4* oct;  // nomadplains FBM octave N: (S, 0.35 S, 1/S, 0), N = 0 .. RT_NP_OCTAVES + 2
     const float2* colt; // colour FBM octave N: (S, 1/S), N = 0 .. RT_COL_OCTAVES + 1
     uint32_t so16;  // kLdsGxy | (lane & 15) * 16: byte 2 = the gxy plane's base >> 16, byte 0 = the lane's slot
-    mutable uint32_t calls; // noise3d evaluations (read only by the STATS kernels; dead otherwise)
+    // noise3d evaluations, read only by the STATS kernels (dead otherwise): low word = this lane's
+    // calls, high word = wave iterations (the wave's first active lane adds 1 << 32 per call), so
+    // calls / (64 * iterations) is the SIMD lane utilisation of the noise work
+    mutable uint64_t calls;
 };
+
+__device__ __forceinline__ void count_noise(const NoiseView& nz)
+{
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    nz.calls += 1ull + ((uint64_t)(__lane_id() == (uint32_t)__builtin_ctzll(ex)) << 32);
+}
 
 __device__ __forceinline__ v2f v2(float a, float b)
 {
@@ -203,7 +212,7 @@ __device__ __forceinline__ float noise3d_z0(const NoiseView& nz, float px, float
 
 __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py, float pz)
 {
-    nz.calls += 1;
+    count_noise(nz);
     return noise3d_raw(nz, px, py, pz);
 }
 
@@ -288,7 +297,7 @@ __device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
     for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
         if (N > n_oct) break;
         const float4 oc = c.nz.oct[N];
-        c.nz.calls += 1;
+        count_noise(c.nz);
         s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * oc.x, q0.y * oc.y, q0.z * oc.x)), oc.z, s);
     }
     return s;
@@ -311,7 +320,7 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     const bool fast = !__ballot(!(qm * c.nz.oct[n_oct].x < kFastCellRange));
     s = fast ? np_fbm<true>(c, q0, n_oct) : np_fbm<false>(c, q0, n_oct);
     s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
-    c.nz.calls += 1u;
+    count_noise(c.nz);
     const float sn = fast ? noise3d_z0<true>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f)
                           : noise3d_z0<false>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f);
     float steep = rtm::sat((sn - 0.2f) * 6.0f) * 7.5f;
@@ -538,6 +547,7 @@ __device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, 
     m.f = {0.0f, 0.0f, 0.0f, 0.0f};
     m.d = 0.0f;
     float dirLength = rtm::length(dir);
+    // tracing.hlsl:54, the one R2 exception: the subtrahend's product is fused
     m.step = fma(-dist, k->one_minus_step_factor, (0.03f * stepmod) * dirLength);
     m.lastStep = m.step;
     float il = rtm::rcp(dirLength);

@@ -57,4 +57,5 @@ struct RtStats {
     unsigned long long hits;
     unsigned long long noise_calls;
     unsigned long long ao_steps;
+    unsigned long long noise_waves; // wave iterations of the noise3d evaluations (not the prepass's)
 };

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 enum {
     RT_OK = 0,
@@ -75,6 +75,9 @@ typedef struct {
     unsigned long long hits;          /* primary hits == shadow rays */
     unsigned long long noise_calls;   /* noise3d evaluations (BASELINE.md algorithmic work unit) */
     unsigned long long ao_steps;      /* traceRay iterations, AO rays (build extension RT_AO_SAMPLES) */
+    unsigned long long noise_wave_iters; /* wave64 iterations of the noise3d evaluations outside the prepass
+                                          * (noise_calls / (64 * this) = SIMD lane utilisation of the
+                                          * noise work; ABI 2) */
 } rt_stats;
 
 /* ---- diagnostics ---- */

@@ -11,7 +11,12 @@
  *  R1  every arithmetic operator is one IEEE binary32 round-to-nearest-even op;
  *  R2  a product that feeds an add/sub in the dataflow (a*b+c, c-a*b, and HLSL
  *      lerp / mad) is ONE fused multiply-add (fxc emits `mad`); where two
- *      products feed one add, the left one is fused;
+ *      products feed one add, the left one is fused.  One site departs from
+ *      that default and is fixed here as written: tracing.hlsl:54
+ *      `RAY_STEP*stepmod*dirLength - dist*(1-RAY_STEP_FACTOR)` fuses the
+ *      subtrahend's product, fma(-dist, 1-F, (0.03*stepmod)*dirLength) (the
+ *      minuend is itself a two-multiply chain, so it is the one kept rounded;
+ *      trace_ray below, rt_shader.h march_begin);
  *  R3  a / b = a * rcp(b), rcp = correctly rounded 1/b (fxc/D3D `div`);
  *  R4  dot(a,b) = fma(a.z,b.z, fma(a.y,b.y, a.x*b.x)); length = sqrt(dot(v,v));
  *      normalize(v) = v * rcp(sqrt(dot(v,v))); mul(v,M) = dp4 fma chain;
@@ -461,6 +466,7 @@ static ray_result trace_ray(ctx* c, f3 p, float dist, float enddist, float stepm
     float d = 0.0f;
     float total = 0.0f;
     float dirLength = len3(dir);
+    /* tracing.hlsl:54: the R2 exception (the subtrahend's product is the fused one) */
     float step = fmaf(-dist, c->one_minus_step_factor, (0.03f * stepmod) * dirLength);
     float lastStep = step;
     float il = rcp(dirLength);

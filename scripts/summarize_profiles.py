@@ -47,7 +47,7 @@ def main(src, dst):
     shutil.copy(ks[0], os.path.join(dst, "kernel_stats.csv"))
     bench = open(os.path.join(src, "kt_bench.json")).read().strip().splitlines()[-1]
     with open(os.path.join(dst, "kernels.md"), "w") as f:
-        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline`\n\n"
+        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 24 --warmup 2 --no-cpu-baseline --no-companions`\n\n"
                 "All launches of the run.  The timed loop keeps several batches of frames in flight, so those\n"
                 "launches share the GPU and each one spans longer than it would alone; the per-launch cost the\n"
                 "roofline uses is the bench's one-batch-in-flight pass, tabulated at the end from the same trace.\n"
