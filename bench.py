@@ -201,33 +201,49 @@ def main():
         ter.set_time_of_day(0.3)
         return dev, ter
 
-    def frame_counts(max_steps, ao, keep_frame=False):
-        """Instrumented frames (untimed): noise3d of each shard this rank traces in a batch, the
-        whole frame's hits and rays, and (keep_frame) the whole frame's pixels."""
+    def frame_counts(max_steps, ao, keep_frame=False, batch_stats=True):
+        """Instrumented frames (untimed): (1) one batch of B frames exactly as the timed loop traces
+        it on this rank (rt_terrain_render_batch, rotated shards): its tracescreen noise3d and the
+        wave iterations of that noise (SIMD lane utilisation); (2) one whole frame: hits, rays,
+        noise per frame and (keep_frame) its pixels."""
+        out = {"batch_noise": None, "noise_lane_util": None}
+        if batch_stats:
+            devs, ters = [], []
+            for _ in range(B):
+                d, t = make(stats=True, max_steps=max_steps, ao=ao)
+                devs.append(d)
+                ters.append(t)
+
+            def total():
+                st = [d.stats(reset=True) for d in devs]
+                return sum(x["noise_calls"] for x in st), sum(x["noise_wave_iters"] for x in st)
+
+            for t in ters:
+                t.update_shaders()
+                t.camera_compute.run(2, 2, 1)
+            pc, pw = total()  # the prepass alone; render_batch runs it again
+            if B > 1:
+                E.render_batch(ters, rank if world > 1 else 0, world)
+            else:
+                ters[0].render_device(rank if world > 1 else 0, world)
+            for d in devs:
+                d.synchronize()
+            c, w = total()
+            out["batch_noise"], out["noise_lane_util"] = c - pc, (c - pc) / (64.0 * (w - pw)) if w > pw else None
+            for d in devs:
+                d.destroy()
         sdev, ster = make(stats=True, max_steps=max_steps, ao=ao, float_output=keep_frame)
-        per_shard, waves, whole, img = {}, {}, None, None
-        for s in sorted({P.frame_shard(rank, f, world) for f in range(B)} | {0}):
-            ster.update_shaders()
-            ster.camera_compute.run(2, 2, 1)
-            pre = sdev.stats(reset=True)
-            ster.render_device(s, world)
-            st = sdev.stats(reset=True)
-            per_shard[s] = st["noise_calls"] - pre["noise_calls"]
-            waves[s] = st["noise_wave_iters"] - pre["noise_wave_iters"]
-            if world == 1:
-                whole = st
-        if world > 1:
-            ster.render_device(0, 1)
-            whole = sdev.stats(reset=True)
-        if keep_frame:
-            img = (sdev.readback_float(), sdev.readback())
+        ster.update_shaders()
+        ster.camera_compute.run(2, 2, 1)
+        pre = sdev.stats(reset=True)
+        ster.render_device(0, 1)
+        whole = sdev.stats(reset=True)
+        img = (sdev.readback_float(), sdev.readback()) if keep_frame else None
         sdev.destroy()
-        batch_noise = sum(per_shard[P.frame_shard(rank, f, world)] for f in range(B))
         hits = whole["hits"]
-        s0 = P.frame_shard(rank, 0, world)
-        return {"batch_noise": batch_noise, "shard_noise": per_shard[s0], "hits": hits,
-                "noise_lane_util": per_shard[s0] / (64.0 * waves[s0]) if waves[s0] else None,
-                "rays": W * H + hits + hits * ao + 1024, "img": img}
+        out.update({"frame_noise": whole["noise_calls"] - pre["noise_calls"], "hits": hits,
+                    "rays": W * H + hits + hits * ao + 1024, "img": img})
+        return out
 
     want_cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
     counts = frame_counts(a.max_steps, a.ao, keep_frame=want_cpu)
@@ -363,7 +379,7 @@ def main():
     ring.destroy()
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
-        rc = frame_counts(0, 0)
+        rc = frame_counts(0, 0, batch_stats=False)
         rring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=0, ao_samples=0, batch=B)
         for _ in range(rring.depth + 1):
@@ -418,8 +434,9 @@ def main():
                 "shadow_rays": hits, "ao_rays": hits * a.ao, "prepass_rays": 1024,
                 "primary_plus_shadow_mrays": round((W * H + hits + 1024) * a.steps / elapsed / 1e6, 3),
                 "hit_fraction": round(hits / (W * H), 4),
-                "noise3d_per_frame_tracescreen": counts["shard_noise"] if world == 1 else None,
-                # noise3d lane-calls / (64 x wave iterations of them): SIMD lane utilisation of the noise work
+                "noise3d_per_frame_tracescreen": counts["frame_noise"],
+                # the timed batch's noise3d lane-calls / (64 x their wave iterations): SIMD lane
+                # utilisation of the noise work
                 "noise_lane_utilisation": round(counts["noise_lane_util"], 4) if counts["noise_lane_util"] else None,
                 "parallelism": "single GPU" if world == 1 else (
                     f"tile-cyclic 32x32 shards x{world} (rotated per frame) + RCCL gather per batch"

@@ -78,6 +78,7 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     c.nz.colt = reinterpret_cast<const float2*>(c.nz.oct + kNpOct);
     c.nz.so16 = kLdsGxy | ((threadIdx.x & 15u) * 16u);
     c.nz.calls = 0;
+    c.nz.phase = RT_PHASE_OTHER;
     c.k = k;
     c.kf = k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
@@ -392,6 +393,26 @@ __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, flo
                      cb.z * fma(b, k->one_minus_shadow[2], k->shadow_color[2]));
     col = rtm::mk(rtm::lerp(col.x, fog.x, fog.w), rtm::lerp(col.y, fog.y, fog.w), rtm::lerp(col.z, fog.z, fog.w));
     col = rtm::mk(rtm::lerp(col.x, ray.x, ray.w), rtm::lerp(col.y, ray.y, ray.w), rtm::lerp(col.z, ray.z, ray.w));
+    return make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 1.0f); // w = 1: a hit (AO applies)
+}
+
+// tracescreen.hlsl:22-27,36-38: the colour of a MISS sample (sky: Rayleigh/Mie + space noise, then the
+// fog and sky-amount blends), saturated; w = 0 (no AO).  Computed where the primary march ends, so
+// misses leave no RayResult behind.
+__device__ __forceinline__ float4 miss_sample(const Ctx& c, float px, float py, float dist, f4 fog)
+{
+    f3 p, dir;
+    get_pixel_ray(c, px, py, &p, &dir);
+    f3 pdn = rtm::normalize(dir);
+    float skyAmount = dist * 0.0005f;
+    skyAmount = rtm::sat(skyAmount * skyAmount);
+    SkyColor scat = get_rayleigh_mie(c, pdn);
+    float space = get_space_color(c, pdn);
+    f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
+                     (scat.mie.z + scat.rayleigh.z) + space);
+    f3 col = rtm::mk(rtm::lerp(sky.x, fog.x, fog.w), rtm::lerp(sky.y, fog.y, fog.w), rtm::lerp(sky.z, fog.z, fog.w));
+    col = rtm::mk(rtm::lerp(col.x, sky.x, skyAmount), rtm::lerp(col.y, sky.y, skyAmount),
+                  rtm::lerp(col.z, sky.z, skyAmount));
     return make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
 }
 
@@ -958,6 +979,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         bool live = false;
         uint32_t t = 0, type = RT_LONG_SHADOW;
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
+        cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
             if (live && !march_live<L, true, true>(cl, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
                 long_finish<L, true>(k, fin, samples, aocc, t, type, st);
@@ -1008,6 +1030,14 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                     continue;
                 }
             }
+#ifdef RT_COUNT_LONG_STEPS // diagnostic build: live lanes per long-ray march step (scripts/phase_util.py);
+                             // 2: only while the unit queue is drained, 3: only before
+            if (live && (RT_COUNT_LONG_STEPS == 1 || (RT_COUNT_LONG_STEPS == 2) == (vload(q.drained) != 0u))) {
+                cl.nz.phase = RT_COUNT_PHASE;
+                count_noise(cl.nz);
+                cl.nz.phase = RT_PHASE_LONG;
+            }
+#endif
             if (live) march_step<L, true, true>(cl, st);
         }
     };
@@ -1026,7 +1056,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         const bool valid = lane < take;
         ShadeHit h;
         per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
-            const Ctx cf = frame_ctx(c, ft, f);
+            Ctx cf = frame_ctx(c, ft, f);
+            cf.nz.phase = RT_PHASE_SHADE;
             h = shade_hit<L, true>(cf, m, res, t, t - f * m.frame_samples, st);
             c.nz.calls = cf.nz.calls;
             more = h.more;
@@ -1053,7 +1084,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
 
     // ---- one 8x8 primary unit ----
     auto do_unit = [&](uint32_t f, uint32_t u) {
-        const Ctx cf = frame_ctx(c, ft, f);
+        Ctx cf = frame_ctx(c, ft, f);
+        cf.nz.phase = RT_PHASE_PRIMARY;
         uint32_t px, py;
         const bool valid = unit_pixel(m, f, u, lane, W, H, &px, &py);
         const float pxf = (float)px, pyf = (float)py;
@@ -1092,11 +1124,11 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             __builtin_amdgcn_s_setprio(0);
             const bool hit = valid && st.d > 0.0f;
             WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
-            WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
             if (valid) {
                 RayResult rr = march_result(st);
-                store_ray(res, t, rr);
                 if constexpr (STATS) psteps += rr.steps;
+                if (hit) store_ray(res, t, rr); // the shading input
+                else samples[t] = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
             }
             const uint64_t hb = __ballot(hit);
             if (hb) {
@@ -1185,60 +1217,31 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     }
 }
 
-// tracescreen.hlsl:22-27,36-38 (miss branch) for the misses, then :67-75: the sum of
-// saturated samples in AA order, / AA, UNORM8 store.  Persistent over 8x8 units,
-// strided statically (wave w takes units w, w + n_waves, ...): the per-unit work is
-// so short that a shared queue atomic would serialise the whole pass.
-template <bool STATS>
-__global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0, const FrameTable* __restrict__ ft,
-                                                 const uint32_t* __restrict__ perm2d,
-                                                 const float4* __restrict__ grad, UnitMap m,
-                                                 const float4* __restrict__ res, const float4* __restrict__ samples,
-                                                 const uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
-                                                 RtStats* stats)
+// tracescreen.hlsl:67-75: the sum of the saturated samples in AA order (misses were coloured by
+// k_trace, hits by the shading / long-ray paths; w marks a hit, whose AO factor applies), / AA,
+// UNORM8 store.  Persistent over 8x8 units, strided statically (wave w takes units w, w + n_waves,
+// ...): the per-unit work is so short that a shared queue atomic would serialise the pass.
+__global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
+                                                 UnitMap m, const float4* __restrict__ samples,
+                                                 const uint32_t* __restrict__ aocc)
 {
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad, k0);
     const uint32_t lane = threadIdx.x & 63u;
-    Ctx c0x = make_ctx(k0, lds);
-    const uint32_t W = (uint32_t)k0->width, H = (uint32_t)k0->height, aa = (uint32_t)k0->aa_samples;
+    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
     const uint32_t total = m.n_units * m.n_frames;
     for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < total; g += n_waves) {
         const uint32_t f = __builtin_amdgcn_readfirstlane(g / m.n_units), u = g - f * m.n_units;
-        const Ctx c = frame_ctx(c0x, ft, f);
-        const RtConsts* k = c.k; // frame-invariant
         uint32_t* out8 = ft->out8[f];
         float4* out32 = ft->out32[f];
         uint32_t px, py;
         if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
-            uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
-            float4 dn = res[3u * t + 2u];
-            float4 v;
-            if (dn.x > 0.0f) {
-                v = samples[t];
-                if (k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
-                    const float ao = ao_factor(aocc[t], k->ao_samples);
-                    v = make_float4(v.x * ao, v.y * ao, v.z * ao, v.w);
-                }
-            } else {
-                float4 pdw = res[3u * t + 0u], fog = res[3u * t + 1u];
-                f3 p, dir;
-                get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
-                f3 pdn = rtm::normalize(dir);
-                float skyAmount = pdw.w * 0.0005f;
-                skyAmount = rtm::sat(skyAmount * skyAmount);
-                SkyColor scat = get_rayleigh_mie(c, pdn);
-                float space = get_space_color(c, pdn);
-                f3 sky = rtm::mk((scat.mie.x + scat.rayleigh.x) + space, (scat.mie.y + scat.rayleigh.y) + space,
-                                 (scat.mie.z + scat.rayleigh.z) + space);
-                f3 col = rtm::mk(rtm::lerp(sky.x, fog.x, fog.w), rtm::lerp(sky.y, fog.y, fog.w),
-                                 rtm::lerp(sky.z, fog.z, fog.w));
-                col = rtm::mk(rtm::lerp(col.x, sky.x, skyAmount), rtm::lerp(col.y, sky.y, skyAmount),
-                              rtm::lerp(col.z, sky.z, skyAmount));
-                v = make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
+            const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
+            float4 v = samples[t];
+            if (v.w > 0.0f && k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
+                const float ao = ao_factor(aocc[t], k->ao_samples);
+                v = make_float4(v.x * ao, v.y * ao, v.z * ao, v.w);
             }
             c0 = c0 + v.x;
             c1 = c1 + v.y;
@@ -1251,9 +1254,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k0
         size_t o = (size_t)py * (size_t)k->width + px;
         out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
         if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
-        c0x.nz.calls = c.nz.calls;
     }
-    if constexpr (STATS) stats_noise(stats, c0x.nz.calls);
 }
 
 // Tile-cyclic shard transport: one 256-thread block per 32x32 tile.
@@ -1368,6 +1369,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
+    // k_finish holds no LDS: up to 2 blocks per CU
+    uint32_t fblocks = need < 2u * blocks ? need : 2u * blocks;
     dim3 blk(1024);
     // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
     // (single frames only: batches have units enough, and a segment's lanes share one eye);
@@ -1394,8 +1397,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
                            a.fin, a.samples, a.aocc, a.long_cap, a.queue, a.stats);
-        hipLaunchKernelGGL((k_finish<S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
-                           a.samples, a.aocc, a.queue, a.stats);
+        hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});
     else primary(std::false_type{});

@@ -45,10 +45,17 @@ struct NoiseView {
     // calls, high word = wave iterations (the wave's first active lane adds 1 << 32 per call), so
     // calls / (64 * iterations) is the SIMD lane utilisation of the noise work
     mutable uint64_t calls;
+    // k_trace work kind of the caller (RT_PHASE_*): a diagnostic build (-DRT_COUNT_PHASE=k, scripts/
+    // phase_util.sh) counts only that kind's noise, to split the lane utilisation by phase
+    uint32_t phase;
 };
+enum { RT_PHASE_OTHER = 0, RT_PHASE_PRIMARY = 1, RT_PHASE_LONG = 2, RT_PHASE_SHADE = 3 };
 
 __device__ __forceinline__ void count_noise(const NoiseView& nz)
 {
+#ifdef RT_COUNT_PHASE
+    if (nz.phase != RT_COUNT_PHASE) return;
+#endif
     const uint64_t ex = __builtin_amdgcn_read_exec();
     nz.calls += 1ull + ((uint64_t)(__lane_id() == (uint32_t)__builtin_ctzll(ex)) << 32);
 }
