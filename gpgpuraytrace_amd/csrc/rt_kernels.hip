@@ -1116,6 +1116,13 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                         break;
                     }
                 }
+#ifdef RT_COUNT_PRIMARY_STEPS // diagnostic build: live lanes per primary march step (scripts/phase_util.py)
+                if (lv) {
+                    cf.nz.phase = RT_COUNT_PHASE;
+                    count_noise(cf.nz);
+                    cf.nz.phase = RT_PHASE_PRIMARY;
+                }
+#endif
                 if (lv) march_step<L, true, false>(cf, st);
                 if (it == 96u) __builtin_amdgcn_s_setprio(1);
                 else if (it == 224u) __builtin_amdgcn_s_setprio(2);

@@ -129,14 +129,16 @@ struct NoiseCell {
     uint32_t t; // perm2D texel of (Px & 127, Py & 127)
 };
 
-// FAST: the integer half without v_cvt_i32_f32 and with one shift.  gfx950 issues v_cvt_*,
-// v_floor, shifts, v_perm and the 3-operand integer ops at half the rate of FP32 add / mul / fma
-// and v_and / v_add_u32 (scripts/ubench_issue.hip), so the lattice integers come from the
+// FAST: the integer half without v_cvt_i32_f32 or shifts.  gfx950 issues v_cvt_*, v_floor,
+// shifts, v_perm and the 3-operand integer ops at half the rate of FP32 add / mul / fma and
+// v_and / v_add_u32 (profiles/r02/ubench_cost_model.md), so the lattice integers come from the
 // float floor values by the magic-number add: for an integer f with |f| < 2^22, the bits of
-// f + 1.5 * 2^23 hold (2^22 + f) in their low 23 bits, so bits & 127 == f & 127, and those of
-// fma(f, 4, 1.5 * 2^23) hold ((f & 127) << 2) under the mask 0x1fc when |4 f| < 2^22.  The caller
-// guarantees |coordinate| < kFastCellRange = 2^20 (floor keeps it).  Same bits as the general path.
-constexpr float kFastCellRange = 1048576.0f;
+// f + 1.5 * 2^23 hold (2^22 + f) in their low 23 bits, so bits & 127 == f & 127; those of
+// fma(f, 4, 1.5 * 2^23) hold ((f & 127) << 2) under the mask 0x1fc when |4 f| < 2^22, and those of
+// fma(f, 512, 1.5 * 2^23) hold ((f & 127) << 9) under the mask 0xfe00 when |512 f| < 2^22.  The
+// caller guarantees |coordinate| < kFastCellRange = 2^13 (floor keeps it).  Same bits as the
+// general path.
+constexpr float kFastCellRange = 8192.0f;
 constexpr float kMagic = 12582912.0f; // 1.5 * 2^23
 
 // Byte offset of perm2D texel (floor x & 127, floor y & 127) in the LDS image (see FAST below).
@@ -144,12 +146,9 @@ template <bool FAST>
 __device__ __forceinline__ uint32_t texel_offset(float fx, float fy)
 {
     if constexpr (FAST) {
-        const uint32_t mx4 = rtm::bits(fma(fx, 4.0f, kMagic)), my = rtm::bits(fy + kMagic);
-        // ((my << 9) | x4) & 0xfffc: one v_lshl_or_b32 (the compiler's lshl + and_or is two
-        // half-rate ops); a pure register op, so the asm needs no wait bookkeeping
-        uint32_t t;
-        asm("v_lshl_or_b32 %0, %1, 9, %2" : "=v"(t) : "v"(my), "v"(mx4 & 0x1fcu));
-        return t & 0xfffcu;
+        // (y << 9) & 0xfe00 | (x << 2) & 0x1fc: two full-rate fma + one v_and + one v_and_or
+        const uint32_t mx4 = rtm::bits(fma(fx, 4.0f, kMagic)), my9 = rtm::bits(fma(fy, 512.0f, kMagic));
+        return (my9 & 0xfe00u) | (mx4 & 0x1fcu);
     } else {
         // texel (Px & 127, Py & 127) at byte ((Py & 127) << 9) | ((Px & 127) << 2): the low
         // term stays below 512, so add-then-mask needs no separate Py mask
@@ -300,13 +299,33 @@ template <bool FAST>
 __device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
 {
     float s = 0.0f;
+#ifndef RT_EXTRA_OCTAVE
+    // The octave-table pointer is the trip counter: a per-lane register from the start (the asm
+    // keeps it out of SGPRs, which would cost a v_mov per iteration for the LDS address), one
+    // v_add and one v_cmp against the lane's end per octave.  n_oct >= 2, so a do-while is exact.
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const v4f lds_f4;
+    uint32_t op = (uint32_t)(uintptr_t)(lds_f4*)(c.nz.oct + 1); // LDS byte address of octave 1
+    asm volatile("" : "+v"(op));
+    const uint32_t oe = op + (uint32_t)n_oct * 16u;
     #pragma unroll 1
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
-        if (N > n_oct) break;
-        const float4 oc = c.nz.oct[N];
+    do {
+        const v4f oc = *(lds_f4*)(uintptr_t)op;
         count_noise(c.nz);
         s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * oc.x, q0.y * oc.y, q0.z * oc.x)), oc.z, s);
+        op += 16u;
+        asm("" : "+v"(op)); // opaque to loop strength reduction (which would add a second counter)
+    } while (op != oe);
+#else // cost experiment: RT_EXTRA_OCTAVE dead octaves per sample (weight 0: fma(v, 0, s) == s, s is never -0)
+    #pragma unroll 1
+    for (int N = 1; N <= RT_NP_OCTAVES + RT_EXTRA_OCTAVE; ++N) {
+        if (N > n_oct + RT_EXTRA_OCTAVE) break;
+        const float4 oc = c.nz.oct[N];
+        count_noise(c.nz);
+        s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * oc.x, q0.y * oc.y, q0.z * oc.x)),
+                N <= n_oct ? oc.z : 0.0f, s);
     }
+#endif
     return s;
 }
 
