@@ -807,7 +807,10 @@ __device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
 // (density_nomadplains_seg: the same fma chain in octave order, so every state bit is what
 // the single-lane march gives).  A phase runs until half its rays are done, hands the
 // states back to the owning lanes, and the survivors re-pack twice as wide.
-constexpr uint32_t kSegLive = 16; // live rays at or below which a wave switches to segment form
+#ifndef RT_SEG_LIVE
+#define RT_SEG_LIVE 16
+#endif
+constexpr uint32_t kSegLive = RT_SEG_LIVE; // live rays at or below which a wave switches to segment form
 // k_trace<.., SEG=true> carries the tail code; inlined, it costs the hot loops some spills
 // (scratch traffic, no measurable time at one GPU), so it is launched only when the shard
 // has few units per wave -- the strong-scaling regime where the last rays set the frame.
@@ -905,6 +908,10 @@ __device__ __forceinline__ void seg_finish(const Ctx& c, March<RT_NOMADPLAINS, t
 
 // Debug build only (make trace, -DRT_WAVE_TRACE): per-wave timeline of k_trace for
 // scheduler studies (scripts/wave_trace.py).  RT_WT_FIELDS u64 per wave slot.
+#ifdef RT_LIVE_HIST
+__device__ unsigned long long g_live_hist[65];
+#endif
+
 #ifdef RT_WAVE_TRACE
 #define RT_WT_FIELDS 18
 #define RT_WT_MAX_WAVES 8192
@@ -1110,6 +1117,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 lv = lv && march_live<L, true, false>(cf, st, RT_CAMERA_FAR, max_steps);
                 const uint64_t lb = __ballot(lv);
                 if (lb == 0ull) break;
+#ifdef RT_LIVE_HIST // diagnostic build: histogram of live lanes per primary march step (rt_debug_live_hist)
+                if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+                    atomicAdd(&g_live_hist[__popcll(lb)], 1ull);
+#endif
                 if constexpr (L == RT_NOMADPLAINS && SEG) {
                     if ((uint32_t)__popcll(lb) <= seg_live) {
                         seg_finish<false>(cf, st, lv, RT_CAMERA_FAR, max_steps, lane);
@@ -1382,8 +1393,12 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
     // (single frames only: batches have units enough, and a segment's lanes share one eye);
     // a.seg_mode (device flags RT_DEVICE_SEG_TAIL_*) forces it off or on
+#ifdef RT_SEG_BATCH // experiment: the segment tail for batches too (primary units only: a unit's lanes share one frame)
+    const bool seg = L == RT_NOMADPLAINS;
+#else
     const bool seg = L == RT_NOMADPLAINS && m.n_frames == 1u &&
                      (a.seg_mode >= 0 ? a.seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
+#endif
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
         (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
@@ -1557,6 +1572,20 @@ void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int 
     default: hipLaunchKernelGGL(k_debug_noise<RT_NOMADPLAINS>, g, b, 0, a.stream, a.consts, a.perm2d, a.grad, xyz, out, n, density); break;
     }
 }
+
+#ifdef RT_LIVE_HIST
+// diagnostic build: copies (and with reset != 0 clears) the live-lanes-per-primary-step histogram
+extern "C" int rt_debug_live_hist(unsigned long long* out, int reset)
+{
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_live_hist), 65 * 8) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[65] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_live_hist), zero, 65 * 8) != hipSuccess) return -1;
+    }
+    return 65;
+}
+#endif
 
 #ifdef RT_WAVE_TRACE
 // copies the last k_trace launch's per-wave timeline (RT_WT_FIELDS u64 per wave slot)

@@ -43,3 +43,17 @@ print("%-8s B=%d noise %d  wave-iterations %d  lane utilisation %.4f" % (
     os.environ.get("RT_LIB_VARIANT", "all"), B, calls, waves, calls / (64.0 * waves) if waves else 0.0))
 for d in devs:
     d.destroy()
+
+if os.environ.get("RT_LIB_VARIANT") == "lh":  # live lanes per primary march step (RT_LIVE_HIST build)
+    import ctypes as C
+    h = (C.c_ulonglong * 65)()
+    G.lib().rt_debug_live_hist(h, 1)  # cumulative over both renders above (the prepass adds none)
+    tot = sum(h)
+    lost = sum((64 - i) * n for i, n in enumerate(h))
+    print("primary wave-steps %d, mean live %.2f / 64" % (tot, sum(i * n for i, n in enumerate(h)) / max(1, tot)))
+    acc = 0
+    for lo in range(0, 64, 8):
+        n = sum(h[lo + 1:lo + 9])
+        l = sum((64 - i) * h[i] for i in range(lo + 1, lo + 9))
+        acc += l
+        print("  live %2d-%2d: %5.1f%% of steps, %5.1f%% of idle lane-steps" % (lo + 1, lo + 8, 100.0 * n / tot, 100.0 * l / max(1, lost)))
