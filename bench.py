@@ -161,6 +161,11 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
     return out, parity
 
 
+def progress(rank, msg):
+    """One progress line on stderr (the JSON line stays alone on stdout)."""
+    print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     import numpy as np
@@ -246,7 +251,9 @@ def main():
         return out
 
     want_cpu = rank == 0 and world == 1 and not a.no_cpu_baseline
+    progress(rank, f"instrumented batch of {B} + whole frame")
     counts = frame_counts(a.max_steps, a.ao, keep_frame=want_cpu)
+    progress(rank, "counts done")
     rays_per_frame, hits = counts["rays"], counts["hits"]
 
     # --- timed: batches of B frames, D batches in flight (FrameRing slot groups) ---
@@ -311,12 +318,14 @@ def main():
         P.run_batch(plan, rank, DeviceOps(n), frames=n)
         ring.frame += B
 
+    progress(rank, "warmup")
     for _ in range(-(-a.warmup // B) + ring.depth):
         batch_step(B)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    progress(rank, f"timed: {len(sizes)} batches")
     t0 = time.perf_counter()
     for n in sizes:
         batch_step(n)
@@ -326,6 +335,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
+    progress(rank, f"timed done ({elapsed * 1e3:.1f} ms)")
     verify = None
     if a.verify and rank == 0:
         # the last timed batch's frames, assembled from every rank's shards, against one whole frame
@@ -346,6 +356,7 @@ def main():
     # --- roofline pass: full batches one at a time on slot group 0 (launches do not overlap),
     # HIP events around every tracescreen launch on the stream it runs on; also the latency ---
     group0 = ring.slots[:B]
+    progress(rank, "roofline pass")
     ring.set_profiling(True)
     ring.kernel_time()
     torch.cuda.synchronize()

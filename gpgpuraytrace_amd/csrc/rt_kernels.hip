@@ -301,11 +301,21 @@ __device__ __forceinline__ uint32_t first_unit_index()
     return (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
 }
 
-__device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t t, const RayResult& rr)
+// A hit's RayResult, the shading input (misses store none).  With fog live (greenrocks): 3 float4
+// per sample (pd + dist, fcolord, density).  Without, fcolord is 0 and is not stored: (pd, dist) as
+// one float4 per sample and the density in a float plane after the batch's n samples (20 B per
+// hit instead of 48).
+template <int L>
+__device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, uint32_t t, const RayResult& rr)
 {
-    res[3u * t + 0u] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
-    res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
-    res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
+    if constexpr (FogLive<L>::value) {
+        res[3u * t + 0u] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+        res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
+        res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
+    } else {
+        res[t] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+        reinterpret_cast<float*>(res + n)[t] = rr.density;
+    }
 }
 
 // Longest-first tile order for k_trace.  A frame's critical path is its few
@@ -497,9 +507,17 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     const RtConsts* k = c.k;
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     ShadeHit h;
-    const float4 pdw = FRESH ? ld_fresh(res + 3u * t) : res[3u * t];
-    const float4 dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
-    h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
+    float4 pdw, dn;
+    if constexpr (FogLive<L>::value) {
+        pdw = FRESH ? ld_fresh(res + 3u * t) : res[3u * t];
+        dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
+        h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
+    } else { // store_ray's fog-free layout; fcolord is 0
+        const float* dp = reinterpret_cast<const float*>(res + m.frame_samples * m.n_frames) + t;
+        pdw = FRESH ? ld_fresh(res + t) : res[t];
+        dn = make_float4(FRESH ? __builtin_nontemporal_load(dp) : *dp, 0.0f, 0.0f, 0.0f);
+        h.fog = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
     uint32_t px, py, a;
     sample_pixel(m, m.frame_rot ? (t - tl) / m.frame_samples : 0u, tl, aa, W, H, &px, &py, &a);
     h.px = px;
@@ -575,6 +593,21 @@ __device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32
     march_begin(c, st, h.hp, 0.4f, h.prec, ao_dir(h.n, h.px, h.py, h.a, kk), false);
 }
 
+// The inputs a long shadow ray needs to finish its sample: (albedo + specular, brightness), fcolord
+// (fog-live landscapes only; 0 otherwise) and (rayleigh, skyAmount).
+template <int L>
+__device__ __forceinline__ void fin_store(float4* __restrict__ fin, uint32_t t, const ShadeHit& h)
+{
+    if constexpr (FogLive<L>::value) {
+        fin[3u * t + 0u] = h.cb;
+        fin[3u * t + 1u] = h.fog;
+        fin[3u * t + 2u] = h.ray;
+    } else {
+        fin[2u * t + 0u] = h.cb;
+        fin[2u * t + 1u] = h.ray;
+    }
+}
+
 // A long ray left its loop: a shadow ray finishes its sample from fin[t]; an AO ray
 // counts its occlusion for k_finish.
 template <int L, bool FRESH>
@@ -585,9 +618,16 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
     if (type == RT_LONG_AO) {
         if (st.d > 0.0f) atomicAdd(&aocc[t], 1u);
     } else {
-        const float4* f = fin + 3u * t;
-        samples[t] = FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
-                           : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w);
+        if constexpr (FogLive<L>::value) {
+            const float4* f = fin + 3u * t;
+            samples[t] = FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
+                               : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w);
+        } else { // fin_store's fog-free layout
+            const float4* f = fin + 2u * t;
+            const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            samples[t] = FRESH ? shade_finish(k, ld_fresh(f), zero, ld_fresh(f + 1), st.d, st.f.w)
+                               : shade_finish(k, f[0], zero, f[1], st.d, st.f.w);
+        }
     }
 }
 
@@ -632,9 +672,7 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
                 if constexpr (STATS) ssteps += (float)st.iters;
             } else {
-                fin[3u * t + 0u] = h.cb;
-                fin[3u * t + 1u] = h.fog;
-                fin[3u * t + 2u] = h.ray;
+                fin_store<L>(fin, t, h);
             }
         });
         const uint64_t lb = __ballot(more);
@@ -1072,9 +1110,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
                 if constexpr (STATS) ssteps += (float)st.iters;
             } else {
-                fin[3u * t + 0u] = h.cb;
-                fin[3u * t + 1u] = h.fog;
-                fin[3u * t + 2u] = h.ray;
+                fin_store<L>(fin, t, h);
             }
         });
         if (__ballot(more)) {
@@ -1145,7 +1181,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             if (valid) {
                 RayResult rr = march_result(st);
                 if constexpr (STATS) psteps += rr.steps;
-                if (hit) store_ray(res, t, rr); // the shading input
+                if (hit) store_ray<L>(res, m.frame_samples * m.n_frames, t, rr); // the shading input
                 else samples[t] = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
             }
             const uint64_t hb = __ballot(hit);
