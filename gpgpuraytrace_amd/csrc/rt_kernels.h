@@ -44,6 +44,7 @@ struct RtLaunch {
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
     uint32_t* order;          // k_order's tile order (rt_split_samples/1024 entries per frame)
+    uint64_t* hitmask;        // per 8x8 unit and AA sample: the primary hits' ballot (k_trace -> k_finish)
     const FrameTable* frames; // device table of the batch's frames
     FrameTable frames_host;   // the same pointers on the host
     uint32_t n_frames;        // frames in the batch (1..RT_MAX_BATCH)

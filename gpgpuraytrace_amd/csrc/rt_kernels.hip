@@ -964,6 +964,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
                                                 UnitMap m, const uint32_t* __restrict__ order,
+                                                uint64_t* __restrict__ hitmask,
                                                 float4* __restrict__ res, float4* __restrict__ samples,
                                                 float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
                                                 float4* __restrict__ shrec, uint32_t long_cap,
@@ -1181,10 +1182,21 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             if (valid) {
                 RayResult rr = march_result(st);
                 if constexpr (STATS) psteps += rr.steps;
-                if (hit) store_ray<L>(res, m.frame_samples * m.n_frames, t, rr); // the shading input
-                else samples[t] = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
+                if (hit) {
+                    store_ray<L>(res, m.frame_samples * m.n_frames, t, rr); // the shading input
+                } else {
+                    const float4 v = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
+                    if (aa == 1u) { // the pixel is final (k_finish's sum of one sample times rcp(1) is v itself)
+                        const size_t o = (size_t)py * W + px;
+                        ft->out8[f][o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
+                        if (float4* o32 = ft->out32[f]) o32[o] = make_float4(v.x, v.y, v.z, 1.0f);
+                    } else {
+                        samples[t] = v;
+                    }
+                }
             }
             const uint64_t hb = __ballot(hit);
+            if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = hb; // k_finish skips the misses
             if (hb) {
                 const uint32_t n = (uint32_t)__popcll(hb), rank = (uint32_t)__popcll(hb & lt_mask);
                 if constexpr (STATS) nhits += hit ? 1u : 0u;
@@ -1271,13 +1283,14 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     }
 }
 
-// tracescreen.hlsl:67-75: the sum of the saturated samples in AA order (misses were coloured by
-// k_trace, hits by the shading / long-ray paths; w marks a hit, whose AO factor applies), / AA,
-// UNORM8 store.  Persistent over 8x8 units, strided statically (wave w takes units w, w + n_waves,
-// ...): the per-unit work is so short that a shared queue atomic would serialise the pass.
+// tracescreen.hlsl:67-75: the sum of the saturated samples in AA order, / AA, UNORM8 store.  Misses
+// were coloured by k_trace (with one sample per pixel their pixels are already final there, and the
+// unit's hit ballot says which lanes remain), hits by the shading / long-ray paths; w marks a hit,
+// whose AO factor applies.  Persistent over 8x8 units, strided statically (wave w takes units w,
+// w + n_waves, ...): the per-unit work is so short that a shared queue atomic would serialise it.
 __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
-                                                 UnitMap m, const float4* __restrict__ samples,
-                                                 const uint32_t* __restrict__ aocc)
+                                                 UnitMap m, const uint64_t* __restrict__ hitmask,
+                                                 const float4* __restrict__ samples, const uint32_t* __restrict__ aocc)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
@@ -1289,6 +1302,8 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         float4* out32 = ft->out32[f];
         uint32_t px, py;
         if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
+        // one sample per pixel: k_trace wrote the misses' pixels, only the hits remain
+        if (aa == 1u && !((hitmask[f * m.n_units + u] >> lane) & 1ull)) continue;
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
             const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
@@ -1445,17 +1460,17 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
         const RtConsts* k0 = a.frames_host.k[0];
         if (seg)
             hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
-                               m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+                               m, a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
                                a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
         else
             hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
-                               m, a.order, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
+                               m, a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
                                a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
                            a.fin, a.samples, a.aocc, a.long_cap, a.queue, a.stats);
-        hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.samples, a.aocc);
+        hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});
     else primary(std::false_type{});

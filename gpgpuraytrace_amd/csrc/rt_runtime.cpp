@@ -118,6 +118,7 @@ struct rt_device_s {
     float4* res = nullptr;
     uint32_t* hitlist = nullptr;
     uint32_t* order = nullptr;
+    uint64_t* hitmask = nullptr; // per unit and AA sample: the primary-hit ballot (k_trace -> k_finish)
     float4* shrec = nullptr;
     float4* fin = nullptr;
     uint32_t* aocc = nullptr;
@@ -443,6 +444,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.res = dev->res;
     a.hitlist = dev->hitlist;
     a.order = dev->order;
+    a.hitmask = dev->hitmask;
     a.shrec = dev->shrec;
     a.long_cap = (uint32_t)std::min<size_t>(dev->long_cap, 0xffffffffu);
     a.fin = dev->fin;
@@ -477,8 +479,9 @@ int check_texture(Shader* s)
 }
 
 // Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded
-// colour (16 B), one primary RayResult (48 B), one hit-list slot (4 B), the
-// shading inputs of a long shadow ray (48 B) and an AO occlusion count (4 B); the
+// colour (16 B), one primary RayResult (48 B; 20 B used without fog), one hit-list slot (4 B),
+// the shading inputs of a long shadow ray (48 B; 32 B used without fog), an AO occlusion count
+// (4 B) and a hit bit (the 64-lane ballot per 8x8 unit and AA sample); the
 // global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
 // (48 B each).
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
@@ -493,6 +496,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     if (dev->res) HIP_TRY(hipFree(dev->res));
     if (dev->hitlist) HIP_TRY(hipFree(dev->hitlist));
     if (dev->order) HIP_TRY(hipFree(dev->order));
+    if (dev->hitmask) HIP_TRY(hipFree(dev->hitmask));
     if (dev->shrec) HIP_TRY(hipFree(dev->shrec));
     if (dev->fin) HIP_TRY(hipFree(dev->fin));
     if (dev->aocc) HIP_TRY(hipFree(dev->aocc));
@@ -503,6 +507,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     dev->res = nullptr;
     dev->hitlist = nullptr;
     dev->order = nullptr;
+    dev->hitmask = nullptr;
     dev->samples_cap = 0;
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
@@ -511,6 +516,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->aocc, need * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * RT_MAX_BATCH * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->hitmask, need / 64 * sizeof(uint64_t)));
     dev->samples_cap = need;
     dev->long_cap = long_need;
     return RT_OK;
@@ -592,6 +598,7 @@ void rt_device_destroy(rt_device d)
     if (d->res) (void)hipFree(d->res);
     if (d->hitlist) (void)hipFree(d->hitlist);
     if (d->order) (void)hipFree(d->order);
+    if (d->hitmask) (void)hipFree(d->hitmask);
     if (d->shrec) (void)hipFree(d->shrec);
     if (d->fin) (void)hipFree(d->fin);
     if (d->aocc) (void)hipFree(d->aocc);
