@@ -1,0 +1,26 @@
+#!/bin/bash
+# k_trace SQ counters of library variants (RT_LIB_VARIANT per argument, "" = default build): one
+# --pmc pass per variant with one batch in flight (12 frames), k_trace means printed per variant.
+# usage: pmc_variants.sh v1 v2 ...
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/pmcv; rm -rf $O; mkdir -p $O
+for v in "$@"; do
+  tag=${v:-default}
+  RT_LIB_VARIANT=$v timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
+    --output-format csv -d $O/$tag -o run -- python3 bench.py --steps 12 --warmup 1 --no-cpu-baseline --no-companions --frames-in-flight 1 > $O/$tag.log 2>&1 || { echo "pmc $tag failed"; exit 1; }
+  python3 - $O/$tag $tag <<'PY'
+import csv, glob, sys, collections
+per = collections.defaultdict(lambda: collections.defaultdict(float))
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+        if n.startswith("k_trace") and "true" not in n:
+            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+d = {c: sum(x[c] for x in per.values()) / len(per) for c in next(iter(per.values()))}
+cyc = d["GRBM_GUI_ACTIVE"] / 8
+print("== %-10s k_trace cycles %.4g  VALU %.4g  SALU %.4g  LDS %.4g  wait_any %.3f  wait_inst %.3f  cyc/VALU %.3f" % (
+    sys.argv[2], cyc, d["SQ_INSTS_VALU"], d["SQ_INSTS_SALU"], d["SQ_INSTS_LDS"], d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"],
+    d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"], cyc * 1024 / d["SQ_INSTS_VALU"]))
+PY
+done

@@ -188,7 +188,25 @@ def test_frame_bitexact_device_path(spec, tail):
     ref = gold[key + "_stats"]  # noise3d, prepass, primary, shadow, rays, hits, ao
     assert (st["noise_calls"], st["prepass_steps"], st["primary_steps"], st["shadow_steps"], st["hits"],
             st["ao_steps"]) == (ref[0], ref[1], ref[2], ref[3], ref[5], ref[6])
+    # wave iterations of the noise work (ABI 2): every one has at least one lane
+    assert 0 < st["noise_wave_iters"] <= st["noise_calls"]
     assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
+    dev.destroy()
+
+
+def test_noise_wave_iterations_bound_lane_utilisation():
+    """rt_stats.noise_wave_iters (ABI 2): over a tracescreen (the prepass's lane-only counts
+    subtracted), 64 * wave iterations >= noise evaluations, i.e. lane utilisation in (0, 1]."""
+    dev, ter = make(GI.consts(64, 48, "reset"), stats=True, max_steps=0, ao=1)
+    ter.update_shaders()
+    ter.camera_compute.run(2, 2, 1)
+    pre = dev.stats(reset=True)
+    ter.render_device()
+    st = dev.stats(reset=True)
+    calls = st["noise_calls"] - pre["noise_calls"]
+    waves = st["noise_wave_iters"] - pre["noise_wave_iters"]
+    assert pre["noise_wave_iters"] == 0 and waves > 0
+    assert 0.5 < calls / (64.0 * waves) <= 1.0
     dev.destroy()
 
 
