@@ -153,9 +153,11 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
         "tolerance": "bit-exact (north_star bound: 1e-4 per channel)",
     }
     out = {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
+           "host_cpus": os.cpu_count(),
            "sample": f"oracle/rt_oracle.c, prepass + rows 0::{row_step} of the {W}x{H} frame "
                      f"({s['primary_rays']} primary + {s['primary_hits']} shadow + {s['ao_rays']} AO + 1024 "
-                     f"prepass rays, {dt:.1f} s, {threads} OpenMP threads)",
+                     f"prepass rays, {dt:.1f} s, {threads} OpenMP threads = this process's CPU share "
+                     f"(OMP_NUM_THREADS / affinity) of the host's {os.cpu_count()})",
            "single_thread": {"value": round(rays1 / dt1 / 1e6, 4), "unit": "Mray/s", "cores": 1,
                              "sample": f"prepass + rows 0::{row_step_1t} ({rays1} rays, {dt1:.1f} s, 1 thread)"}}
     return out, parity
