@@ -304,7 +304,9 @@ __device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
     // keeps it out of SGPRs, which would cost a v_mov per iteration for the LDS address), one
     // v_add and one v_cmp against the lane's end per octave.  n_oct >= 2, so a do-while is exact.
     typedef float v4f __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(3))) const v4f lds_f4;
+    // volatile: one ds_read_b128 (4 LDS cycles, lane groups of 16 on one broadcast address) rather
+    // than the b96 the compiler narrows an unused .w to (8 cycles: lane groups of 8)
+    typedef __attribute__((address_space(3))) const volatile v4f lds_f4;
     uint32_t op = (uint32_t)(uintptr_t)(lds_f4*)(c.nz.oct + 1); // LDS byte address of octave 1
     asm volatile("" : "+v"(op));
     const uint32_t oe = op + (uint32_t)n_oct * 16u;

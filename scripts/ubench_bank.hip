@@ -15,6 +15,9 @@ constexpr int kIters = 2048;
 template <int K>
 __global__ void __launch_bounds__(1024) k_bank(float* out, unsigned long long* clk)
 {
+    __shared__ float lds_pad[4096 + 64 * 4];
+    if (threadIdx.x < 64) lds_pad[threadIdx.x] = 0.0f;
+    __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     const float x = (float)threadIdx.x * 1e-9f;
     asm volatile(
@@ -26,6 +29,7 @@ __global__ void __launch_bounds__(1024) k_bank(float* out, unsigned long long* c
         "v_mov_b32 v57, %0\n v_mov_b32 v61, %0\n v_mov_b32 v65, %0\n v_mov_b32 v69, %0\n"
         :: "v"(x) : "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v44", "v45", "v48",
         "v49", "v52", "v53", "v56", "v57", "v60", "v61", "v64", "v65", "v68", "v69");
+    const unsigned int laddr = (threadIdx.x & 63u) * 16u;
     for (int it = 0; it < kIters; ++it) {
         if constexpr (K == 0) // acc bank 0, sources banks 1 and 2: no conflict
             asm volatile("v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n"
@@ -115,6 +119,18 @@ __global__ void __launch_bounds__(1024) k_bank(float* out, unsigned long long* c
             asm volatile("v_and_b32 v40, 0x7f7f7f7f, v40\n v_and_b32 v44, 0x7f7f7f7f, v44\n v_and_b32 v48, 0x7f7f7f7f, v48\n v_and_b32 v52, 0x7f7f7f7f, v52\n v_and_b32 v56, 0x7f7f7f7f, v56\n v_and_b32 v60, 0x7f7f7f7f, v60\n v_and_b32 v64, 0x7f7f7f7f, v64\n v_and_b32 v68, 0x7f7f7f7f, v68\n " ::: "v40", "v41", "v44", "v45", "v48", "v49", "v52", "v53", "v56", "v57", "v60", "v61", "v64", "v65", "v68", "v69");
         if constexpr (K == 31) // v_add acc, literal
             asm volatile("v_add_f32 v40, 0x4b400000, v40\n v_add_f32 v44, 0x4b400000, v44\n v_add_f32 v48, 0x4b400000, v48\n v_add_f32 v52, 0x4b400000, v52\n v_add_f32 v56, 0x4b400000, v56\n v_add_f32 v60, 0x4b400000, v60\n v_add_f32 v64, 0x4b400000, v64\n v_add_f32 v68, 0x4b400000, v68\n " ::: "v40", "v41", "v44", "v45", "v48", "v49", "v52", "v53", "v56", "v57", "v60", "v61", "v64", "v65", "v68", "v69");
+        if constexpr (K == 40) // 8 fma (no conflict) + 0 LDS
+            asm volatile("v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
+        if constexpr (K == 41) // 8 fma + 1 ds_read_b128
+            asm volatile("ds_read_b128 v[92:95], v90\n v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
+        if constexpr (K == 42) // 8 fma + 2 ds_read_b128
+            asm volatile("ds_read_b128 v[92:95], v90\n ds_read_b128 v[96:99], v90 offset:1024\n v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
+        if constexpr (K == 43) // 8 fma + 4 ds_read_b128
+            asm volatile("ds_read_b128 v[92:95], v90\n ds_read_b128 v[96:99], v90 offset:1024\n ds_read_b128 v[100:103], v90 offset:2048\n ds_read_b128 v[104:107], v90 offset:3072\n v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
+        if constexpr (K == 44) // 8 fma + 4 ds_read_b64
+            asm volatile("ds_read_b64 v[92:93], v90\n ds_read_b64 v[96:97], v90 offset:1024\n ds_read_b64 v[100:101], v90 offset:2048\n ds_read_b64 v[104:105], v90 offset:3072\n v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
+        if constexpr (K == 45) // 8 fma + 4 ds_read_b32
+            asm volatile("ds_read_b32 v92, v90\n ds_read_b32 v96, v90 offset:1024\n ds_read_b32 v100, v90 offset:2048\n ds_read_b32 v104, v90 offset:3072\n v_fma_f32 v40, v40, v33, v34\n v_fma_f32 v44, v44, v33, v34\n v_fma_f32 v48, v48, v33, v34\n v_fma_f32 v52, v52, v33, v34\n v_fma_f32 v56, v56, v33, v34\n v_fma_f32 v60, v60, v33, v34\n v_fma_f32 v64, v64, v33, v34\n v_fma_f32 v68, v68, v33, v34\n s_waitcnt lgkmcnt(0)\n " :: "v"(laddr) : "v40", "v44", "v48", "v52", "v56", "v60", "v64", "v68", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107");
     }
     float r;
     asm volatile("v_add_f32 %0, v40, v44\n v_add_f32 %0, %0, v48\n v_add_f32 %0, %0, v68" : "=v"(r));
@@ -152,6 +168,12 @@ int main()
     unsigned long long* clk;
     (void)hipMalloc(&out, 256 * 1024 * sizeof(float));
     (void)hipMalloc(&clk, 16);
+    run<40>("8 fma (no conflict) + 0 LDS", out, clk);
+    run<41>("8 fma + 1 ds_read_b128", out, clk);
+    run<42>("8 fma + 2 ds_read_b128", out, clk);
+    run<43>("8 fma + 4 ds_read_b128", out, clk);
+    run<44>("8 fma + 4 ds_read_b64", out, clk);
+    run<45>("8 fma + 4 ds_read_b32", out, clk);
     run<0>("v_fma acc b0, src b1, b2 (distinct banks)", out, clk);
     run<1>("v_fma acc b0, src b0, b2 (2 in bank 0)", out, clk);
     run<2>("v_fma acc b0, src b0, b0 (3 in bank 0)", out, clk);
