@@ -263,6 +263,7 @@ struct UnitMap {
     uint32_t off_x, off_y, ext_x, ext_y, tiles32_x, tile_first, tile_stride, n_units;
     uint32_t n_frames, frame_samples;
     uint32_t frame_rot; // 1: frame f of a batch traces shard (tile_first + f) % tile_stride
+    uint32_t order_batch; // k_order: 1 one longest-first order over the batch, 0 one per frame (frame-major)
 };
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
@@ -326,32 +327,44 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, 
 // graze).  One workgroup buckets the shard's 32x32 tiles by that key (64 buckets,
 // descending); the order only decides which wave takes a unit when, never what
 // it computes.
-// One workgroup per frame of the batch; frame f's order at order + f * (n_units / 16).
+// The order spans the whole batch: entry i = (frame << 24) | tile, the batch's tiles of all frames
+// longest-first.  Frame-major order (each frame longest-first in turn) left the last frame's
+// grazing units to start in the last twelfth of the launch: at an 8-way shard, where a frame's
+// share of the launch is shorter than one such unit, they set the batch time (k_trace 5.7 ms for
+// 4.0 ms of work).  One workgroup; frame by frame it loads the frame's cell keys and buckets its
+// tiles (the bucket bytes stay in LDS for the scatter pass when they fit).
+constexpr uint32_t kOrderLdsBuckets = 144u * 1024u;
+constexpr uint32_t kOrderBatchUnitsPerWave = 4u;
 __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
                                                 uint32_t* __restrict__ order)
 {
-    const RtConsts* k = ft->k[blockIdx.x];
-    const float2* cells = ft->cells[blockIdx.x];
-    order += blockIdx.x * (m.n_units >> 4);
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
-    for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) {
-        float2 cd = cells[i];
-        s_key[i] = __log2f(cd.y / cd.x);
-    }
+    __shared__ uint8_t s_b[kOrderLdsBuckets];
     if (threadIdx.x < 64) s_hist[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
     const uint32_t n_tiles = m.n_units >> 4;
+    const bool cached = n_tiles * m.n_frames <= kOrderLdsBuckets;
+    uint32_t f = 0;
+    auto load_keys = [&]() {
+        __syncthreads(); // the previous frame's keys are no longer read
+        const float2* cells = ft->cells[f];
+        for (int i = threadIdx.x; i < RT_CAMERA_RES * RT_CAMERA_RES; i += blockDim.x) {
+            float2 cd = cells[i];
+            s_key[i] = __log2f(cd.y / cd.x);
+        }
+        __syncthreads();
+    };
     auto bucket = [&](uint32_t tile) -> uint32_t {
+        const RtConsts* k = ft->k[f];
+        const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height;
         float key = 0.0f;
         // corner pixels of the tile: unit 0 lane 0, unit 3 lane 7, unit 12 lane 56, unit 15 lane 63
         for (uint32_t corner = 0; corner < 4; ++corner) {
             uint32_t px, py;
             uint32_t u = tile * 16u + (corner & 1u) * 3u + (corner >> 1) * 12u;
             uint32_t lane = (corner & 1u) * 7u + (corner >> 1) * 56u;
-            if (!unit_pixel(m, blockIdx.x, u, lane, W, H, &px, &py)) {
-                if (!unit_pixel(m, blockIdx.x, tile * 16u, 0u, W, H, &px, &py)) continue;
+            if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) {
+                if (!unit_pixel(m, f, tile * 16u, 0u, W, H, &px, &py)) continue;
                 px = px + (corner & 1u) * 31u < W ? px + (corner & 1u) * 31u : W - 1u;
                 py = py + (corner >> 1) * 31u < H ? py + (corner >> 1) * 31u : H - 1u;
             }
@@ -362,18 +375,38 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
         int b = (int)(key * 3.3f);
         return (uint32_t)(b < 0 ? 0 : (b > 63 ? 63 : b));
     };
-    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) atomicAdd(&s_hist[bucket(t)], 1u);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int b = 63; b >= 0; --b) {
-            uint32_t c = s_hist[b];
-            s_hist[b] = run;
-            run += c;
+    // frames [g0, g0 + group) share one longest-first order: the whole batch, or one frame
+    const uint32_t group = m.order_batch ? m.n_frames : 1u;
+    for (uint32_t g0 = 0; g0 < m.n_frames; g0 += group) {
+        const uint32_t g1 = g0 + group < m.n_frames ? g0 + group : m.n_frames;
+        for (f = g0; f < g1; ++f) {
+            load_keys();
+            for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+                const uint32_t b = bucket(t);
+                if (cached) s_b[f * n_tiles + t] = (uint8_t)b;
+                atomicAdd(&s_hist[b], 1u);
+            }
         }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t run = g0 * n_tiles;
+            for (int b = 63; b >= 0; --b) {
+                uint32_t c = s_hist[b];
+                s_hist[b] = run;
+                run += c;
+            }
+        }
+        for (f = g0; f < g1; ++f) {
+            if (cached) __syncthreads();
+            else load_keys();
+            for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+                const uint32_t b = cached ? (uint32_t)s_b[f * n_tiles + t] : bucket(t);
+                order[atomicAdd(&s_hist[b], 1u)] = (f << 24) | t;
+            }
+        }
+        __syncthreads(); // the scatter's atomics are done before the next group clears the histogram
+        if (threadIdx.x < 64) s_hist[threadIdx.x] = 0;
     }
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) order[atomicAdd(&s_hist[bucket(t)], 1u)] = t;
 }
 
 // Shading (tracescreen.hlsl:28-35, nomadplains/color.hlsl:8-72).  Per hit, the
@@ -1248,9 +1281,9 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             const uint32_t qi = first_unit ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
             first_unit = false;
             if (qi < m.n_units * m.n_frames) {
-                // frame-major over the batch: frame f's units in its own longest-first order
-                const uint32_t f = __builtin_amdgcn_readfirstlane(qi / m.n_units), ql = qi - f * m.n_units;
-                do_unit(f, __builtin_amdgcn_readfirstlane(order[f * (m.n_units >> 4) + (ql >> 4)]) * 16u + (ql & 15u));
+                // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
+                const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);
+                do_unit(e >> 24, (e & 0xffffffu) * 16u + (qi & 15u));
                 WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
             } else if (lane == 0) q.drained = 1u;
             if (lane == 0) atomicSub(&q.active, 1u);
@@ -1438,6 +1471,11 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
+#ifdef RT_ORDER_BATCH // A/B: force the batch-wide (1) or the frame-major (0) unit order
+    m.order_batch = RT_ORDER_BATCH;
+#else
+    m.order_batch = m.n_frames > 1u && m.n_units < kOrderBatchUnitsPerWave * pblocks * 16u;
+#endif
     // k_finish holds no LDS: up to 2 blocks per CU
     uint32_t fblocks = need < 2u * blocks ? need : 2u * blocks;
     dim3 blk(1024);
@@ -1453,7 +1491,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
         (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
-    hipLaunchKernelGGL(k_order, dim3(m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
+    hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.frames, m, a.order);
     // primary + shading + long rays; what did not fit the CU's rings goes to the global lists
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
