@@ -303,9 +303,10 @@ __device__ __forceinline__ uint32_t first_unit_index()
 }
 
 // A hit's RayResult, the shading input (misses store none).  With fog live (greenrocks): 3 float4
-// per sample (pd + dist, fcolord, density).  Without, fcolord is 0 and is not stored: (pd, dist) as
-// one float4 per sample and the density in a float plane after the batch's n samples (20 B per
-// hit instead of 48).
+// per sample (pd + dist, fcolord, density).  Without, fcolord is 0 and is not stored, and the hit
+// position is not either: the shading re-derives it from the pixel's ray and the last sample's
+// distance (march_result's fma).  (sd, dist) as one float2 per sample and the density in a float
+// plane after the batch's n samples: 12 B per hit instead of 48.
 template <int L>
 __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, uint32_t t, const RayResult& rr)
 {
@@ -314,8 +315,9 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, 
         res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
         res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
     } else {
-        res[t] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
-        reinterpret_cast<float*>(res + n)[t] = rr.density;
+        float2* sdd = reinterpret_cast<float2*>(res);
+        sdd[t] = make_float2(rr.sd, rr.pd.w);
+        reinterpret_cast<float*>(sdd + n)[t] = rr.density;
     }
 }
 
@@ -461,6 +463,13 @@ __device__ __forceinline__ float4 miss_sample(const Ctx& c, float px, float py, 
 
 // Loads of data another wave of this kernel wrote: bypass the CU's L1 (a line cached
 // there earlier would be stale), served by the XCD's L2 the producer wrote through.
+__device__ __forceinline__ float ld_fresh1(const float* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ float2 ld_fresh2(const float2* p)
+{
+    typedef float v2f __attribute__((ext_vector_type(2)));
+    const v2f v = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p));
+    return make_float2(v.x, v.y);
+}
 __device__ __forceinline__ float4 ld_fresh(const float4* p)
 {
     typedef float v4f __attribute__((ext_vector_type(4)));
@@ -546,9 +555,11 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
         dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
         h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
     } else { // store_ray's fog-free layout; fcolord is 0
-        const float* dp = reinterpret_cast<const float*>(res + m.frame_samples * m.n_frames) + t;
-        pdw = FRESH ? ld_fresh(res + t) : res[t];
-        dn = make_float4(FRESH ? __builtin_nontemporal_load(dp) : *dp, 0.0f, 0.0f, 0.0f);
+        const float2* sdd = reinterpret_cast<const float2*>(res);
+        const float* dp = reinterpret_cast<const float*>(sdd + m.frame_samples * m.n_frames) + t;
+        const float2 sdw = FRESH ? ld_fresh2(sdd + t) : sdd[t];
+        pdw = make_float4(sdw.x, 0.0f, 0.0f, sdw.y); // (sd, -, -, dist) until the position is re-derived
+        dn = make_float4(FRESH ? ld_fresh1(dp) : *dp, 0.0f, 0.0f, 0.0f);
         h.fog = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     uint32_t px, py, a;
@@ -558,6 +569,12 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     h.a = a;
     f3 p, dir;
     get_pixel_ray(c, (float)px + k->aa_off[a][0], (float)py + k->aa_off[a][1], &p, &dir);
+    if constexpr (!FogLive<L>::value) {
+        // the primary march's last sample: march_begin's normalised direction, the step's fma
+        const f3 md = rtm::scale(dir, rtm::rcp(rtm::length(dir)));
+        const float sd = pdw.x;
+        pdw = make_float4(fma(md.x, sd, p.x), fma(md.y, sd, p.y), fma(md.z, sd, p.z), pdw.w);
+    }
     f3 pdn = rtm::normalize(dir);
     float skyAmount = pdw.w * 0.0005f;
     skyAmount = rtm::sat(skyAmount * skyAmount);
@@ -892,7 +909,7 @@ __device__ __forceinline__ void march_shfl(March<L, CF>& d, const March<L, CF>& 
     auto f = [&](float x) { return __shfl(x, (int)src, 64); };
     d.p = rtm::mk(f(s.p.x), f(s.p.y), f(s.p.z));
     d.dir = rtm::mk(f(s.dir.x), f(s.dir.y), f(s.dir.z));
-    d.rayp = rtm::mk(f(s.rayp.x), f(s.rayp.y), f(s.rayp.z));
+    d.sd = f(s.sd);
     d.dist = f(s.dist);
     d.step = f(s.step);
     d.lastStep = f(s.lastStep);

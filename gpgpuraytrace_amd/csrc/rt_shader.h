@@ -548,6 +548,7 @@ struct RayResult {
     f4 fc;
     float density;
     float steps;
+    float sd; // the last sample's distance (pd.xyz = p + dir * sd)
 };
 
 // Media/common/shaders/tracing.hlsl:47-105 (+ build extension max_steps) as an
@@ -559,7 +560,8 @@ struct RayResult {
 template <int L, bool CALCFOG>
 struct March {
     static constexpr bool FOG = CALCFOG && FogLive<L>::value;
-    f3 p, dir, rayp;
+    f3 p, dir;
+    float sd; // the distance of the last density sample: that sample is at p + dir * sd (march_result)
     float dist, step, lastStep, d;
     f4 f;
     int iters;
@@ -592,7 +594,7 @@ __device__ __forceinline__ void march_begin(const Ctx& c, March<L, CALCFOG>& m, 
     m.p = p;
     m.dir = dir;
     m.dist = dist;
-    m.rayp = rtm::mk(0.0f, 0.0f, 0.0f);
+    m.sd = 0.0f;
     m.iters = 0;
 }
 
@@ -608,11 +610,12 @@ __device__ __forceinline__ void march_step_with(const Ctx& c, March<L, CALCFOG>&
 {
     const RtConsts* k = c.k;
     ++m.iters;
-    m.rayp = rtm::mk(fma(m.dir.x, m.dist, m.p.x), fma(m.dir.y, m.dist, m.p.y), fma(m.dir.z, m.dist, m.p.z));
-    m.d = density(m.rayp);
+    const f3 rayp = rtm::mk(fma(m.dir.x, m.dist, m.p.x), fma(m.dir.y, m.dist, m.p.y), fma(m.dir.z, m.dist, m.p.z));
+    m.sd = m.dist;
+    m.d = density(rayp);
     f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
     if constexpr (March<L, CALCFOG>::FOG) if (m.fog) {
-        f4 g = get_fog<L>(c, m.rayp, m.dist);
+        f4 g = get_fog<L>(c, rayp, m.dist);
         fs.x = g.x * m.step;
         fs.y = g.y * m.step;
         fs.z = g.z * m.step;
@@ -659,9 +662,13 @@ template <int L, bool CALCFOG>
 __device__ __forceinline__ RayResult march_result(const March<L, CALCFOG>& m)
 {
     RayResult rr;
-    rr.pd.x = m.rayp.x;
-    rr.pd.y = m.rayp.y;
-    rr.pd.z = m.rayp.z;
+    // the last sample's position, recomputed from its distance with the step's own fma (no step:
+    // rayp's initial 0); carrying one distance instead of the position frees 2 VGPRs per march
+    const bool stepped = m.iters > 0;
+    rr.pd.x = stepped ? fma(m.dir.x, m.sd, m.p.x) : 0.0f;
+    rr.pd.y = stepped ? fma(m.dir.y, m.sd, m.p.y) : 0.0f;
+    rr.pd.z = stepped ? fma(m.dir.z, m.sd, m.p.z) : 0.0f;
+    rr.sd = m.sd;
     rr.pd.w = m.dist;
     rr.fc = m.f;
     rr.density = m.d;
