@@ -377,10 +377,10 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
         int b = (int)(key * 3.3f);
         return (uint32_t)(b < 0 ? 0 : (b > 63 ? 63 : b));
     };
-    // frames [g0, g0 + group) share one longest-first order: the whole batch, or one frame
-    const uint32_t group = m.order_batch ? m.n_frames : 1u;
-    for (uint32_t g0 = 0; g0 < m.n_frames; g0 += group) {
-        const uint32_t g1 = g0 + group < m.n_frames ? g0 + group : m.n_frames;
+    // frames [g0, g1) share one longest-first order: the whole batch (one workgroup), or frame
+    // blockIdx.x alone (a workgroup per frame)
+    {
+        const uint32_t g0 = m.order_batch ? 0u : blockIdx.x, g1 = m.order_batch ? m.n_frames : blockIdx.x + 1u;
         for (f = g0; f < g1; ++f) {
             load_keys();
             for (uint32_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
@@ -406,8 +406,6 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
                 order[atomicAdd(&s_hist[b], 1u)] = (f << 24) | t;
             }
         }
-        __syncthreads(); // the scatter's atomics are done before the next group clears the histogram
-        if (threadIdx.x < 64) s_hist[threadIdx.x] = 0;
     }
 }
 
@@ -1448,7 +1446,7 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
         using L32 = std::integral_constant<int, 32>;
         if (n <= 2) go(C256{}, L32{});
         else if (n <= 4) go(C512{}, L32{});
-        else go(C512{}, std::integral_constant<int, 8>{});
+        else go(C512{}, std::integral_constant<int, 8>{}); // 64 rays of 16 lanes per 1024 threads: same
         return;
     }
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64, n), block(64);
@@ -1508,7 +1506,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
         (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
-    hipLaunchKernelGGL(k_order, dim3(1), blk, 0, a.stream, a.frames, m, a.order);
+    hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
     // primary + shading + long rays; what did not fit the CU's rings goes to the global lists
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
