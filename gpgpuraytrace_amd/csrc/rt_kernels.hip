@@ -70,6 +70,20 @@ __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __
     __syncthreads();
 }
 
+// A buffer pointer read from a FrameTable, as a global-address-space pointer: plain pointers
+// loaded from memory are generic, and their accesses flat instructions that wait on the LDS
+// counter too.
+template <class T>
+__device__ __forceinline__ T __attribute__((address_space(1)))* gptr(T* p)
+{
+    return (T __attribute__((address_space(1)))*)p;
+}
+__device__ __forceinline__ void gstore(float4* p, float4 v)
+{
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    *(v4f __attribute__((address_space(1)))*)p = v4f{v.x, v.y, v.z, v.w};
+}
+
 __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
 {
     Ctx c;
@@ -80,7 +94,7 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     c.nz.calls = 0;
     c.nz.phase = RT_PHASE_OTHER;
     c.k = k;
-    c.kf = k;
+    c.kf = (KPtr)k;
     c.eye = rtm::mk(k->eye[0], k->eye[1], k->eye[2]);
     c.sun = rtm::mk(k->sun[0], k->sun[1], k->sun[2]);
     return c;
@@ -102,7 +116,7 @@ __device__ __forceinline__ float uniform_f(float x)
 __device__ __forceinline__ Ctx frame_ctx_cam(const Ctx& c, const FrameTable* __restrict__ ft, uint32_t f)
 {
     Ctx cf = c;
-    cf.kf = ft->kcam[f];
+    cf.kf = (KPtr)ft->kcam[f];
     cf.eye = rtm::mk(uniform_f(cf.kf->eye[0]), uniform_f(cf.kf->eye[1]), uniform_f(cf.kf->eye[2]));
     cf.sun = rtm::mk(uniform_f(cf.kf->sun[0]), uniform_f(cf.kf->sun[1]), uniform_f(cf.kf->sun[2]));
     return cf;
@@ -491,7 +505,7 @@ enum { RT_LONG_SHADOW = 0, RT_LONG_AO = 1 };
 __device__ __forceinline__ Ctx frame_ctx(const Ctx& c, const FrameTable* __restrict__ ft, uint32_t f)
 {
     Ctx cf = c;
-    cf.kf = ft->k[f];
+    cf.kf = (KPtr)ft->k[f];
     cf.eye = rtm::mk(uniform_f(cf.kf->eye[0]), uniform_f(cf.kf->eye[1]), uniform_f(cf.kf->eye[2]));
     cf.sun = rtm::mk(uniform_f(cf.kf->sun[0]), uniform_f(cf.kf->sun[1]), uniform_f(cf.kf->sun[2]));
     return cf;
@@ -862,10 +876,14 @@ struct TraceQueues {
     float4 longs[kLongRing * kShadowRec];
 };
 
+// A fresh read of a ring field another wave may have written: a relaxed workgroup-scope atomic
+// load.  (A volatile read kept its generic pointer -- the address-space inference leaves volatile
+// accesses alone -- so every ring poll was a flat load with system-scope cache bits, waiting on
+// the vector memory counter too, with the fields' 64-bit flat addresses held in VGPRs.)
 template <class T>
 __device__ __forceinline__ T vload(const T& x)
 {
-    return *const_cast<const volatile T*>(&x);
+    return __hip_atomic_load(&x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 __device__ __forceinline__ void q_lock(uint32_t* lock, uint32_t lane)
@@ -1184,7 +1202,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         float plane_x = 0.0f;
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-            plane_x = ft->cells[f][(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))].x;
+            plane_x = gptr(ft->cells[f])[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))].x;
         }
         for (uint32_t a = 0; a < aa; ++a) {
             const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
@@ -1236,8 +1254,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                     const float4 v = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
                     if (aa == 1u) { // the pixel is final (k_finish's sum of one sample times rcp(1) is v itself)
                         const size_t o = (size_t)py * W + px;
-                        ft->out8[f][o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
-                        if (float4* o32 = ft->out32[f]) o32[o] = make_float4(v.x, v.y, v.z, 1.0f);
+                        gptr(ft->out8[f])[o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
+                        if (float4* o32 = ft->out32[f]) gstore(o32 + o, make_float4(v.x, v.y, v.z, 1.0f));
                     } else {
                         samples[t] = v;
                     }
@@ -1346,7 +1364,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
     const uint32_t total = m.n_units * m.n_frames;
     for (uint32_t g = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); g < total; g += n_waves) {
         const uint32_t f = __builtin_amdgcn_readfirstlane(g / m.n_units), u = g - f * m.n_units;
-        uint32_t* out8 = ft->out8[f];
+        auto* out8 = gptr(ft->out8[f]);
         float4* out32 = ft->out32[f];
         uint32_t px, py;
         if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
@@ -1370,7 +1388,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         c2 = c2 * ia;
         size_t o = (size_t)py * (size_t)k->width + px;
         out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
-        if (out32) out32[o] = make_float4(c0, c1, c2, 1.0f);
+        if (out32) gstore(out32 + o, make_float4(c0, c1, c2, 1.0f));
     }
 }
 

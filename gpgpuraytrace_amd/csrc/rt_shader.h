@@ -228,10 +228,15 @@ __device__ __forceinline__ float noise3d(const NoiseView& nz, float px, float py
 // block of the frame being traced, for the fields that change per frame (ViewInverse, the
 // eye-dependent sky terms; Eye and SunDirection are copied into eye / sun).  kf == k except
 // in frame batches.
+// A frame's constant block as the kernels read it: in the constant address space, so that its
+// uniform loads are scalar (the pointer comes from a FrameTable in memory, where a plain pointer
+// would be generic and every read a flat load waiting on both memory counters).
+typedef const __attribute__((address_space(4))) RtConsts* KPtr;
+
 struct Ctx {
     NoiseView nz;
     const RtConsts* k;
-    const RtConsts* kf;
+    KPtr kf;
     f3 eye;
     f3 sun;
 };
@@ -710,7 +715,7 @@ __device__ __forceinline__ void get_pixel_ray(const Ctx& c, float px, float py, 
     float sy = fma(py + 0.5f, k->rcp_h, -0.5f) * 2.0f;
     sx = sx * c.kf->proj22;
     sy = sy * c.kf->proj11;
-    const float* m = c.kf->view_inverse;
+    const auto* m = c.kf->view_inverse;
     float r0 = fma(1.0f, m[12], fma(1.0f, m[8], fma(sy, m[4], sx * m[0])));
     float r1 = fma(1.0f, m[13], fma(1.0f, m[9], fma(sy, m[5], sx * m[1])));
     float r2 = fma(1.0f, m[14], fma(1.0f, m[10], fma(sy, m[6], sx * m[2])));
@@ -756,7 +761,7 @@ __device__ __forceinline__ SkyColor get_rayleigh_mie(const Ctx& c, f3 org)
 {
     const RtConsts* k = c.k;
     f3 rd = mod_ray_dir(org);
-    const RtConsts* kf = c.kf;
+    const KPtr kf = c.kf;
     float far = fma((1.0f - rd.y) * kf->sky_dist_to_top, 2.0f, kf->sky_dist_to_top);
     f3 start = rtm::mk(kf->sky_start[0], kf->sky_start[1], kf->sky_start[2]);
     float fStartAngle = rtm::dot(rd, rtm::mk(kf->sky_start_n[0], kf->sky_start_n[1], kf->sky_start_n[2]));
