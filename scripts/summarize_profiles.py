@@ -116,7 +116,10 @@ def main(src, dst):
                "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
                "kernels": "tracescreen launch: k_order + k_trace + k_shade_pre + k_shadow + k_finish (uninstrumented)",
                "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"}
-    json.dump(tr, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    tpath = os.path.join(dst, "traffic.json")
+    old = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    old.update(tr)  # other configs' launches (traffic_summary.py merges) stay
+    json.dump(old, open(tpath, "w"), indent=1)
     print(open(os.path.join(dst, "kernels.md")).read())
     print(json.dumps(tr, indent=1))
 
