@@ -418,8 +418,8 @@ def main():
     value = rays_per_frame * a.steps / elapsed / 1e6
     batch_noise = counts["batch_noise"]
     achieved = batch_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
-    traffic = None
-    if os.path.exists(a.traffic_json):
+    traffic = None  # measured for whole frames (one GPU); a rank's shard launch has no entry
+    if world == 1 and os.path.exists(a.traffic_json):
         try:
             with open(a.traffic_json) as f:
                 tj = json.load(f)
