@@ -313,7 +313,8 @@ __device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane,
 // the unit index a wave takes first: wave-slot-major over the grid, see k_trace
 __device__ __forceinline__ uint32_t first_unit_index()
 {
-    return (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+    // wave-uniform: computed in scalar registers, so no VGPR has to carry threadIdx to the first unit
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * gridDim.x + blockIdx.x;
 }
 
 // A hit's RayResult, the shading input (misses store none).  With fog live (greenrocks): 3 float4
@@ -610,7 +611,7 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
 }
 
 // Long-ray record (48 B): (p, dist), (step, lastStep, iters | type << 31, t),
-// (shadow fog | AO dir).  A shadow ray's direction is SunDirection /
+// (shadow fog | AO dir; a fog-free landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
 // length(SunDirection) (tracing.hlsl:60-61) for every ray; an AO ray carries its own
 // (normalised) direction in the fog slot, since AO rays march without fog.  The
 // density d is not kept: a stored ray is live, so its next step overwrites d before
@@ -621,7 +622,8 @@ __device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, 
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
     r[1] = make_float4(st.step, st.lastStep, __uint_as_float((uint32_t)st.iters | (type << 31)), __uint_as_float(t));
     if (type == RT_LONG_AO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
-    else r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
+    else if constexpr (March<L, true>::FOG) r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
+    // no fog: a shadow ray's f is +0 throughout (march_step), so r2 is neither written nor read
 }
 
 template <int L>
@@ -642,7 +644,10 @@ __device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1
         st.fog = false;
     } else {
         st.dir = sun_dir;
-        st.f = {r2.x, r2.y, r2.z, r2.w};
+        // without fog the stored f is the +0 long_pack wrote: restating it as a constant lets the
+        // compiler drop f from the long-ray loops' live state
+        if constexpr (March<L, true>::FOG) st.f = {r2.x, r2.y, r2.z, r2.w};
+        else st.f = {0.0f, 0.0f, 0.0f, 0.0f};
         st.fog = true;
     }
     return __float_as_uint(r1.w);
