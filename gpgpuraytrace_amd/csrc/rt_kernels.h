@@ -40,7 +40,7 @@ struct RtLaunch {
     float4* shrec;            // 3 float4 per long ray on the global list: march state + sample id + type
     uint32_t long_cap;        // entries shrec holds
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
-    uint32_t* aocc;           // per sample: occluded AO rays (AO extension)
+    uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
     uint32_t* order;          // k_order's tile order (rt_split_samples/1024 entries per frame)

@@ -320,8 +320,8 @@ __device__ __forceinline__ uint32_t first_unit_index()
 // A hit's RayResult, the shading input (misses store none).  With fog live (greenrocks): 3 float4
 // per sample (pd + dist, fcolord, density).  Without, fcolord is 0 and is not stored, and the hit
 // position is not either: the shading re-derives it from the pixel's ray and the last sample's
-// distance (march_result's fma).  (sd, dist) as one float2 per sample and the density in a float
-// plane after the batch's n samples: 12 B per hit instead of 48.
+// distance (march_result's fma).  (sd, dist, density) as 3 floats at a 12-byte stride: 12 B per hit
+// instead of 48, in one contiguous record.
 template <int L>
 __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, uint32_t t, const RayResult& rr)
 {
@@ -330,9 +330,11 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, 
         res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
         res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
     } else {
-        float2* sdd = reinterpret_cast<float2*>(res);
-        sdd[t] = make_float2(rr.sd, rr.pd.w);
-        reinterpret_cast<float*>(sdd + n)[t] = rr.density;
+        (void)n;
+        float* r = reinterpret_cast<float*>(res) + 3u * t;
+        r[0] = rr.sd;
+        r[1] = rr.pd.w;
+        r[2] = rr.density;
     }
 }
 
@@ -477,17 +479,39 @@ __device__ __forceinline__ float4 miss_sample(const Ctx& c, float px, float py, 
 // Loads of data another wave of this kernel wrote: bypass the CU's L1 (a line cached
 // there earlier would be stale), served by the XCD's L2 the producer wrote through.
 __device__ __forceinline__ float ld_fresh1(const float* p) { return __builtin_nontemporal_load(p); }
-__device__ __forceinline__ float2 ld_fresh2(const float2* p)
-{
-    typedef float v2f __attribute__((ext_vector_type(2)));
-    const v2f v = __builtin_nontemporal_load(reinterpret_cast<const v2f*>(p));
-    return make_float2(v.x, v.y);
-}
 __device__ __forceinline__ float4 ld_fresh(const float4* p)
 {
     typedef float v4f __attribute__((ext_vector_type(4)));
     const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
     return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// A hit's finished sample.  With one sample per pixel only hits reach `samples` (misses are
+// finished where their march ends) and every sample k_finish reads is a hit, so the record is the
+// colour alone: 12 B (a float3 array over the same buffer); with AA, misses are stored too and w
+// marks the hits (16 B).
+__device__ __forceinline__ void sample_store(const RtConsts* k, float4* __restrict__ samples, uint32_t t, float4 v)
+{
+    if (k->aa_samples == 1) { // 3 floats at 12-byte stride (a float3 vector type would pad to 16)
+        float* c = reinterpret_cast<float*>(samples) + 3u * t;
+        c[0] = v.x;
+        c[1] = v.y;
+        c[2] = v.z;
+    } else {
+        samples[t] = v;
+    }
+}
+
+// The AO extension's per-sample count of occluded AO rays: one byte per sample (at most 16 AO
+// rays), four to a word, so a count's atomic add and k_finish's read touch a quarter of the lines
+// a word per sample did (and the per-launch memset a quarter of the bytes).
+__device__ __forceinline__ void ao_count(uint32_t* __restrict__ aocc, uint32_t t)
+{
+    atomicAdd(&aocc[t >> 2], 1u << ((t & 3u) * 8u));
+}
+__device__ __forceinline__ uint32_t ao_occluded(const uint32_t* __restrict__ aocc, uint32_t t)
+{
+    return (aocc[t >> 2] >> ((t & 3u) * 8u)) & 0xffu;
 }
 
 struct ShadeHit {
@@ -568,9 +592,9 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
         dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
         h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
     } else { // store_ray's fog-free layout; fcolord is 0
-        const float2* sdd = reinterpret_cast<const float2*>(res);
-        const float* dp = reinterpret_cast<const float*>(sdd + m.frame_samples * m.n_frames) + t;
-        const float2 sdw = FRESH ? ld_fresh2(sdd + t) : sdd[t];
+        const float* r = reinterpret_cast<const float*>(res) + 3u * t;
+        const float2 sdw = make_float2(FRESH ? ld_fresh1(r) : r[0], FRESH ? ld_fresh1(r + 1) : r[1]);
+        const float* dp = r + 2;
         pdw = make_float4(sdw.x, 0.0f, 0.0f, sdw.y); // (sd, -, -, dist) until the position is re-derived
         dn = make_float4(FRESH ? ld_fresh1(dp) : *dp, 0.0f, 0.0f, 0.0f);
         h.fog = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -683,17 +707,17 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
                                             uint32_t type, const March<L, true>& st)
 {
     if (type == RT_LONG_AO) {
-        if (st.d > 0.0f) atomicAdd(&aocc[t], 1u);
+        if (st.d > 0.0f) ao_count(aocc, t);
     } else {
         if constexpr (FogLive<L>::value) {
             const float4* f = fin + 3u * t;
-            samples[t] = FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
-                               : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w);
+            sample_store(k, samples, t, FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
+                                              : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w));
         } else { // fin_store's fog-free layout
             const float4* f = fin + 2u * t;
             const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            samples[t] = FRESH ? shade_finish(k, ld_fresh(f), zero, ld_fresh(f + 1), st.d, st.f.w)
-                               : shade_finish(k, f[0], zero, f[1], st.d, st.f.w);
+            sample_store(k, samples, t, FRESH ? shade_finish(k, ld_fresh(f), zero, ld_fresh(f + 1), st.d, st.f.w)
+                                              : shade_finish(k, f[0], zero, f[1], st.d, st.f.w));
         }
     }
 }
@@ -736,7 +760,7 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
             c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
-                samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
+                sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
                 if constexpr (STATS) ssteps += (float)st.iters;
             } else {
                 fin_store<L>(fin, t, h);
@@ -1179,7 +1203,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
-                samples[t] = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
+                sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
                 if constexpr (STATS) ssteps += (float)st.iters;
             } else {
                 fin_store<L>(fin, t, h);
@@ -1378,9 +1402,15 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
             const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
-            float4 v = samples[t];
+            float4 v;
+            if (aa == 1u) { // sample_store's colour-only record of a hit
+                const float* c = reinterpret_cast<const float*>(samples) + 3u * t;
+                v = make_float4(c[0], c[1], c[2], 1.0f);
+            } else {
+                v = samples[t];
+            }
             if (v.w > 0.0f && k->ao_samples > 0) { // AO extension: ao multiplies the saturated sample
-                const float ao = ao_factor(aocc[t], k->ao_samples);
+                const float ao = ao_factor(ao_occluded(aocc, t), k->ao_samples);
                 v = make_float4(v.x * ao, v.y * ao, v.z * ao, v.w);
             }
             c0 = c0 + v.x;
@@ -1528,7 +1558,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
 #endif
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
-        (void)hipMemsetAsync(a.aocc, 0, (size_t)m.frame_samples * m.n_frames * sizeof(uint32_t), a.stream);
+        (void)hipMemsetAsync(a.aocc, 0, ((size_t)m.frame_samples * m.n_frames + 3) / 4 * sizeof(uint32_t), a.stream);
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
     // primary + shading + long rays; what did not fit the CU's rings goes to the global lists
     auto primary = [&](auto stats_tag) {

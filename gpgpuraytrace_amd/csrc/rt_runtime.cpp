@@ -514,7 +514,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->shrec, long_need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->aocc, need * sizeof(uint32_t)));
+    HIP_TRY(hipMalloc(&dev->aocc, (need + 3) / 4 * sizeof(uint32_t))); // a byte per sample (ao_count)
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * RT_MAX_BATCH * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->hitmask, need / 64 * sizeof(uint64_t)));
     dev->samples_cap = need;
