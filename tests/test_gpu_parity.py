@@ -324,6 +324,24 @@ def test_1080p_full_frame_rows_and_properties(pose):
     dev.destroy()
 
 
+@pytest.mark.parametrize("aa", [1, 4])
+def test_max_ao_bitexact(aa):
+    """RT_AO_SAMPLES=16, the most the AO extension takes: k_trace counts each sample's occluded AO
+    rays in one byte, four samples to a word (16 fits; neighbours' counts must not bleed), and
+    k_finish applies them -- bit-exact against the oracle's whole frame, one and four samples per
+    pixel (the look-down pose: most pixels hit, many AO rays occluded)."""
+    consts = GI.consts(64, 48, "lookdown")
+    fr = O.make_frame(consts, aa=aa, max_steps=128, ao=16)
+    ref = O.render(O.noise_tables(), fr)
+    dev, ter = make(consts, aa=aa, max_steps=128, ao=16, stats=True)
+    ter.render_device()
+    assert bits_equal(dev.readback_float(), ref["rgba32f"])
+    assert np.array_equal(dev.readback(), ref["rgba8"])
+    st = dev.stats()
+    assert st["ao_steps"] == ref["stats"]["ao_steps"] and st["hits"] == ref["stats"]["primary_hits"]
+    dev.destroy()
+
+
 # BASELINE.json GPU configs at their full sizes (configs[1], [2], [4]): the product path vs the
 # oracle on a row sample (rows r0::step; the oracle renders only those rows).  C3 is the
 # bench's headline workload, C5 the 4K / 1024-step / 4-AO one.
