@@ -182,6 +182,9 @@ def main():
     backend = os.environ.get("RT_DIST_BACKEND", "nccl")
     if os.environ.get("RT_BENCH_SAME_GPU") == "1":
         local = 0
+    if os.environ.get("RT_BENCH_WATCHDOG"):  # diagnostics: every rank's Python stack every N s on stderr
+        import faulthandler
+        faulthandler.dump_traceback_later(int(os.environ["RT_BENCH_WATCHDOG"]), repeat=True)
     if world > 1:
         dist.init_process_group(backend)
     torch.cuda.set_device(local)
@@ -363,12 +366,14 @@ def main():
     ring.kernel_time()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(n_full):
+    for i in range(n_full):
         E.render_batch([t for _, t in group0], rank if world > 1 else 0, world)
         for d, _ in group0:
             d.present()
+        progress(rank, f"roofline batch {i + 1}/{n_full} queued")
     for d, _ in group0:
         d.synchronize()
+    progress(rank, "roofline pass done")
     latency_ms = (time.perf_counter() - t1) / n_full * 1e3
     kms, kn = ring.kernel_time()
     ring.set_profiling(False)

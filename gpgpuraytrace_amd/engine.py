@@ -644,6 +644,8 @@ class FrameRing:
         return tot, n
 
     def destroy(self):
-        for dev, _ in self.slots:
+        # last slot first: a group's devices run on its first device's stream (set_stream), and
+        # rt_device_destroy synchronizes the stream a device uses, so the owner must go last
+        for dev, _ in reversed(self.slots):
             dev.destroy()
         self.slots = []

@@ -110,7 +110,9 @@ int rt_device_readback_bgrx(rt_device dev, void* dst, size_t row_pitch);
 int rt_device_size(rt_device dev, int* width, int* height);
 void* rt_device_framebuffer(rt_device dev);       /* device pointer, W*H uint32 RGBA8 */
 void* rt_device_stream(rt_device dev);            /* hipStream_t */
-int rt_device_set_stream(rt_device dev, void* hip_stream); /* NULL = the device's own stream */
+/* NULL = the device's own stream.  A borrowed stream (another device's, or the caller's) must
+ * outlive the device: rt_device_destroy synchronizes the stream its device uses. */
+int rt_device_set_stream(rt_device dev, void* hip_stream);
 int rt_device_stats(rt_device dev, rt_stats* out, int reset); /* needs RT_DEVICE_STATS */
 /* HIP-event timing of the dominant kernel (tracescreen) on the device stream:
  * enable, then rt_device_kernel_time returns the summed elapsed ms and launch count
