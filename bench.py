@@ -44,6 +44,8 @@ PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, =
 # BASELINE.json configs (GPU ones): resolution, primary step cap, AO rays per hit, and the
 # CPU baseline's row samples (all host cores: parity + value; one thread: single_thread)
 CONFIGS = {
+    "c1": {"width": 256, "height": 256, "max_steps": 64, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 1,
+           "name": "C1: 256x256, 64-step primary + shadow (the reference's CPU-scale plumbing case)"},
     "c2": {"width": 1280, "height": 720, "max_steps": 256, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 8,
            "name": "C2: 1280x720, 256-step primary + 1 shadow ray"},
     "c3": {"width": 1920, "height": 1080, "max_steps": 512, "ao": 1, "cpu_rows": 1, "cpu_rows_1t": 16,

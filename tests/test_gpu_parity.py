@@ -346,6 +346,7 @@ def test_max_ao_bitexact(aa):
 # oracle on a row sample (rows r0::step; the oracle renders only those rows).  C3 is the
 # bench's headline workload, C5 the 4K / 1024-step / 4-AO one.
 BASELINE_CONFIGS = {  # name: (W, H, max_steps, ao, row_step)
+    "c1": (256, 256, 64, 0, 1),
     "c2": (1280, 720, 256, 0, 8),
     "c3": (1920, 1080, 512, 1, 8),
     "c5": (3840, 2160, 1024, 4, 36),
