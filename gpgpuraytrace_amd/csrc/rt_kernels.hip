@@ -439,7 +439,10 @@ constexpr uint32_t kShadowRec = 3;
 
 // Lanes idle before a long-ray wave refills them: amortises the refill's divergent
 // prologue against the idle lanes it leaves.
-constexpr uint32_t kRefillIdle = 4;
+#ifndef RT_REFILL_IDLE // A/B: make variant FLAGS=-DRT_REFILL_IDLE=n
+#define RT_REFILL_IDLE 4
+#endif
+constexpr uint32_t kRefillIdle = RT_REFILL_IDLE;
 
 // color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
 __device__ __forceinline__ float4 shade_finish(const RtConsts* k, float4 cb, float4 fog, float4 ray,
@@ -891,8 +894,14 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 // ring spills to the global lists, which k_shade_pre / k_shadow drain afterwards.
 constexpr uint32_t kHitRing = 512;
 constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
-constexpr uint32_t kLongBatch = 128; // queued long rays that make a wave switch to them
-constexpr uint32_t kCompactLive = 56; // live lanes below which a dry wave hands its rays back
+#ifndef RT_LONG_BATCH // A/B: make variant FLAGS=-DRT_LONG_BATCH=n
+#define RT_LONG_BATCH 128
+#endif
+constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a wave switch to them
+#ifndef RT_COMPACT_LIVE // A/B: make variant FLAGS=-DRT_COMPACT_LIVE=n
+#define RT_COMPACT_LIVE 56
+#endif
+constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
 
 struct TraceQueues {
     uint32_t lock;
