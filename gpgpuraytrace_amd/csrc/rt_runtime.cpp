@@ -479,10 +479,10 @@ int check_texture(Shader* s)
 }
 
 // Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded
-// colour (16 B), one primary RayResult (48 B; 20 B used without fog), one hit-list slot (4 B),
-// the shading inputs of a long shadow ray (48 B; 32 B used without fog), an AO occlusion count
-// (4 B) and a hit bit (the 64-lane ballot per 8x8 unit and AA sample); the
-// global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
+// colour (16 B; 12 B used with one sample per pixel), one primary RayResult (48 B; 12 B used
+// without fog), one hit-list slot (4 B), the shading inputs of a long shadow ray (48 B; 32 B used
+// without fog), an AO occlusion count (1 B) and a hit bit (the 64-lane ballot per 8x8 unit and
+// AA sample); the global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
 // (48 B each).
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
