@@ -968,7 +968,10 @@ __device__ __forceinline__ void march_shfl(March<L, CF>& d, const March<L, CF>& 
     d.step = f(s.step);
     d.lastStep = f(s.lastStep);
     d.d = f(s.d);
-    d.f = {f(s.f.x), f(s.f.y), f(s.f.z), f(s.f.w)};
+    // without fog f is +0 throughout the march (march_step): restate it, so that the tail's
+    // shuffles do not make it a live value of the march loops
+    if constexpr (March<L, CF>::FOG) d.f = {f(s.f.x), f(s.f.y), f(s.f.z), f(s.f.w)};
+    else d.f = {0.0f, 0.0f, 0.0f, 0.0f};
     d.iters = __shfl(s.iters, (int)src, 64);
     d.fog = __shfl(s.fog ? 1 : 0, (int)src, 64) != 0;
 }
