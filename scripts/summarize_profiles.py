@@ -116,6 +116,9 @@ def main(src, dst):
                "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
                "kernels": "tracescreen launch: k_order + k_trace + k_shade_pre + k_shadow + k_finish (uninstrumented)",
                "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"}
+    if fetch == 0.0 and write == 0.0:  # a kernel-trace-only profile (PMC=0): no traffic to record
+        print(open(os.path.join(dst, "kernels.md")).read())
+        return
     tpath = os.path.join(dst, "traffic.json")
     old = json.load(open(tpath)) if os.path.exists(tpath) else {}
     old.update(tr)  # other configs' launches (traffic_summary.py merges) stay
