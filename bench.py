@@ -307,15 +307,19 @@ def main():
         def render(self):
             E.render_batch(self.ters, rank if world > 1 else 0, world)
 
-        def pack(self, f, shard, off):
-            E.shard_pack(self.devs[f], shard, world, self.b["packed"].data_ptr() + off)
+        def pack_batch(self, items):
+            base = self.b["packed"].data_ptr()
+            E.shard_pack_batch([self.devs[f] for f, _, _ in items], [s for _, s, _ in items], world,
+                               [base + off for _, _, off in items])
 
         def gather(self):
             with torch.cuda.stream(self.b["stream"]):
                 coll.gather(self.b["packed"], self.b["gathered"])
 
-        def unpack(self, src, f, shard, off):
-            E.shard_unpack(self.devs[f], shard, world, self.b["gathered"][src].data_ptr() + off)
+        def unpack_batch(self, items):
+            g = self.b["gathered"]
+            E.shard_unpack_batch([self.devs[f] for _, f, _, _ in items], [s for _, _, s, _ in items], world,
+                                 [g[src].data_ptr() + off for src, _, _, off in items])
 
         def present(self):
             for d in self.devs:

@@ -90,6 +90,8 @@ SIGNATURES = {
     "rt_shard_bytes": (_sz, [_vp, _i, _i]),
     "rt_shard_pack": (_i, [_vp, _i, _i, _vp]),
     "rt_shard_unpack": (_i, [_vp, _i, _i, _vp]),
+    "rt_shard_pack_batch": (_i, [C.POINTER(_vp), C.POINTER(_i), _i, C.POINTER(_vp), _i]),
+    "rt_shard_unpack_batch": (_i, [C.POINTER(_vp), C.POINTER(_i), _i, C.POINTER(_vp), _i]),
     "rt_noise_generate": (_i, [C.c_uint32, _i, _vp, _vp]),
     "rt_terrain_set_target_depths": (_i, [_vp, _vp]),
     "rt_recorder_create": (_i, [_vp, _i, _i, _cp, C.POINTER(_vp)]),

@@ -73,10 +73,17 @@ inline size_t rt_shard_tiles(int w, int h, int rank, int count)
     size_t tx = (size_t)(w + RT_TILE - 1) / RT_TILE, ty = (size_t)(h + RT_TILE - 1) / RT_TILE, total = tx * ty;
     return total > (size_t)rank ? (total - (size_t)rank + (size_t)count - 1) / (size_t)count : 0;
 }
-// pack != 0: framebuffer tiles of shard `rank` -> packed (1024 px per tile); else packed -> framebuffer.
 // RGBA8 framebuffer -> BGRX rows (RecorderWinAPI::write's swizzle), dst pitch in uint32 words
 void rt_launch_bgrx(hipStream_t s, const uint32_t* fb, uint32_t* dst, int w, int h, int pitch_words);
-void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack);
+// Shard transport jobs of one launch (a kernel argument: 2.5 KiB): job j copies shard shard[j]
+// of the w x h framebuffer fb[j] to packed[j] (pack != 0: 1024 px per tile, tiles ascending) or back.
+#define RT_SHARD_JOBS 128
+struct ShardJobs {
+    uint32_t* fb[RT_SHARD_JOBS];
+    uint32_t* packed[RT_SHARD_JOBS];
+    int shard[RT_SHARD_JOBS];
+};
+void rt_launch_shard_copy(hipStream_t s, const ShardJobs& jobs, int n, int w, int h, int count, int pack);
 
 // diagnostics (primitive-level parity tests)
 void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n);

@@ -1469,19 +1469,32 @@ __global__ void __launch_bounds__(256) k_bgrx(const uint32_t* __restrict__ fb, u
     }
 }
 
-__global__ void __launch_bounds__(256) k_shard_copy(uint32_t* __restrict__ fb, uint32_t* __restrict__ packed, int w,
-                                                    int h, int rank, int count, int pack)
+// Shard transport: job blockIdx.y copies tile blockIdx.x of its shard (tile blockIdx.x * count +
+// shard, row-major) between its framebuffer and its packed buffer (1024 RGBA8 pixels per tile,
+// row-major in the tile).  Thread t moves pixels 4 (t & 7) .. +3 of tile row t >> 3: one 16-byte
+// access each way when the row segment lies inside the frame and both pointers allow it.  Pixels
+// outside the frame are neither read nor written.  A batch's pack or unpack (rank 0 unpacks
+// (N-1) x B shards per batch) is one launch instead of one per frame and rank: those small
+// launches queue behind the other batch's persistent k_trace and each costs a dispatch.
+__global__ void __launch_bounds__(256) k_shard_copy(ShardJobs jobs, int w, int h, int count, int pack)
 {
-    int tiles_x = (w + 31) / 32;
-    int kk = blockIdx.x;
-    int tile = kk * count + rank;
-    int tx0 = (tile % tiles_x) * 32, ty0 = (tile / tiles_x) * 32;
-    for (int i = threadIdx.x; i < 1024; i += 256) {
-        int x = tx0 + (i & 31), y = ty0 + (i >> 5);
-        if (x >= w || y >= h) continue;
-        size_t f = (size_t)y * w + x, p = (size_t)kk * 1024 + i;
-        if (pack) packed[p] = fb[f];
-        else fb[f] = packed[p];
+    const int job = blockIdx.y;
+    const int tiles_x = (w + 31) / 32, total = tiles_x * ((h + 31) / 32);
+    const int tile = (int)blockIdx.x * count + jobs.shard[job];
+    if (tile >= total) return; // a shard smaller than the grid (ragged shards)
+    const int r = (int)threadIdx.x >> 3, c = ((int)threadIdx.x & 7) * 4;
+    const int x = (tile % tiles_x) * 32 + c, y = (tile / tiles_x) * 32 + r;
+    if (y >= h || x >= w) return;
+    uint32_t* fb = jobs.fb[job] + (size_t)y * w + x;
+    uint32_t* pk = jobs.packed[job] + (size_t)blockIdx.x * 1024 + r * 32 + c;
+    if (x + 3 < w && (((uintptr_t)fb | (uintptr_t)pk) & 15u) == 0) {
+        if (pack) *reinterpret_cast<uint4*>(pk) = *reinterpret_cast<const uint4*>(fb);
+        else *reinterpret_cast<uint4*>(fb) = *reinterpret_cast<const uint4*>(pk);
+    } else {
+        for (int i = 0; i < 4 && x + i < w; ++i) {
+            if (pack) pk[i] = fb[i];
+            else fb[i] = pk[i];
+        }
     }
 }
 
@@ -1653,11 +1666,13 @@ void rt_launch_bgrx(hipStream_t s, const uint32_t* fb, uint32_t* dst, int w, int
     hipLaunchKernelGGL(k_bgrx, dim3(bx, h), dim3(256), 0, s, fb, dst, w, h, pitch_words);
 }
 
-void rt_launch_shard_copy(hipStream_t s, uint32_t* fb, uint32_t* packed, int w, int h, int rank, int count, int pack)
+void rt_launch_shard_copy(hipStream_t s, const ShardJobs& jobs, int n, int w, int h, int count, int pack)
 {
-    size_t n = rt_shard_tiles(w, h, rank, count);
-    if (n == 0) return;
-    hipLaunchKernelGGL(k_shard_copy, dim3((unsigned)n), dim3(256), 0, s, fb, packed, w, h, rank, count, pack);
+    if (n <= 0 || n > RT_SHARD_JOBS) return;
+    // shard 0 holds the most tiles: its count is the grid's x extent
+    const size_t tiles = rt_shard_tiles(w, h, 0, count);
+    if (tiles == 0) return;
+    hipLaunchKernelGGL(k_shard_copy, dim3((unsigned)tiles, (unsigned)n), dim3(256), 0, s, jobs, w, h, count, pack);
 }
 
 // ---------------------------------------------------------------------------

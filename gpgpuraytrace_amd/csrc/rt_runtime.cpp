@@ -1329,20 +1329,69 @@ size_t rt_shard_bytes(rt_device d, int rank, int count)
     return tiles * RT_TILE * RT_TILE * 4;
 }
 
+// n (device, shard, buffer) jobs in launches of up to RT_SHARD_JOBS on devs[0]'s stream; devices on
+// other streams are ordered around them with events (their earlier work first, their later work after)
+static int shard_copy(const rt_device* devs, const int* shards, int count, void* const* bufs, int n, int pack)
+{
+    if (!devs || !shards || !bufs || n < 0 || count < 1) return fail(RT_ERR_INVALID, "bad arguments");
+    if (n == 0) return RT_OK;
+    rt_device d0 = devs[0];
+    for (int i = 0; i < n; ++i) {
+        if (!devs[i] || !bufs[i] || shards[i] < 0 || shards[i] >= count) return fail(RT_ERR_INVALID, "bad arguments");
+        if (devs[i]->width != d0->width || devs[i]->height != d0->height)
+            return fail(RT_ERR_INVALID, "shard batch: devices differ in size");
+    }
+    auto order = [&](rt_device from, rt_device to) -> int {
+        if (!from->sync_ev) HIP_TRY(hipEventCreateWithFlags(&from->sync_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(from->sync_ev, from->stream));
+        HIP_TRY(hipStreamWaitEvent(to->stream, from->sync_ev, 0));
+        return RT_OK;
+    };
+    int rc;
+    for (int i = 1; i < n; ++i)
+        if (devs[i]->stream != d0->stream && (rc = order(devs[i], d0))) return rc;
+    ShardJobs jobs;
+    for (int b = 0; b < n; b += RT_SHARD_JOBS) {
+        const int m = n - b < RT_SHARD_JOBS ? n - b : RT_SHARD_JOBS;
+        for (int j = 0; j < m; ++j) {
+            jobs.fb[j] = devs[b + j]->fb8;
+            jobs.packed[j] = (uint32_t*)bufs[b + j];
+            jobs.shard[j] = shards[b + j];
+        }
+        rt_launch_shard_copy(d0->stream, jobs, m, d0->width, d0->height, count, pack);
+    }
+    HIP_TRY(hipGetLastError());
+    bool others = false;
+    for (int i = 1; i < n; ++i) others |= devs[i]->stream != d0->stream;
+    if (others) {
+        if (!d0->sync_ev) HIP_TRY(hipEventCreateWithFlags(&d0->sync_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(d0->sync_ev, d0->stream));
+        for (int i = 1; i < n; ++i)
+            if (devs[i]->stream != d0->stream) HIP_TRY(hipStreamWaitEvent(devs[i]->stream, d0->sync_ev, 0));
+    }
+    return RT_OK;
+}
+
 int rt_shard_pack(rt_device d, int rank, int count, void* dst)
 {
-    if (!d || !dst || count < 1 || rank < 0 || rank >= count) return fail(RT_ERR_INVALID, "bad arguments");
-    rt_launch_shard_copy(d->stream, d->fb8, (uint32_t*)dst, d->width, d->height, rank, count, 1);
-    HIP_TRY(hipGetLastError());
-    return RT_OK;
+    return shard_copy(&d, &rank, count, &dst, 1, 1);
 }
 
 int rt_shard_unpack(rt_device d, int rank, int count, const void* src)
 {
-    if (!d || !src || count < 1 || rank < 0 || rank >= count) return fail(RT_ERR_INVALID, "bad arguments");
-    rt_launch_shard_copy(d->stream, d->fb8, (uint32_t*)src, d->width, d->height, rank, count, 0);
-    HIP_TRY(hipGetLastError());
-    return RT_OK;
+    void* p = const_cast<void*>(src);
+    return shard_copy(&d, &rank, count, &p, 1, 0);
+}
+
+int rt_shard_pack_batch(const rt_device* devs, const int* shard_ranks, int shard_count, void* const* dst_device, int n)
+{
+    return shard_copy(devs, shard_ranks, shard_count, dst_device, n, 1);
+}
+
+int rt_shard_unpack_batch(const rt_device* devs, const int* shard_ranks, int shard_count,
+                          const void* const* src_device, int n)
+{
+    return shard_copy(devs, shard_ranks, shard_count, const_cast<void* const*>(src_device), n, 0);
 }
 
 int rt_noise_generate(uint32_t seed, int rand_kind, uint8_t* perm2d, float* grad)

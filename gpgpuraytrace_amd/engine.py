@@ -556,6 +556,28 @@ def shard_unpack(device, rank, count, src_ptr):
     check(lib().rt_shard_unpack(device._h, rank, count, src_ptr), "shard_unpack")
 
 
+def _shard_batch(fn, what, devices, shards, count, ptrs):
+    n = len(devices)
+    if not (n == len(shards) == len(ptrs)):
+        raise ValueError(f"{what}: devices, shards and buffers differ in length")
+    if n == 0:
+        return
+    hs = (C.c_void_p * n)(*[d._h for d in devices])
+    ss = (C.c_int * n)(*[int(s) for s in shards])
+    ps = (C.c_void_p * n)(*[int(p) for p in ptrs])
+    check(fn(hs, ss, count, ps, n), what)
+
+
+def shard_pack_batch(devices, shards, count, dst_ptrs):
+    """rt_shard_pack_batch: device i's shard shards[i] -> dst_ptrs[i], one launch on devices[0]'s stream."""
+    _shard_batch(lib().rt_shard_pack_batch, "shard_pack_batch", devices, shards, count, dst_ptrs)
+
+
+def shard_unpack_batch(devices, shards, count, src_ptrs):
+    """rt_shard_unpack_batch: src_ptrs[i] -> device i's shard shards[i], one launch on devices[0]'s stream."""
+    _shard_batch(lib().rt_shard_unpack_batch, "shard_unpack_batch", devices, shards, count, src_ptrs)
+
+
 class FrameRing:
     """Frames in flight: `depth` complete frame contexts (Device + Terrain: own constants,
     CameraResults/CellDistance, ray buffers and framebuffer), each on its own non-blocking HIP

@@ -19,9 +19,9 @@ tests/test_dist.py with host ops (numpy, gloo), so the CPU tests exercise the sa
      rays.  Unsplit: every rank runs every frame's prepass.
   2. trace: each rank traces its shard of every frame (setTargetDepths + tracescreen).
   3. pack: frame f's shard (r + f) % N goes to packed[f * max_bytes : ...] (k_shard_copy;
-     1024 RGBA8 pixels per tile, tiles in ascending order).
+     1024 RGBA8 pixels per tile, tiles in ascending order), the batch's frames in one launch.
   4. ONE gather of the packed buffers to rank 0, which unpacks rank src's frame f as shard
-     (src + f) % N from gathered[src][f * max_bytes : ...].
+     (src + f) % N from gathered[src][f * max_bytes : ...], all (N-1) x B in one launch.
 
 The tile mapping is the one the HIP kernels use (rt_kernels.h rt_shard_tiles, k_shard_copy).
 """
@@ -140,8 +140,10 @@ class BatchPlan:
 def run_batch(plan, rank, ops, frames=None):
     """One batch on this rank.  `ops` supplies the actions (bench.py: HIP + RCCL; tests: numpy
     + gloo): prepass(first, count), all_gather_cameras(), trace(), render() (prepass + trace of
-    every frame, the unsplit path), pack(f, shard, offset), gather(), unpack(src, f, shard,
-    offset), present().  `frames` < plan.batch renders a partial batch (its first frames)."""
+    every frame, the unsplit path), pack_batch([(f, shard, offset)]) (this rank's frames; one
+    rt_shard_pack_batch launch on the GPU), gather(), unpack_batch([(src, f, shard, offset)])
+    (rank 0: every other rank's frames in one rt_shard_unpack_batch launch), present().
+    `frames` < plan.batch renders a partial batch (its first frames)."""
     n = plan.batch if frames is None else int(frames)
     if plan.split_prepass:
         first, count = plan.prepass_range(rank)
@@ -152,12 +154,10 @@ def run_batch(plan, rank, ops, frames=None):
     else:
         ops.render()
     if plan.world > 1:
-        for f, shard, off in plan.packs(rank, n):
-            ops.pack(f, shard, off)
+        ops.pack_batch(plan.packs(rank, n))
         ops.gather()
         if rank == 0:
-            for src, f, shard, off in plan.unpacks(n):
-                ops.unpack(src, f, shard, off)
+            ops.unpack_batch(plan.unpacks(n))
     ops.present()
 
 

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 enum {
     RT_OK = 0,
@@ -214,6 +214,15 @@ int rt_terrain_trace_batch(const rt_compute* camera_cs, const rt_compute* screen
 size_t rt_shard_bytes(rt_device dev, int shard_rank, int shard_count);
 int rt_shard_pack(rt_device dev, int shard_rank, int shard_count, void* dst_device);
 int rt_shard_unpack(rt_device dev, int shard_rank, int shard_count, const void* src_device);
+/* The same for n frames in one launch (ABI 3): job i packs shard shard_ranks[i] of devs[i]'s
+ * framebuffer into dst_device[i] (or unpacks src_device[i] into it).  Every device has the same
+ * size; the launch runs on devs[0]'s stream, and devices on other streams are ordered around it
+ * (their earlier work before, their later work after).  A batch's root unpacks its (N-1) x B
+ * shards with one call (parallel.run_batch) instead of one launch each. */
+int rt_shard_pack_batch(const rt_device* devs, const int* shard_ranks, int shard_count, void* const* dst_device,
+                        int n);
+int rt_shard_unpack_batch(const rt_device* devs, const int* shard_ranks, int shard_count,
+                          const void* const* src_device, int n);
 
 /* ---- host helpers (Noise.cpp:39-94, Camera.cpp, Terrain.cpp:285-311) ----
  * rt_noise_generate: the engine's noise tables; rand_kind 0 = MSVC CRT rand (the

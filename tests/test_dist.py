@@ -135,6 +135,11 @@ class HostOps:
         pk = P.pack_host(self.frames[f], shard, self.p.world).view(np.int32)
         self.packed[off // 4:off // 4 + pk.size] = torch.from_numpy(pk.copy())
 
+    def pack_batch(self, items):
+        self.log.append(("pack_batch", len(items)))
+        for f, shard, off in items:
+            self.pack(f, shard, off)
+
     def gather(self):
         self.coll.gather(self.packed, self.gathered)
 
@@ -143,6 +148,11 @@ class HostOps:
         n = P.shard_bytes(self.w, self.h, shard, self.p.world) // 4
         buf = self.gathered[src].numpy().view(np.uint32)[off // 4:off // 4 + n]
         P.unpack_host(self.frames[f], buf, shard, self.p.world)
+
+    def unpack_batch(self, items):
+        self.log.append(("unpack_batch", len(items)))
+        for src, f, shard, off in items:
+            self.unpack(src, f, shard, off)
 
     def present(self):
         self.log.append(("present",))
@@ -200,6 +210,8 @@ def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
         assert log[0] == ("prepass", 0, min(plan.chunk, frames)) and ("trace",) in log
     else:
         assert log[0] == ("render",)
+    # rank 0: one pack of its frames, one unpack of every other rank's (one launch each on the GPU)
+    assert ("pack_batch", frames) in log and ("unpack_batch", (world - 1) * frames) in log
 
 
 def test_batch_plan_bookkeeping():

@@ -423,6 +423,56 @@ def test_shards_assemble_to_full_frame(world):
     full_dev.destroy()
 
 
+@pytest.mark.parametrize("w,h,world,frames", [(1920, 1080, 8, 12), (50, 36, 3, 5), (64, 48, 3, 4)])
+def test_shard_batch_pack_unpack_roundtrip(w, h, world, frames):
+    """rt_shard_pack_batch / rt_shard_unpack_batch (one launch for a batch's frames, devices on
+    separate streams) against the host tile mapping (parallel.pack_host): random framebuffers
+    are packed with frame f's rotated shard (f % N) into offsets of one buffer, which must hold
+    exactly pack_host's tiles; unpacked into fresh devices, every shard's pixels come back and no
+    other pixel is touched.  1920x1080 takes the 16-byte path (its last tile row is partial),
+    50x36 the per-pixel one (W % 4 != 0), 64x48 ragged shards of 2/1/1 tiles."""
+    import torch
+
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    rng = np.random.default_rng(11)
+    devs = [G.DeviceFactory.construct(G.DeviceAPI.HIP, w, h) for _ in range(frames)]
+    imgs = [rng.integers(0, 2**32, (h, w), dtype=np.uint32) for _ in range(frames)]
+    # fill each framebuffer through the single-job unpack of every shard from host-packed tiles
+    for d, img in zip(devs, imgs):
+        for s in range(world):
+            src = torch.from_numpy(P.pack_host(img, s, world).view(np.int32)).to("cuda:0")
+            if src.numel():
+                E.shard_unpack(d, s, world, src.data_ptr())
+        d.synchronize()
+        assert np.array_equal(d.readback().view(np.uint32).reshape(h, w), img)
+    plan = P.BatchPlan(w, h, frames, world)
+    packed = torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0")
+    items = [(f, f % world, plan.pack_offset(f)) for f in range(frames)]
+    E.shard_pack_batch([devs[f] for f, _, _ in items], [s for _, s, _ in items], world,
+                       [packed.data_ptr() + off for _, _, off in items])
+    devs[0].synchronize()
+    got = packed.cpu().numpy().view(np.uint32)
+    for f, s, off in items:
+        want = P.pack_host(imgs[f], s, world)
+        inside = P.pack_host(np.ones((h, w), np.uint32), s, world) == 1  # pixels of the frame
+        part = got[off // 4:off // 4 + want.size]
+        assert np.array_equal(part[inside], want[inside]), (f, s)
+        assert not part[~inside].any(), (f, s)  # padding pixels of partial tiles are not written
+    fresh = [G.DeviceFactory.construct(G.DeviceAPI.HIP, w, h) for _ in range(frames)]
+    E.shard_unpack_batch([fresh[f] for f, _, _ in items], [s for _, s, _ in items], world,
+                         [packed.data_ptr() + off for _, _, off in items])
+    for f, s, _ in items:
+        img = fresh[f].readback().view(np.uint32).reshape(h, w)
+        mine = P.unpack_host(np.zeros((h, w), np.uint32), P.pack_host(imgs[f], s, world), s, world)
+        assert np.array_equal(img, mine), (f, s)
+    with pytest.raises(Exception):
+        E.shard_pack_batch([devs[0]], [world], world, [packed.data_ptr()])  # shard out of range
+    for d in devs + fresh:
+        d.destroy()
+
+
 @pytest.mark.parametrize("land", ["nomadplains", "greenrocks"])
 def test_recording_macro_bitexact(land):
     consts = GI.consts(48, 32, "reset")
@@ -689,12 +739,14 @@ def test_batch_ragged_rotated_shards_bitexact(w, h, world, split):
             E.trace_batch(ters, r, world, cams.data_ptr())
         else:
             E.render_batch(ters, r, world)
-        for f, shard, off in plan.packs(r):
-            E.shard_pack(frames[f][0], shard, world, packed[r].data_ptr() + off)
+        items = plan.packs(r)  # one rt_shard_pack_batch launch, as bench.py's run_batch does
+        E.shard_pack_batch([frames[f][0] for f, _, _ in items], [s for _, s, _ in items], world,
+                           [packed[r].data_ptr() + off for _, _, off in items])
         for d, _ in frames:
             d.synchronize()
-    for src, f, shard, off in plan.unpacks():
-        E.shard_unpack(ranks[0][f][0], shard, world, packed[src].data_ptr() + off)
+    items = plan.unpacks()
+    E.shard_unpack_batch([ranks[0][f][0] for _, f, _, _ in items], [s for _, _, s, _ in items], world,
+                         [packed[src].data_ptr() + off for src, _, _, off in items])
     for (d, _), s in zip(ranks[0], specs):
         assert np.array_equal(d.readback(), want[s[1]]), s
     for frames in ranks:

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes binding covers the whole header
     assert set(names) <= set(_native.SIGNATURES), set(names) - set(_native.SIGNATURES)
-    assert L.rt_abi_version() == 2
+    assert L.rt_abi_version() == 3
 
 
 def test_product_loads_only_in_tree_library():
