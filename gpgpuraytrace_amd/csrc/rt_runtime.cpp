@@ -1226,13 +1226,14 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     // an empty range is valid anywhere: a rank past the last frame of a split prepass (B < N * chunk)
     if (count > n || (count > 0 && (first < 0 || first > n - count))) return fail(RT_ERR_INVALID, "bad prepass frame range");
     const bool graphs = (dev->flags & RT_DEVICE_GRAPH) && dev->stream != nullptr && phases == (PH_PRE | PH_TRACE);
+    // gathered prepass results: the table reads them, and each frame's CameraResults array
+    // receives its copy (Terrain::getCameraView stays valid) once the trace is queued, so the
+    // copies do not delay it
+    float4* cam_copy[RT_MAX_BATCH] = {};
     if (camera_in) {
-        // gathered prepass results: the table reads them, and each frame's CameraResults
-        // array receives its copy (Terrain::getCameraView stays valid)
         for (int f = 0; f < n; ++f) {
             const float4* src = camera_in + (size_t)f * 1024;
-            if (ft.cam[f] != scrs[f]->dev->scratch_cam)
-                HIP_TRY(hipMemcpyAsync(ft.cam[f], src, 1024 * sizeof(float4), hipMemcpyDeviceToDevice, dev->stream));
+            if (ft.cam[f] != scrs[f]->dev->scratch_cam) cam_copy[f] = ft.cam[f];
             ft.cam[f] = const_cast<float4*>(src);
         }
     }
@@ -1300,6 +1301,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             trace();
         }
     }
+    for (int f = 0; f < n; ++f)
+        if (cam_copy[f])
+            HIP_TRY(hipMemcpyAsync(cam_copy[f], camera_in + (size_t)f * 1024, 1024 * sizeof(float4),
+                                   hipMemcpyDeviceToDevice, dev->stream));
     return batch_end(scrs, n, b);
 }
 
