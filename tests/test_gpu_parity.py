@@ -380,6 +380,24 @@ def test_baseline_config_rows_bitexact(name, pose):
     dev.destroy()
 
 
+@pytest.mark.parametrize("land,ao", [("testing", 0), ("simple", 1), ("greenrocks", 1)])
+def test_other_landscapes_720p_rows_bitexact(land, ao):
+    """The other live landscapes (analytic testing, simple, greenrocks with its fog live) at the
+    C2 size and step cap, with and without AO, through rt_terrain_render: float32 colour and
+    UNORM8 bit-exact against the oracle on every 24th row, CellDistance exact."""
+    w, h, ms, step = 1280, 720, 256, 24
+    consts = _consts_1080p_like(w, h, "reset")
+    fr = O.make_frame(consts, landscape=O.LANDSCAPES[land], max_steps=ms, ao=ao, rows=(7, h, step))
+    ref, ref8, _, cd, _ = O.render_rows(O.noise_tables(), fr)
+    rows = slice(7, h, step)
+    dev, ter = make(consts, land=land, max_steps=ms, ao=ao)
+    ter.render_device()
+    assert bits_equal(dev.readback_float()[rows], ref[rows])
+    assert np.array_equal(dev.readback()[rows], ref8[rows])
+    assert np.array_equal(_device_cells(ter), cd)
+    dev.destroy()
+
+
 @pytest.mark.parametrize("name", ["c2", "c3"])
 def test_baseline_config_batch_rows_bitexact(name):
     """The bench's entry point: one rt_terrain_render_batch of 4 frames (reset, look-down,
