@@ -7,10 +7,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# RT_LIB_VARIANT=<name> loads an experiment build _build/librt_hip_<name>.so instead (make trace:
-# k_trace's wave timeline; make variant NAME=<name> FLAGS=...: A/B builds of compile-time switches)
-_VARIANT = os.environ.get("RT_LIB_VARIANT", "")
-LIB_PATH = os.path.join(HERE, "_build", f"librt_hip_{_VARIANT}.so" if _VARIANT else "librt_hip.so")
+# the product loads this library only (experiment builds are selected by scripts/with_variant.py,
+# outside the package, before the first lib() call)
+LIB_PATH = os.path.join(HERE, "_build", "librt_hip.so")
 ROOT = os.path.dirname(HERE)
 HEADER = os.path.join(ROOT, "include", "frosttrace.h")
 
@@ -18,8 +17,9 @@ RT_OK = 0
 RT_DEVICE_FLOAT_OUTPUT = 1
 RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
-RT_DEVICE_SEG_TAIL_OFF = 8
-RT_DEVICE_SEG_TAIL_ON = 16
+RT_DEVICE_SEG_TAIL_OFF = 8  # reserved since ABI 4 (no effect)
+RT_DEVICE_SEG_TAIL_ON = 16  # reserved since ABI 4 (no effect)
+ABI_VERSION = 4  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -56,6 +56,8 @@ SIGNATURES = {
     "rt_device_stream": (_vp, [_vp]),
     "rt_device_set_stream": (_i, [_vp, _vp]),
     "rt_device_stats": (_i, [_vp, C.POINTER(RtStats), _i]),
+    "rt_device_stats_sized": (_i, [_vp, C.POINTER(RtStats), _sz, _i]),
+    "rt_stream_refs": (_i, [_vp]),
     "rt_device_set_profiling": (_i, [_vp, _i]),
     "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
@@ -123,6 +125,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        if L.rt_abi_version() < ABI_VERSION:  # an older library: its structs are shorter than ours
+            raise ImportError(f"gpgpuraytrace_amd: {LIB_PATH} has ABI {L.rt_abi_version()}, this binding "
+                              f"needs >= {ABI_VERSION}; rebuild it (make -C gpgpuraytrace_amd/csrc)")
         _lib = L
     return _lib
 

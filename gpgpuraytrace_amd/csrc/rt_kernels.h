@@ -32,7 +32,6 @@ struct RtLaunch {
     RtStats* stats;           // nullptr = uninstrumented kernels
     uint32_t* queue;          // RT_CTR_BYTES of device work counters
     int num_cus;              // compute units (persistent grid size)
-    int seg_mode;             // k_trace segment tail: -1 auto, 0 off, 1 on (RT_DEVICE_SEG_TAIL_*)
     // per-sample buffers, rt_split_samples() entries per frame (sample t, see rt_kernels.hip)
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
     float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)

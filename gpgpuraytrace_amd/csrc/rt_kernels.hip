@@ -28,13 +28,12 @@ namespace {
 
 // LDS image (rts::NoiseView): perm2D texels at offset 0 (64 KiB), the paired lane-private
 // gradients gxy at kLdsGxy (32 KiB) and gz at kLdsGz (32 KiB, 8 of every 16 B used), then the
-// octave constants (NoiseView::oct / colt): nomadplains FBM (S, 0.35 S, 1/S, 0) for
-// N = 0..RT_NP_OCTAVES + 2 and colour FBM (S, 1/S) for N = 0..RT_COL_OCTAVES + 2 (the entries past
-// the last octave are padding).  A kernel declares it as its ONLY static LDS array, so it sits
+// nomadplains FBM octave constants (NoiseView::oct): (S, 0.35 S, 1/S, 0) for N = 0..RT_NP_OCTAVES + 2
+// (the entries past the last octave are padding).  A kernel declares it as its ONLY static LDS array, so it sits
 // at LDS address 0 and the texel address needs no base (other LDS a kernel needs is carved after it).
 constexpr int kPermWords = 128 * 128;
-constexpr int kNpOct = RT_NP_OCTAVES + 3, kColOct = RT_COL_OCTAVES + 3;
-constexpr int kOctWords = (kNpOct * 4 + kColOct * 2 + 3) / 4 * 4;
+constexpr int kNpOct = RT_NP_OCTAVES + 3;
+constexpr int kOctWords = kNpOct * 4;
 constexpr int kOctBase = (int)kLdsGz / 4 + (int)(kLdsGz - kLdsGxy) / 4; // words
 constexpr int kNoiseLdsWords = kOctBase + kOctWords;
 static_assert(kNoiseLdsWords % 4 == 0, "LDS carved after the noise image stays 16-byte aligned");
@@ -45,15 +44,10 @@ __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __
 {
     {
         float4* oct = reinterpret_cast<float4*>(lds + kOctBase);
-        float2* colt = reinterpret_cast<float2*>(oct + kNpOct);
         const int i = threadIdx.x;
         if (i < kNpOct) {
             const int n = i <= RT_NP_OCTAVES ? i : RT_NP_OCTAVES;
             oct[i] = make_float4(k->np_scale[n], k->np_scale_y[n], k->np_rcp[n], 0.0f);
-        }
-        if (i < kColOct) {
-            const int n = i <= RT_COL_OCTAVES ? i : RT_COL_OCTAVES;
-            colt[i] = make_float2(k->col_scale[n], k->col_rcp[n]);
         }
     }
     float4* gxy = reinterpret_cast<float4*>(lds + kLdsGxy / 4);
@@ -89,7 +83,6 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     Ctx c;
     c.nz.img = reinterpret_cast<const char*>(lds);
     c.nz.oct = reinterpret_cast<const float4*>(lds + kOctBase);
-    c.nz.colt = reinterpret_cast<const float2*>(c.nz.oct + kNpOct);
     c.nz.so16 = kLdsGxy | ((threadIdx.x & 15u) * 16u);
     c.nz.calls = 0;
     c.nz.phase = RT_PHASE_OTHER;
@@ -940,117 +933,6 @@ __device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
     if (lane == 0) atomicExch(lock, 0u);
 }
 
-// ---------------------------------------------------------------------------
-// Octave-parallel tail (nomadplains).  A wave left with a few live rays would march them
-// on a few of its 64 lanes, one full FBM per lane per step, its LDS latency exposed: the
-// frame's last rays then set its length (and, on N GPUs, every rank's).  seg_finish
-// instead re-packs the live rays into segments of LPR lanes (16 rays x 4 lanes, 8 x 8,
-// 4 x 16, 2 x 32) that each march one ray with its octaves spread over the segment
-// (density_nomadplains_seg: the same fma chain in octave order, so every state bit is what
-// the single-lane march gives).  A phase runs until half its rays are done, hands the
-// states back to the owning lanes, and the survivors re-pack twice as wide.
-#ifndef RT_SEG_LIVE
-#define RT_SEG_LIVE 16
-#endif
-constexpr uint32_t kSegLive = RT_SEG_LIVE; // live rays at or below which a wave switches to segment form
-// k_trace<.., SEG=true> carries the tail code; inlined, it costs the hot loops some spills
-// (scratch traffic, no measurable time at one GPU), so it is launched only when the shard
-// has few units per wave -- the strong-scaling regime where the last rays set the frame.
-
-template <int L, bool CF>
-__device__ __forceinline__ void march_shfl(March<L, CF>& d, const March<L, CF>& s, uint32_t src)
-{
-    auto f = [&](float x) { return __shfl(x, (int)src, 64); };
-    d.p = rtm::mk(f(s.p.x), f(s.p.y), f(s.p.z));
-    d.dir = rtm::mk(f(s.dir.x), f(s.dir.y), f(s.dir.z));
-    d.sd = f(s.sd);
-    d.dist = f(s.dist);
-    d.step = f(s.step);
-    d.lastStep = f(s.lastStep);
-    d.d = f(s.d);
-    // without fog f is +0 throughout the march (march_step): restate it, so that the tail's
-    // shuffles do not make it a live value of the march loops
-    if constexpr (March<L, CF>::FOG) d.f = {f(s.f.x), f(s.f.y), f(s.f.z), f(s.f.w)};
-    else d.f = {0.0f, 0.0f, 0.0f, 0.0f};
-    d.iters = __shfl(s.iters, (int)src, 64);
-    d.fog = __shfl(s.fog ? 1 : 0, (int)src, 64) != 0;
-}
-
-// One phase at width LPR: segment k marches the k-th live ray (<= 64/LPR of them) until
-// at most `stop` segments are still live, then the states go back to their owners.
-template <int LPR, bool SKIPREFINE>
-__device__ __forceinline__ void seg_phase(const Ctx& c, March<RT_NOMADPLAINS, true>& st, bool& live, float enddist,
-                                          int max_steps, uint32_t lane, uint32_t stop, uint32_t& own)
-{
-    constexpr int L = RT_NOMADPLAINS;
-    const uint32_t seg = lane / LPR, j = lane % LPR, base = seg * LPR;
-    const uint64_t lb = __ballot(live);
-    const uint32_t n = (uint32_t)__popcll(lb);
-    uint32_t owner = 0;
-    {
-        uint64_t b = lb;
-        for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t o = (uint32_t)__builtin_ctzll(b);
-            b &= b - 1ull;
-            owner = k == seg ? o : owner;
-        }
-    }
-    March<L, true> gs;
-    march_shfl(gs, st, owner);
-    const float ge = __shfl(enddist, (int)owner, 64);
-    const int gm = __shfl(max_steps, (int)owner, 64);
-    const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
-    uint32_t cnt = 0;
-    bool glive = seg < n;
-    for (;;) {
-        glive = glive && march_live<L, true, SKIPREFINE>(c, gs, ge, gm);
-        if ((uint32_t)__popcll(__ballot(glive)) <= stop * LPR) break;
-        if (glive) {
-            auto dens = [&](f3 q) {
-                uint32_t used;
-                const float d = density_nomadplains_seg<LPR>(c, g, q, j, base, &used);
-                cnt += used + 1u;
-                return d;
-            };
-            march_step_with<L, true, SKIPREFINE, decltype(dens), true>(c, gs, dens);
-        }
-    }
-    // owner of rank r takes segment r's first lane
-    const bool mine = (lb >> lane) & 1ull;
-    const uint32_t src = mine ? (uint32_t)__popcll(lb & ((1ull << lane) - 1ull)) * LPR : lane;
-    March<L, true> back;
-    march_shfl(back, gs, src);
-    const bool bl = __shfl(glive ? 1 : 0, (int)src, 64) != 0;
-    const uint32_t bc = (uint32_t)__shfl((int)cnt, (int)src, 64);
-    if (mine) {
-        st = back;
-        live = bl;
-        own += bc;
-    }
-}
-
-// Finish every live ray of the wave (the caller checked there are at most kSegLive) in
-// segment form.  enddist/max_steps are the lane's own (shadow and AO rays differ); all
-// lanes must be active.  On return each owning lane's st is the final state of its ray.
-template <bool SKIPREFINE>
-__device__ __forceinline__ void seg_finish(const Ctx& c, March<RT_NOMADPLAINS, true>& st, bool live, float enddist,
-                                           int max_steps, uint32_t lane)
-{
-    const uint64_t calls0 = c.nz.calls;
-    uint32_t own = 0; // noise3d of this lane's own ray (STATS)
-    __builtin_amdgcn_s_setprio(3);
-    for (;;) {
-        const uint32_t n = (uint32_t)__popcll(__ballot(live));
-        if (n == 0u) break;
-        if (n > 8u) seg_phase<4, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
-        else if (n > 4u) seg_phase<8, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
-        else if (n > 2u) seg_phase<16, SKIPREFINE>(c, st, live, enddist, max_steps, lane, n / 2u, own);
-        else seg_phase<32, SKIPREFINE>(c, st, live, enddist, max_steps, lane, 0u, own);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    c.nz.calls = calls0 + own;
-}
-
 // Debug build only (make trace, -DRT_WAVE_TRACE): per-wave timeline of k_trace for
 // scheduler studies (scripts/wave_trace.py).  RT_WT_FIELDS u64 per wave slot.
 #ifdef RT_LIVE_HIST
@@ -1066,7 +948,7 @@ __device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
 #define WT(...)
 #endif
 
-template <int L, bool STATS, bool SEG>
+template <int L, bool STATS>
 __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
@@ -1077,7 +959,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 float4* __restrict__ shrec, uint32_t long_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live, uint32_t seg_live)
+                                                uint32_t compact_live)
 {
     // one LDS array (the noise image at address 0, then the frame table and the rings)
     __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords + (sizeof(FrameRays) + sizeof(TraceQueues)) / 4];
@@ -1175,14 +1057,6 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 c.nz.calls = cl.nz.calls;
                 return;
             }
-            if constexpr (L == RT_NOMADPLAINS && SEG) {
-                // drained, nothing queued and only a few rays left: finish them in group form
-                // (single frames only: a segment marches another lane's ray with its own eye)
-                if (m.n_frames == 1u && (uint32_t)__popcll(lv) <= seg_live && vload(q.l_tail) == vload(q.l_head)) {
-                    seg_finish<true>(cl, st, live, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0, lane);
-                    continue;
-                }
-            }
 #ifdef RT_COUNT_LONG_STEPS // diagnostic build: live lanes per long-ray march step (scripts/phase_util.py);
                              // 2: only while the unit queue is drained, 3: only before
             if (live && (RT_COUNT_LONG_STEPS == 1 || (RT_COUNT_LONG_STEPS == 2) == (vload(q.drained) != 0u))) {
@@ -1265,12 +1139,6 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
                     atomicAdd(&g_live_hist[__popcll(lb)], 1ull);
 #endif
-                if constexpr (L == RT_NOMADPLAINS && SEG) {
-                    if ((uint32_t)__popcll(lb) <= seg_live) {
-                        seg_finish<false>(cf, st, lv, RT_CAMERA_FAR, max_steps, lane);
-                        break;
-                    }
-                }
 #ifdef RT_COUNT_PRIMARY_STEPS // diagnostic build: live lanes per primary march step (scripts/phase_util.py)
                 if (lv) {
                     cf.nz.phase = RT_COUNT_PHASE;
@@ -1572,15 +1440,6 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     // k_finish holds no LDS: up to 2 blocks per CU
     uint32_t fblocks = need < 2u * blocks ? need : 2u * blocks;
     dim3 blk(1024);
-    // segment tail (k_trace<.., true>) when units are scarce: fewer than 2 per wave of the grid
-    // (single frames only: batches have units enough, and a segment's lanes share one eye);
-    // a.seg_mode (device flags RT_DEVICE_SEG_TAIL_*) forces it off or on
-#ifdef RT_SEG_BATCH // experiment: the segment tail for batches too (primary units only: a unit's lanes share one frame)
-    const bool seg = L == RT_NOMADPLAINS;
-#else
-    const bool seg = L == RT_NOMADPLAINS && m.n_frames == 1u &&
-                     (a.seg_mode >= 0 ? a.seg_mode > 0 : m.n_units < 2u * pblocks * 16u);
-#endif
     (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
     if (a.ao_samples > 0)
         (void)hipMemsetAsync(a.aocc, 0, ((size_t)m.frame_samples * m.n_frames + 3) / 4 * sizeof(uint32_t), a.stream);
@@ -1589,14 +1448,9 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        if (seg)
-            hipLaunchKernelGGL((k_trace<L, S, true>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
-                               m, a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
-                               a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
-        else
-            hipLaunchKernelGGL((k_trace<L, S, false>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad,
-                               m, a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc,
-                               a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive, kSegLive);
+        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m,
+                           a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
+                           a.stats, kLongBatch, kRefillIdle, kCompactLive);
         hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
                            a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
         hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
@@ -1611,10 +1465,6 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
 
 void rt_launch_camerarays(const RtLaunch& a, float4* out)
 {
-#ifdef RT_EXPERIMENT_SKIP_PREPASS // timing experiment only (variant builds): reuse stale results
-    static int launches = 0;
-    if (++launches > 8) return;
-#endif
     switch (a.landscape) {
     case RT_TESTING: launch_camerarays_l<RT_TESTING>(a, out, nullptr, 1u); break;
     case RT_SIMPLE: launch_camerarays_l<RT_SIMPLE>(a, out, nullptr, 1u); break;
@@ -1625,10 +1475,6 @@ void rt_launch_camerarays(const RtLaunch& a, float4* out)
 
 void rt_launch_camerarays_batch(const RtLaunch& a)
 {
-#ifdef RT_EXPERIMENT_SKIP_PREPASS // timing experiment only (variant builds): reuse stale results
-    static int launches = 0;
-    if (++launches > 8) return;
-#endif
     switch (a.landscape) {
     case RT_TESTING: launch_camerarays_l<RT_TESTING>(a, nullptr, a.frames, a.n_frames); break;
     case RT_SIMPLE: launch_camerarays_l<RT_SIMPLE>(a, nullptr, a.frames, a.n_frames); break;

@@ -20,6 +20,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -106,6 +107,8 @@ struct Staging {
 struct rt_device_s {
     int ordinal = 0, width = 0, height = 0;
     unsigned flags = 0;
+    // own_stream: created with the device; stream: the one it launches on (own, or borrowed via
+    // rt_device_set_stream); both are reference-counted in the stream registry below
     hipStream_t own_stream = nullptr, stream = nullptr;
     uint32_t* fb8 = nullptr;
     float4* fb32 = nullptr;
@@ -113,7 +116,6 @@ struct rt_device_s {
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
-    int seg_mode = -1;             // k_trace segment tail: -1 auto, 0 off, 1 on (RT_DEVICE_SEG_TAIL_*)
     float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
     float4* res = nullptr;
     uint32_t* hitlist = nullptr;
@@ -149,6 +151,7 @@ struct rt_device_s {
     // children (IDevice::createCompute / createTexture); destroyed with the device
     std::vector<struct rt_compute_s*> computes;
     std::vector<struct rt_texture_s*> textures;
+    ~rt_device_s();
 };
 
 static int recorder_capture(rt_recorder r);
@@ -439,7 +442,6 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.stats = (dev->flags & RT_DEVICE_STATS) ? dev->stats : nullptr;
     a.queue = dev->queue;
     a.num_cus = dev->num_cus;
-    a.seg_mode = dev->seg_mode;
     a.samples = dev->samples;
     a.res = dev->res;
     a.hitlist = dev->hitlist;
@@ -545,20 +547,90 @@ int rt_vfs_clear(void)
 }
 
 // ---- device ---------------------------------------------------------------
+// ---- stream ownership ------------------------------------------------------
+// A device's own stream may be lent to other devices (rt_device_set_stream: FrameRing's slot
+// groups share one stream per batch).  The registry counts the devices using each own stream
+// (its owner while alive, plus its borrowers); the stream is destroyed when the count drops to
+// zero, so an owner destroyed before its borrowers leaves them a live stream (and nothing
+// synchronizes or launches on a destroyed one).  Streams the caller passes in that no device
+// created (e.g. a torch stream) are not tracked: the caller keeps them alive.
+namespace {
+std::mutex g_stream_mu;
+std::map<hipStream_t, int> g_stream_refs;
+
+void stream_ref(hipStream_t s)
+{
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto it = g_stream_refs.find(s);
+    if (it != g_stream_refs.end()) ++it->second;
+}
+
+// drop one reference; the last one destroys the stream (after draining it)
+void stream_unref(hipStream_t s)
+{
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        auto it = g_stream_refs.find(s);
+        if (it == g_stream_refs.end()) return;
+        if (--it->second == 0) {
+            g_stream_refs.erase(it);
+            last = true;
+        }
+    }
+    if (last) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+    }
+}
+} // namespace
+
+rt_device_s::~rt_device_s()
+{
+    (void)hipSetDevice(ordinal);
+    if (stream) (void)hipStreamSynchronize(stream); // the stream in use is alive: a reference is held
+    for (auto* c : computes) delete c;              // children die with their device
+    for (auto* t : textures) {
+        if (t->data) (void)hipFree(t->data);
+        delete t;
+    }
+    for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
+                    (void*)res, (void*)hitlist, (void*)order, (void*)hitmask, (void*)shrec, (void*)fin, (void*)aocc,
+                    (void*)bgrx, (void*)table.d, (void*)pre_table.d})
+        if (p) (void)hipFree(p);
+    if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
+    if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
+    if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
+    if (sync_ev) (void)hipEventDestroy(sync_ev);
+    for (auto& pr : ev_pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    if (stream && stream != own_stream) stream_unref(stream); // a borrowed stream
+    if (own_stream) stream_unref(own_stream);                 // destroyed here unless lent out
+}
+
 int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_device* out)
 {
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
+    if ((flags & RT_DEVICE_SEG_TAIL_OFF) && (flags & RT_DEVICE_SEG_TAIL_ON))
+        return fail(RT_ERR_INVALID, "RT_DEVICE_SEG_TAIL_OFF and RT_DEVICE_SEG_TAIL_ON are exclusive");
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (ordinal < 0 || ordinal >= n) return fail(RT_ERR_INVALID, "GPU ordinal %d out of range (%d devices)", ordinal, n);
     HIP_TRY(hipSetDevice(ordinal));
+    // from here on every early return frees what was made (the destructor)
     auto d = std::make_unique<rt_device_s>();
     d->ordinal = ordinal;
     d->width = width;
     d->height = height;
     d->flags = flags;
     HIP_TRY(hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking));
+    {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        g_stream_refs[d->own_stream] = 1;
+    }
     d->stream = d->own_stream;
     HIP_TRY(hipMalloc(&d->fb8, (size_t)width * height * 4));
     HIP_TRY(hipMemset(d->fb8, 0, (size_t)width * height * 4));
@@ -570,53 +642,19 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
     HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
-    if ((flags & RT_DEVICE_SEG_TAIL_OFF) && (flags & RT_DEVICE_SEG_TAIL_ON))
-        return fail(RT_ERR_INVALID, "RT_DEVICE_SEG_TAIL_OFF and RT_DEVICE_SEG_TAIL_ON are exclusive");
-    d->seg_mode = (flags & RT_DEVICE_SEG_TAIL_OFF) ? 0 : (flags & RT_DEVICE_SEG_TAIL_ON) ? 1 : -1;
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
     return RT_OK;
 }
 
-void rt_device_destroy(rt_device d)
-{
-    if (!d) return;
-    (void)hipSetDevice(d->ordinal);
-    if (d->own_stream) (void)hipStreamSynchronize(d->own_stream);
-    if (d->stream && d->stream != d->own_stream) (void)hipStreamSynchronize(d->stream);
-    for (auto* c : d->computes) delete c; // children die with their device
-    for (auto* t : d->textures) {
-        if (t->data) (void)hipFree(t->data);
-        delete t;
-    }
-    if (d->fb8) (void)hipFree(d->fb8);
-    if (d->fb32) (void)hipFree(d->fb32);
-    if (d->stats) (void)hipFree(d->stats);
-    if (d->scratch_cam) (void)hipFree(d->scratch_cam);
-    if (d->queue) (void)hipFree(d->queue);
-    if (d->samples) (void)hipFree(d->samples);
-    if (d->res) (void)hipFree(d->res);
-    if (d->hitlist) (void)hipFree(d->hitlist);
-    if (d->order) (void)hipFree(d->order);
-    if (d->hitmask) (void)hipFree(d->hitmask);
-    if (d->shrec) (void)hipFree(d->shrec);
-    if (d->fin) (void)hipFree(d->fin);
-    if (d->aocc) (void)hipFree(d->aocc);
-    if (d->bgrx) (void)hipFree(d->bgrx);
-    if (d->recorder) recorder_detach(d->recorder); // the recorder outlives its device: it stops capturing
-    if (d->graph_pre.exec) (void)hipGraphExecDestroy(d->graph_pre.exec);
-    if (d->table.d) (void)hipFree(d->table.d);
-    if (d->pre_table.d) (void)hipFree(d->pre_table.d);
-    if (d->sync_ev) (void)hipEventDestroy(d->sync_ev);
-    if (d->graph_trace.exec) (void)hipGraphExecDestroy(d->graph_trace.exec);
-    for (auto& pr : d->ev_pool) {
-        (void)hipEventDestroy(pr.first);
-        (void)hipEventDestroy(pr.second);
-    }
-    if (d->own_stream) (void)hipStreamDestroy(d->own_stream);
-    delete d;
-}
+void rt_device_destroy(rt_device d) { delete d; }
 
+int rt_stream_refs(void* hip_stream)
+{
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto it = g_stream_refs.find((hipStream_t)hip_stream);
+    return it == g_stream_refs.end() ? 0 : it->second;
+}
 
 int rt_device_present(rt_device d)
 {
@@ -697,26 +735,34 @@ void* rt_device_stream(rt_device d) { return d ? (void*)d->stream : nullptr; }
 int rt_device_set_stream(rt_device d, void* s)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
-    d->stream = s ? (hipStream_t)s : d->own_stream;
+    hipStream_t want = s ? (hipStream_t)s : d->own_stream;
+    if (want == d->stream) return RT_OK;
+    if (want != d->own_stream) stream_ref(want);             // borrow (tracked if another device owns it)
+    if (d->stream != d->own_stream) stream_unref(d->stream); // return the previous loan
+    d->stream = want;
     return RT_OK;
 }
 
-int rt_device_stats(rt_device d, rt_stats* out, int reset)
+int rt_device_stats_sized(rt_device d, rt_stats* out, size_t size, int reset)
 {
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
     RtStats h;
     HIP_TRY(hipMemcpyAsync(&h, d->stats, sizeof(h), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
-    out->primary_steps = h.primary_steps;
-    out->shadow_steps = h.shadow_steps;
-    out->prepass_steps = h.prepass_steps;
-    out->hits = h.hits;
-    out->noise_calls = h.noise_calls;
-    out->ao_steps = h.ao_steps;
-    out->noise_wave_iters = h.noise_waves;
+    rt_stats v{};
+    v.primary_steps = h.primary_steps;
+    v.shadow_steps = h.shadow_steps;
+    v.prepass_steps = h.prepass_steps;
+    v.hits = h.hits;
+    v.noise_calls = h.noise_calls;
+    v.ao_steps = h.ao_steps;
+    v.noise_wave_iters = h.noise_waves;
+    std::memcpy(out, &v, size < sizeof(v) ? size : sizeof(v));
     if (reset) HIP_TRY(hipMemsetAsync(d->stats, 0, sizeof(RtStats), d->stream));
     return RT_OK;
 }
+
+int rt_device_stats(rt_device d, rt_stats* out, int reset) { return rt_device_stats_sized(d, out, sizeof(rt_stats), reset); }
 
 int rt_device_set_profiling(rt_device d, int enable)
 {
@@ -1075,7 +1121,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
 {
     const uint64_t v[] = {(uint64_t)(uintptr_t)a.stream, (uint64_t)a.landscape, (uint64_t)(uintptr_t)a.consts,
                           (uint64_t)(uintptr_t)a.perm2d, (uint64_t)(uintptr_t)a.grad, (uint64_t)(uintptr_t)a.stats,
-                          (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(a.seg_mode + 1),
+                          (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.hitlist,
                           (uint64_t)(uintptr_t)a.shrec, (uint64_t)a.long_cap, (uint64_t)(uintptr_t)a.fin,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,

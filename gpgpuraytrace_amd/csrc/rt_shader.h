@@ -32,14 +32,13 @@ using rtm::fma;
 //               (base byte from so16, index byte from the texel, slot byte from so16); the b128
 //               loads are conflict-free however random the indices, the b64 loads 2-way.
 //   kLdsGz      gz at the same slot layout (ds_read_b64 ... offset:32768 from the gxy address).
-//   then        the octave tables (oct, colt).
+//   then        the nomadplains FBM octave table (oct).
 constexpr uint32_t kLdsGxy = 0x10000u, kLdsGz = 0x18000u;
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 struct NoiseView {
     const char* img;    // the LDS image (perm2D texels at its offset 0)
     const float4* oct;  // nomadplains FBM octave N: (S, 0.35 S, 1/S, 0), N = 0 .. RT_NP_OCTAVES + 2
-    const float2* colt; // colour FBM octave N: (S, 1/S), N = 0 .. RT_COL_OCTAVES + 1
     uint32_t so16;  // kLdsGxy | (lane & 15) * 16: byte 2 = the gxy plane's base >> 16, byte 0 = the lane's slot
     // noise3d evaluations, read only by the STATS kernels (dead otherwise): low word = this lane's
     // calls, high word = wave iterations (the wave's first active lane adds 1 << 32 per call), so
@@ -346,8 +345,9 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     f3 q0 = rtm::scale(p1, 0.006f);
     const int n_oct = np_octaves(c, p);
     // The octave cells take the short integer path (noise3d_cell<true>) when every lattice
-    // coordinate of the wave's noises stays below 2^20 in magnitude: |q0| * S_n < 2^20 for the
-    // lane's last octave n (S grows with N; the steep noise's coordinates are 1.19 |q0| < S_1 |q0|).
+    // coordinate of the wave's noises stays below kFastCellRange = 2^13 in magnitude: |q0| * S_n <
+    // 2^13 for the lane's last octave n (S grows with N; the steep noise's coordinates are 1.19 |q0|
+    // < S_1 |q0|).  2^13 is the bound of the magic-number texel offset (texel_offset: |512 f| < 2^22).
     // Wave-uniform, so the sample runs one of two copies.
     const float qm = rtm::max(rtm::max(rtm::abs(q0.x), rtm::abs(q0.y)), rtm::abs(q0.z));
     const bool fast = !__ballot(!(qm * c.nz.oct[n_oct].x < kFastCellRange));
@@ -365,8 +365,7 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
 }
 
 // density_nomadplains with the FBM spread over a segment of LPR lanes that march ONE
-// ray together (latency-bound passes: the camerarays prepass has 1024 rays for 256 CUs;
-// the last rays of a k_trace wave).  The 18 noise values of a sample are numbered
+// ray together (the camerarays prepass: 1024 latency-bound rays for 256 CUs).  The 18 noise values of a sample are numbered
 // v = 0 (the steep noise) and v = N (octave N = 1..17); lane j of the segment evaluates
 // v = j, j + LPR, j + 2 LPR, ... (rounds), then every lane gathers the values in v order
 // and runs the same fma chain, so the result is bit-identical to density_nomadplains.

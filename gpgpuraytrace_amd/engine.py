@@ -157,13 +157,10 @@ class Compute:
 class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
-    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, seg_tail=None):
-        """seg_tail: None = the trace kernel picks its tail form per launch; False / True force
-        it off / on (RT_DEVICE_SEG_TAIL_OFF / _ON; same bits either way)."""
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False):
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
-                      | (_native.RT_DEVICE_GRAPH if graph else 0)
-                      | {None: 0, False: _native.RT_DEVICE_SEG_TAIL_OFF, True: _native.RT_DEVICE_SEG_TAIL_ON}[seg_tail])
+                      | (_native.RT_DEVICE_GRAPH if graph else 0))
         self._h = None
 
     def create(self):
@@ -208,7 +205,7 @@ class Device:
 
     def stats(self, reset=True):
         s = _native.RtStats()
-        check(lib().rt_device_stats(self._h, C.byref(s), 1 if reset else 0), "stats")
+        check(lib().rt_device_stats_sized(self._h, C.byref(s), C.sizeof(s), 1 if reset else 0), "stats")
         return {n: int(getattr(s, n)) for n, _ in s._fields_}
 
     def graph_info(self):
@@ -666,8 +663,8 @@ class FrameRing:
         return tot, n
 
     def destroy(self):
-        # last slot first: a group's devices run on its first device's stream (set_stream), and
-        # rt_device_destroy synchronizes the stream a device uses, so the owner must go last
+        # any order is safe: a group's devices borrow its first device's stream, and the runtime
+        # keeps a lent stream alive until its last user is destroyed (rt_stream_refs)
         for dev, _ in reversed(self.slots):
             dev.destroy()
         self.slots = []

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 enum {
     RT_OK = 0,
@@ -52,10 +52,8 @@ enum {
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
  * every frame; a changed launch argument (shader swap, buffers, shard, stats) re-captures.
  * No reference counterpart (the D3D frame loop re-records its dispatches every frame).
- * RT_DEVICE_SEG_TAIL_OFF / _ON: force the trace kernel's octave-parallel tail form off or on
- * (default: chosen per launch, on when a single frame's shard has fewer than 2 work units per
- * wave of the grid).  Both forms produce the same bits; the flags exist for the parity tests
- * and A/B timing.  Setting both fails with RT_ERR_INVALID. */
+ * RT_DEVICE_SEG_TAIL_OFF / _ON: reserved (ABI <= 3 selected a trace-kernel tail variant that
+ * ABI 4 removed; both are accepted and have no effect).  Setting both fails with RT_ERR_INVALID. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };
@@ -110,10 +108,18 @@ int rt_device_readback_bgrx(rt_device dev, void* dst, size_t row_pitch);
 int rt_device_size(rt_device dev, int* width, int* height);
 void* rt_device_framebuffer(rt_device dev);       /* device pointer, W*H uint32 RGBA8 */
 void* rt_device_stream(rt_device dev);            /* hipStream_t */
-/* NULL = the device's own stream.  A borrowed stream (another device's, or the caller's) must
- * outlive the device: rt_device_destroy synchronizes the stream its device uses. */
+/* NULL = the device's own stream.  Devices' own streams are reference-counted: a device that
+ * borrows another device's stream keeps it alive, so the owner may be destroyed first (its stream
+ * is destroyed with its last user).  A stream no device created (the caller's) must outlive every
+ * device using it: rt_device_destroy synchronizes the stream its device uses. */
 int rt_device_set_stream(rt_device dev, void* hip_stream);
+/* (ABI 4) devices currently holding `hip_stream` (its owner while alive + its borrowers); 0 for a
+ * stream no live device created. */
+int rt_stream_refs(void* hip_stream);
 int rt_device_stats(rt_device dev, rt_stats* out, int reset); /* needs RT_DEVICE_STATS */
+/* (ABI 4) the same with the caller's struct size: writes min(size, sizeof(rt_stats)) bytes, so a
+ * caller built against an older, shorter rt_stats is never written past its struct. */
+int rt_device_stats_sized(rt_device dev, rt_stats* out, size_t size, int reset);
 /* HIP-event timing of the dominant kernel (tracescreen) on the device stream:
  * enable, then rt_device_kernel_time returns the summed elapsed ms and launch count
  * since the last call (synchronises). */

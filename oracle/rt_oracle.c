@@ -258,7 +258,15 @@ typedef struct {
     f3 eye, sun;
     float density_factor, step_factor, one_minus_step_factor, min_limit;
     uint64_t noise_calls, density_calls;
+#ifdef RO_STUDY /* scripts/skip_study.c: which pixel / ray the samples belong to */
+    int64_t study_pixel;
+#endif
 } ctx;
+
+#ifdef RO_STUDY
+static void ro_study_sample(ctx* c, f3 p, float d, int calcfog, int skiprefine, int max_steps, int iters,
+                            float dist, float enddist, float step, float lastStep);
+#endif
 
 static void ctx_init(ctx* c, const ro_noise* nz, const ro_frame* fr)
 {
@@ -273,6 +281,9 @@ static void ctx_init(ctx* c, const ro_noise* nz, const ro_frame* fr)
     c->min_limit = (float)((double)0.02f * (double)0.03f);
     c->noise_calls = 0;
     c->density_calls = 0;
+#ifdef RO_STUDY
+    c->study_pixel = -1;
+#endif
 }
 
 /* noise.hlsl:145-150 gradperm: dot(permGradients[x % 128].xyz, p) under R4 */
@@ -487,6 +498,9 @@ static ray_result trace_ray(ctx* c, f3 p, float dist, float enddist, float stepm
         rayp = v3(fmaf(dir.x, dist, p.x), fmaf(dir.y, dist, p.y), fmaf(dir.z, dist, p.z));
         f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
         d = get_density(c, rayp);
+#ifdef RO_STUDY
+        ro_study_sample(c, rayp, d, calcfog, skiprefine, max_steps, iters, dist, enddist, step, lastStep);
+#endif
         if (calcfog) {
             f4 g = get_fog(c, rayp, dist);
             fs.x = g.x * step; fs.y = g.y * step; fs.z = g.z * step; fs.w = g.w * step;
@@ -930,6 +944,9 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
         ctx c;
         ctx_init(&c, nz, fr);
         for (int x = 0; x < W; ++x) {
+#ifdef RO_STUDY
+            c.study_pixel = (int64_t)y * W + x;
+#endif
             float pxf = (float)x, pyf = (float)y;
             float spx = pxf * rcp((float)W), spy = pyf * rcp((float)H);
             uint32_t cell = (uint32_t)fmaf(floorf(spy * 32.0f), 32.0f, floorf(spx * 32.0f));

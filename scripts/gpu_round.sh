@@ -4,7 +4,7 @@
 # usage: gpu_round.sh <variant>   (gpgpuraytrace_amd/_build/librt_hip_<variant>.so)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 V=$1
-RT_LIB_VARIANT=$V timeout -k 10 400 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+RT_LIB_VARIANT=$V timeout -k 10 400 python3 -u scripts/with_variant.py -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/${V}_tests.log 2>&1 || { tail -5 gpurun_out/${V}_tests.log; exit 1; }
 tail -1 gpurun_out/${V}_tests.log
 bash scripts/ab_bench.sh RT_LIB_VARIANT= RT_LIB_VARIANT=$V RT_LIB_VARIANT= RT_LIB_VARIANT=$V || exit 1

@@ -8,6 +8,10 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import with_variant  # noqa: E402
+
+with_variant.apply()
 import gpgpuraytrace_amd as G  # noqa: E402
 from gpgpuraytrace_amd import engine as E  # noqa: E402
 

@@ -12,6 +12,10 @@ import sys
 
 os.environ.setdefault("RT_LIB_VARIANT", "trace")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import with_variant  # noqa: E402
+
+with_variant.apply()
 
 F = 18
 

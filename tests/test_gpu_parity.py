@@ -31,10 +31,10 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         seg_tail=None, ao=0, graph=False):
+         ao=0, graph=False):
     import gpgpuraytrace_amd as G
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
-                                    stats=stats, graph=graph, seg_tail=seg_tail)
+                                    stats=stats, graph=graph)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -169,22 +169,25 @@ def test_density_bitexact(land):
 
 
 # --- whole frames vs the golden oracle frames ----------------------------------------------
-@pytest.mark.parametrize("tail", ["auto", "noseg", "seg"])
+@pytest.mark.parametrize("kernels", ["stats", "product"])
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
-def test_frame_bitexact_device_path(spec, tail):
-    """auto: k_trace picks its tail form (at these sizes, few units per wave: the segment
-    tail); noseg forces the plain form the large single-GPU frames use, seg the segment tail."""
+def test_frame_bitexact_device_path(spec, kernels):
+    """stats: the instrumented kernels (their counts equal the oracle's too); product: the
+    uninstrumented kernels the bench times."""
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=True,
-                    seg_tail={"auto": None, "noseg": False, "seg": True}[tail], ao=ao)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=kernels == "stats", ao=ao)
     ter.render_device()
     dev.present()
     img, img8 = dev.readback_float(), dev.readback()
-    st = dev.stats()
     assert bits_equal(img, gold[key + "_rgba32f"])
     assert np.array_equal(img8, gold[key + "_rgba8"])
+    if kernels != "stats":
+        assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
+        dev.destroy()
+        return
+    st = dev.stats()
     ref = gold[key + "_stats"]  # noise3d, prepass, primary, shadow, rays, hits, ao
     assert (st["noise_calls"], st["prepass_steps"], st["primary_steps"], st["shadow_steps"], st["hits"],
             st["ao_steps"]) == (ref[0], ref[1], ref[2], ref[3], ref[5], ref[6])
@@ -982,3 +985,29 @@ def test_variable_manager_live_tweak_changes_frame():
         dev.destroy()
     finally:
         G.VariableManager.stop()
+
+
+# --- stream ownership (frosttrace.h rt_device_set_stream / rt_stream_refs, ABI 4) -------------
+def test_stream_owner_destroyed_before_borrower():
+    """A device borrowing another device's stream keeps it alive: destroying the owner first (the
+    order that hung FrameRing.destroy in round 2's multi-rank rehearsals) leaves the borrower a live
+    stream it renders a bit-exact frame on, and the stream goes with its last user."""
+    import gpgpuraytrace_amd as G
+    gold = GI.load()
+    key = GI.frame_key("nomadplains", "reset", 64, 48, 1, 0)
+    owner, _ = make(GI.consts(64, 48, "reset"))
+    dev, ter = make(GI.consts(64, 48, "reset"))
+    s = owner.stream()
+    assert G.lib().rt_stream_refs(s) == 1
+    dev.set_stream(s)
+    assert G.lib().rt_stream_refs(s) == 2
+    owner.destroy()
+    assert G.lib().rt_stream_refs(s) == 1  # the borrower's reference keeps it
+    ter.render_device()
+    dev.present()
+    assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])
+    dev.set_stream(None)  # back to its own stream: the loan ends and the lent stream is destroyed
+    assert G.lib().rt_stream_refs(s) == 0
+    ter.render_device()
+    assert np.array_equal(dev.readback(), gold[key + "_rgba8"])
+    dev.destroy()

@@ -31,7 +31,26 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes binding covers the whole header
     assert set(names) <= set(_native.SIGNATURES), set(names) - set(_native.SIGNATURES)
-    assert L.rt_abi_version() == 3
+    assert L.rt_abi_version() == _native.ABI_VERSION == 4
+
+
+def test_product_reads_no_environment_and_has_no_experiment_switches():
+    """The product's loader takes no environment variable (experiment builds are selected by
+    scripts/with_variant.py) and the kernels carry no work-skipping experiment switch."""
+    src = open(os.path.join(ROOT, "gpgpuraytrace_amd", "_native.py")).read()
+    assert "os.environ" not in src
+    kern = open(os.path.join(ROOT, "gpgpuraytrace_amd", "csrc", "rt_kernels.hip")).read()
+    assert "SKIP_PREPASS" not in kern
+
+
+def test_stats_sized_never_writes_past_a_short_struct():
+    """rt_device_stats_sized (ABI 4) on a null device fails before touching the buffer; the ctypes
+    binding refuses a library older than itself (ABI-1 callers and the 8-byte overrun)."""
+    import ctypes as C
+    import gpgpuraytrace_amd as G
+    buf = (C.c_ubyte * 64)(*([0xAB] * 64))
+    assert G.lib().rt_device_stats_sized(None, C.cast(buf, C.POINTER(G._native.RtStats)), 48, 0) != 0
+    assert bytes(buf) == b"\xab" * 64
 
 
 def test_product_loads_only_in_tree_library():
