@@ -85,6 +85,7 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     c.nz.oct = reinterpret_cast<const float4*>(lds + kOctBase);
     c.nz.so16 = kLdsGxy | ((threadIdx.x & 15u) * 16u);
     c.nz.calls = 0;
+    c.nz.lds_calls = nullptr;
     c.nz.phase = RT_PHASE_OTHER;
     c.k = k;
     c.kf = (KPtr)k;
@@ -300,6 +301,13 @@ __device__ __forceinline__ uint32_t wave_fetch(uint32_t* counter, uint32_t lane,
     uint32_t u = 0;
     if (lane == 0) u = atomicAdd(counter, n);
     return __builtin_amdgcn_readfirstlane(u);
+}
+
+// Set bits of `mask` below this lane (its rank among the lanes of `mask`): v_mbcnt_lo/hi, so no
+// 64-bit lane mask stays live in VGPRs across the persistent kernels' loops.
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
 // Per-sample RayResult of the primary march: 3 float4 (pd, fcolord, density).
@@ -736,7 +744,6 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
     __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
     load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds);
     const uint32_t n_units = (n_hits + 63u) / 64u;
     float ssteps = 0.0f;
@@ -765,14 +772,14 @@ __global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__
         const uint64_t lb = __ballot(more);
         if (lb) {
             const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
-            const uint32_t j = b + (uint32_t)__popcll(lb & lt_mask);
+            const uint32_t j = b + lane_rank(lb);
             if (more && j < long_cap) long_pack(st, t, RT_LONG_SHADOW, shrec + (size_t)kShadowRec * j);
         }
         // AO extension: every AO ray of every hit goes to the long list
         const uint64_t vb = __ballot(valid);
         for (int kk = 0; kk < k->ao_samples; ++kk) {
             const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(vb));
-            const uint32_t j = b + (uint32_t)__popcll(vb & lt_mask);
+            const uint32_t j = b + lane_rank(vb);
             if (valid && j < long_cap) {
                 March<L, true> ao;
                 ao_begin(c, h, (uint32_t)kk, ao);
@@ -805,7 +812,6 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
     frame_rays_load(s_fr, ft, m.n_frames);
     load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
     Ctx c = make_ctx(k, lds); // c.eye: the lane's ray's frame (set on refill)
     March<L, true> st;
     st.d = 0.0f;
@@ -840,7 +846,7 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
                         pool_left = (n_long - b) < 64u ? (n_long - b) : 64u;
                     }
                     const uint32_t take = (uint32_t)__popcll(idle) < pool_left ? (uint32_t)__popcll(idle) : pool_left;
-                    const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                    const uint32_t rank = lane_rank(idle);
                     const bool mine = ((idle >> lane) & 1ull) && rank < take;
                     if (mine) {
                         const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
@@ -895,6 +901,14 @@ constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a w
 #define RT_COMPACT_LIVE 56
 #endif
 constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
+
+// STATS kernels: a k_trace block's march-step and hit counters (LDS atomics; the block's last wave
+// adds them to the frame statistics)
+struct BlockStats {
+    enum { PRIMARY = 0, SHADOW = 1, AO = 2, HITS = 3, NOISE = 4, NOISE_WAVES = 5 };
+    unsigned long long v[6];
+    uint32_t done, pad;
+};
 
 struct TraceQueues {
     uint32_t lock;
@@ -961,10 +975,14 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
                                                 uint32_t compact_live)
 {
-    // one LDS array (the noise image at address 0, then the frame table and the rings)
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords + (sizeof(FrameRays) + sizeof(TraceQueues)) / 4];
+    // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
+    // kernels' block counters)
+    __shared__ __attribute__((aligned(16))) uint32_t
+        lds[kNoiseLdsWords + (sizeof(FrameRays) + sizeof(TraceQueues) + sizeof(BlockStats)) / 4];
     FrameRays& s_fr = *reinterpret_cast<FrameRays*>(lds + kNoiseLdsWords);
     TraceQueues& q = *reinterpret_cast<TraceQueues*>(lds + kNoiseLdsWords + sizeof(FrameRays) / 4);
+    BlockStats& s_st =
+        *reinterpret_cast<BlockStats*>(lds + kNoiseLdsWords + (sizeof(FrameRays) + sizeof(TraceQueues)) / 4);
     frame_rays_load(s_fr, ft, m.n_frames);
     if (threadIdx.x == 0) {
         q.lock = 0;
@@ -972,15 +990,18 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         q.l_head = q.l_tail = 0;
         q.active = 0;
         q.drained = 0;
+        if constexpr (STATS) s_st = BlockStats{};
     }
     load_noise_lds(lds, perm2d, grad, k);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    const uint32_t lane = __lane_id(); // v_mbcnt of constants: rematerialisable (threadIdx & 63 spilled)
     Ctx c = make_ctx(k, lds); // k: frame-invariant constants (per-frame ones: frame_ctx / s_fr)
+    if constexpr (STATS) c.nz.lds_calls = (__attribute__((address_space(3))) unsigned long long*)&s_st.v[BlockStats::NOISE];
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
-    float psteps = 0.0f, ssteps = 0.0f, aosteps = 0.0f;
-    uint32_t nhits = 0;
+    // STATS: march steps and hits go to the block's LDS counters (no VGPRs held across the loops)
+    auto stat = [&](int i, uint32_t v) {
+        if constexpr (STATS) atomicAdd(&s_st.v[i], (unsigned long long)v);
+    };
 
     // wt: begin, end, t_unit, t_shade, t_long, n_unit, n_shade, n_long, last unit end, t_idle, hw_id, xcc_id,
     // loop iterations, long rays finished (lane), max long-ray iters (lane), last iteration, max primary iters (lane)
@@ -991,7 +1012,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t type) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
-        const uint32_t n = (uint32_t)__popcll(lb), rank = (uint32_t)__popcll(lb & lt_mask);
+        const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
         const bool fits = lt - lh + n <= kLongRing;
@@ -1020,10 +1041,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 long_finish<L, true>(k, fin, samples, aocc, t, type, st);
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 live = false;
-                if constexpr (STATS) {
-                    if (type == RT_LONG_AO) aosteps += (float)st.iters;
-                    else ssteps += (float)st.iters;
-                }
+                stat(type == RT_LONG_AO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -1031,7 +1049,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 q_lock(&q.lock, lane);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
-                const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+                const uint32_t rank = lane_rank(idle);
                 if (((idle >> lane) & 1ull) && rank < take) {
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
                     t = long_unpack(r[0], r[1], r[2], rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
@@ -1090,7 +1108,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             more = h.more;
             if (!more) {
                 sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
-                if constexpr (STATS) ssteps += (float)st.iters;
+                stat(BlockStats::SHADOW, (uint32_t)st.iters);
             } else {
                 fin_store<L>(fin, t, h);
             }
@@ -1156,7 +1174,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
             if (valid) {
                 RayResult rr = march_result(st);
-                if constexpr (STATS) psteps += rr.steps;
+                stat(BlockStats::PRIMARY, (uint32_t)st.iters);
                 if (hit) {
                     store_ray<L>(res, m.frame_samples * m.n_frames, t, rr); // the shading input
                 } else {
@@ -1173,8 +1191,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             const uint64_t hb = __ballot(hit);
             if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = hb; // k_finish skips the misses
             if (hb) {
-                const uint32_t n = (uint32_t)__popcll(hb), rank = (uint32_t)__popcll(hb & lt_mask);
-                if constexpr (STATS) nhits += hit ? 1u : 0u;
+                const uint32_t n = (uint32_t)__popcll(hb), rank = lane_rank(hb);
+                if (hit) stat(BlockStats::HITS, 1u);
                 __builtin_amdgcn_s_waitcnt(0); // res[t] is in L2 before the hit is visible
                 q_lock(&q.lock, lane);
                 const uint32_t hh = vload(q.h_head), ht = vload(q.h_tail);
@@ -1250,11 +1268,17 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
            g_wave_trace[slot * RT_WT_FIELDS + lane] = v;
        })
     if constexpr (STATS) {
-        atomicAdd(&stats->primary_steps, (unsigned long long)psteps);
-        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
-        atomicAdd(&stats->hits, (unsigned long long)nhits);
-        stats_noise(stats, c.nz.calls);
+        // the block's last wave out adds its counters to the frame statistics
+        uint32_t done = 0;
+        if (lane == 0) done = atomicAdd(&s_st.done, 1u);
+        if (__builtin_amdgcn_readfirstlane(done) == (blockDim.x >> 6) - 1u && lane == 0) {
+            atomicAdd(&stats->primary_steps, vload(s_st.v[BlockStats::PRIMARY]));
+            atomicAdd(&stats->shadow_steps, vload(s_st.v[BlockStats::SHADOW]));
+            atomicAdd(&stats->ao_steps, vload(s_st.v[BlockStats::AO]));
+            atomicAdd(&stats->hits, vload(s_st.v[BlockStats::HITS]));
+            atomicAdd(&stats->noise_calls, vload(s_st.v[BlockStats::NOISE]));
+            atomicAdd(&stats->noise_waves, vload(s_st.v[BlockStats::NOISE_WAVES]));
+        }
     }
 }
 

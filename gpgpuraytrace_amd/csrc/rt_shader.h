@@ -44,6 +44,10 @@ struct NoiseView {
     // calls, high word = wave iterations (the wave's first active lane adds 1 << 32 per call), so
     // calls / (64 * iterations) is the SIMD lane utilisation of the noise work
     mutable uint64_t calls;
+    // k_trace's STATS kernels count in LDS instead ({lane calls, wave iterations}, added by the
+    // wave's first active lane per call): no per-lane 64-bit counter held across its loops.
+    // nullptr elsewhere (then `calls` counts).
+    __attribute__((address_space(3))) unsigned long long* lds_calls;
     // k_trace work kind of the caller (RT_PHASE_*): a diagnostic build (-DRT_COUNT_PHASE=k, scripts/
     // phase_util.sh) counts only that kind's noise, to split the lane utilisation by phase
     uint32_t phase;
@@ -56,6 +60,13 @@ __device__ __forceinline__ void count_noise(const NoiseView& nz)
     if (nz.phase != RT_COUNT_PHASE) return;
 #endif
     const uint64_t ex = __builtin_amdgcn_read_exec();
+    if (nz.lds_calls) {
+        if (__lane_id() == (uint32_t)__builtin_ctzll(ex)) {
+            __atomic_fetch_add(&nz.lds_calls[0], (unsigned long long)__popcll(ex), __ATOMIC_RELAXED);
+            __atomic_fetch_add(&nz.lds_calls[1], 1ull, __ATOMIC_RELAXED);
+        }
+        return;
+    }
     nz.calls += 1ull + ((uint64_t)(__lane_id() == (uint32_t)__builtin_ctzll(ex)) << 32);
 }
 
