@@ -87,7 +87,8 @@ def parse():
                     help="skip config.single_frame / config.ref_semantics (extra timed passes)")
     ap.add_argument("--verify", action="store_true",
                     help="after the timed loop rank 0 checks every assembled frame of the last batch against a "
-                         "whole-frame render on one device (RGBA8, bit for bit); adds config.verify")
+                         "whole-frame render on one device (RGBA8, bit for bit); adds config.verify (always on "
+                         "at N>1)")
     ap.add_argument("--cpu-row-step", type=int, default=None, help="CPU baseline (all cores): every n-th row")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the host's share)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
@@ -122,10 +123,12 @@ def batch_sizes(steps, batch):
     return [base + (1 if i < extra else 0) for i in range(n)]
 
 
-def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, threads, gpu_rgba32f, gpu_rgba8):
+def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, threads, gpu_rgba32f, gpu_rgba8,
+                 timed_frames):
     """Oracle (scalar C restatement, OpenMP over rows) on the host cores: (1) all `threads` on
-    rows 0::row_step (the reported value; its pixels are compared with the GPU frame), (2) one
-    thread on rows 0::row_step_1t."""
+    rows 0::row_step (the reported value; its pixels are compared with the GPU's: the frames the
+    timed loop rendered, `timed_frames` = [(label, rgba8)], and the instrumented whole frame's
+    float32 colour), (2) one thread on rows 0::row_step_1t."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
@@ -146,13 +149,20 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
     sl = slice(0, H, row_step)
     a, b = gpu_rgba32f[sl], rgba[sl]
     same_bits = bool(np.all((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))))
+    timed = {label: bool(np.array_equal(img[sl], rgba8[sl])) for label, img in timed_frames}
     parity = {
         "oracle": "oracle/rt_oracle.c (CPU restatement of the HLSL; D3D path not runnable here)",
-        "rows": f"0::{row_step} of {H} ({len(range(0, H, row_step)) * W} pixels)",
-        "rgba32f_bitexact": same_bits,
-        "max_abs_delta_rgba32f": float(np.max(np.abs(a.astype(np.float64) - b.astype(np.float64)))) if a.size else 0.0,
-        "rgba8_equal": bool(np.array_equal(gpu_rgba8[sl], rgba8[sl])),
-        "tolerance": "bit-exact (north_star bound: 1e-4 per channel)",
+        "rows": f"0::{row_step} of {H} ({len(range(0, H, row_step)) * W} pixels per frame)",
+        # the frames the timed loop itself rendered (RGBA8 framebuffers read back after the timed region)
+        "timed_frames_rgba8_equal": timed,
+        "timed_frames_all_equal": all(timed.values()),
+        # the instrumented whole frame (float32 output enabled, same kernels' instrumented build)
+        "whole_frame_rgba32f_bitexact": same_bits,
+        "whole_frame_max_abs_delta_rgba32f": float(np.max(np.abs(a.astype(np.float64) - b.astype(np.float64))))
+        if a.size else 0.0,
+        "whole_frame_rgba8_equal": bool(np.array_equal(gpu_rgba8[sl], rgba8[sl])),
+        "tolerance": "bit-exact (north_star bound: 1e-4 per channel; profiles/r03/parity_sensitivity.md bounds "
+                     "the oracle's own arithmetic conventions)",
     }
     out = {"value": round(rays / dt / 1e6, 4), "unit": "Mray/s", "cores": threads, "kind": "port",
            "host_cpus": os.cpu_count(),
@@ -347,16 +357,25 @@ def main():
     elapsed = time.perf_counter() - t0
 
     progress(rank, f"timed done ({elapsed * 1e3:.1f} ms)")
+    # the timed loop's own output: the first and last frame of its last batch (rank 0 holds every
+    # frame whole: at N>1 assembled from all ranks' shards), read back now, before any other pass
+    # reuses the slots; N=1 compares them with the oracle (config.parity), N>1 with a whole-frame
+    # render on one device (config.verify)
+    g_last = ((ring.frame // B) - 1) % ring.depth
+    last = ring.slots[g_last * B:g_last * B + sizes[-1]]
+    timed_frames = []
+    if rank == 0:
+        for f in sorted({0, len(last) - 1}):
+            timed_frames.append((f"batch {len(sizes) - 1} frame {f}", last[f][0].readback()))
     verify = None
-    if a.verify and rank == 0:
+    if (a.verify or world > 1) and rank == 0:
         # the last timed batch's frames, assembled from every rank's shards, against one whole frame
-        g_last = ((ring.frame // B) - 1) % ring.depth
         vdev, vter = make(stats=False)
         vter.render_device(0, 1)
         want = vdev.readback()
         vdev.destroy()
         verify = []
-        for f, (d, _) in enumerate(ring.slots[g_last * B:g_last * B + sizes[-1]]):
+        for f, (d, _) in enumerate(last):
             bad = np.any(d.readback() != want, axis=-1)
             if bad.any():  # which tiles (and so which shards) came out wrong
                 ty, tx = np.nonzero(bad)
@@ -471,7 +490,8 @@ def main():
                               else "direct launches",
                 "frame_latency_ms": round(latency_ms, 4),  # one batch of B frames at a time
                 **companions,
-                **({"verify": "frames equal a whole-frame render" if not verify else {"MISMATCH": verify}}
+                **({"verify": f"all {sizes[-1]} frames of the last timed batch equal a whole-frame render on one "
+                              f"device" if not verify else {"MISMATCH": verify}}
                    if verify is not None else {}),
             },
             "roofline": {
@@ -491,7 +511,8 @@ def main():
             threads = a.cpu_threads or host_threads()
             img32, img8 = counts["img"]
             out["cpu_baseline"], out["config"]["parity"] = cpu_baseline(
-                consts, a.landscape, a.max_steps, a.ao, a.cpu_row_step, preset["cpu_rows_1t"], threads, img32, img8)
+                consts, a.landscape, a.max_steps, a.ao, a.cpu_row_step, preset["cpu_rows_1t"], threads, img32, img8,
+                timed_frames)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

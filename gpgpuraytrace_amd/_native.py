@@ -110,6 +110,7 @@ SIGNATURES = {
     "rt_varmgr_register_compute": (_i, [_vp]),
     "rt_debug_math": (_i, [_vp, _i, _vp, _vp, _vp, _i]),
     "rt_debug_noise": (_i, [_vp, _vp, _vp, _i, _i]),
+    "rt_debug_sky": (_i, [_vp, _vp, _vp, _i]),
 }
 
 

@@ -87,3 +87,4 @@ void rt_launch_shard_copy(hipStream_t s, const ShardJobs& jobs, int n, int w, in
 // diagnostics (primitive-level parity tests)
 void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n);
 void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int n, int density);
+void rt_launch_debug_sky(const RtLaunch& a, const float* dirs, float* out, int n);

@@ -1154,7 +1154,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 const uint64_t lb = __ballot(lv);
                 if (lb == 0ull) break;
 #ifdef RT_LIVE_HIST // diagnostic build: histogram of live lanes per primary march step (rt_debug_live_hist)
-                if (lane == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+                if (lane == (uint32_t)__builtin_ctzll(__ballot(1)))
                     atomicAdd(&g_live_hist[__popcll(lb)], 1ull);
 #endif
 #ifdef RT_COUNT_PRIMARY_STEPS // diagnostic build: live lanes per primary march step (scripts/phase_util.py)
@@ -1609,7 +1609,35 @@ __global__ void __launch_bounds__(256) k_debug_noise(const RtConsts* __restrict_
     }
 }
 
+// sky.hlsl:26-36,83-137 for one view direction per thread: (mie, rayleigh, space)
+__global__ void __launch_bounds__(256) k_debug_sky(const RtConsts* __restrict__ k, const uint32_t* __restrict__ perm2d,
+                                                   const float4* __restrict__ grad, const float* __restrict__ dirs,
+                                                   float* __restrict__ out, int n)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
+    load_noise_lds(lds, perm2d, grad, k);
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Ctx c = make_ctx(k, lds);
+    const f3 d = rtm::mk(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+    const SkyColor sc = get_rayleigh_mie(c, d);
+    const float space = get_space_color(c, d);
+    float* o = out + 7 * i;
+    o[0] = sc.mie.x;
+    o[1] = sc.mie.y;
+    o[2] = sc.mie.z;
+    o[3] = sc.rayleigh.x;
+    o[4] = sc.rayleigh.y;
+    o[5] = sc.rayleigh.z;
+    o[6] = space;
+}
+
 } // namespace
+
+void rt_launch_debug_sky(const RtLaunch& a, const float* dirs, float* out, int n)
+{
+    hipLaunchKernelGGL(k_debug_sky, dim3((n + 255) / 256), dim3(256), 0, a.stream, a.consts, a.perm2d, a.grad, dirs, out, n);
+}
 
 void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n)
 {

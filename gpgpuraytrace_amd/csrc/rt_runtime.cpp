@@ -1556,6 +1556,25 @@ extern "C" int rt_debug_noise(rt_compute c, const float* xyz, float* out, int n,
     return RT_OK;
 }
 
+extern "C" int rt_debug_sky(rt_compute c, const float* dirs, float* out, int n)
+{
+    if (!c || !c->shader || !dirs || !out || n <= 0) return fail(RT_ERR_INVALID, "bad arguments");
+    rt_device dev = c->dev;
+    int rc;
+    if ((rc = check_texture(c->shader)) || (rc = sync_shader(dev, c->shader))) return rc;
+    float *dx = nullptr, *dy = nullptr;
+    HIP_TRY(hipMalloc(&dx, (size_t)n * 12));
+    HIP_TRY(hipMalloc(&dy, (size_t)n * 28));
+    HIP_TRY(hipMemcpyAsync(dx, dirs, (size_t)n * 12, hipMemcpyHostToDevice, dev->stream));
+    rt_launch_debug_sky(make_launch(dev, c->shader), dx, dy, n);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, dy, (size_t)n * 28, hipMemcpyDeviceToHost, dev->stream));
+    HIP_TRY(hipStreamSynchronize(dev->stream));
+    HIP_TRY(hipFree(dx));
+    HIP_TRY(hipFree(dy));
+    return RT_OK;
+}
+
 // ---------------------------------------------------------------------------
 // IRecorder / RecorderWinAPI (Factories/IRecorder.h, Adapters/RecorderWinAPI.cpp) over a
 // raw-video sink: Media Foundation's WMV sink writer does not exist here, so the frames

@@ -59,7 +59,10 @@ __device__ __forceinline__ void count_noise(const NoiseView& nz)
 #ifdef RT_COUNT_PHASE
     if (nz.phase != RT_COUNT_PHASE) return;
 #endif
-    const uint64_t ex = __builtin_amdgcn_read_exec();
+    // the active lanes as a ballot (convergent: evaluated where the call is; a plain read of EXEC
+    // can be hoisted out of the FBM loop, crediting later octaves' wave iterations to a lane that
+    // already left it, which undercounted iterations before ABI 4)
+    const uint64_t ex = __ballot(1);
     if (nz.lds_calls) {
         if (__lane_id() == (uint32_t)__builtin_ctzll(ex)) {
             __atomic_fetch_add(&nz.lds_calls[0], (unsigned long long)__popcll(ex), __ATOMIC_RELAXED);

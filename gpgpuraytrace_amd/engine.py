@@ -589,11 +589,12 @@ class FrameRing:
     batch on the first one's stream); render_batch() queues the next B frames."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 graph=False, batch=1, **terrain_kw):
+                 graph=False, batch=1, float_output=False, **terrain_kw):
         self.depth, self.frame, self.batch = int(depth), 0, int(batch)
         self.slots = []
         for _ in range(self.depth * self.batch):
-            dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph)
+            dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph,
+                                          float_output=float_output)
             if dev is None:
                 raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
             ter = Terrain(dev, theme, **terrain_kw)

@@ -251,6 +251,10 @@ int rt_terrain_set_target_depths(const float* camera_results, float* cell_distan
  *   current tables and constants. */
 int rt_debug_math(rt_device dev, int op, const float* a, const float* b, float* out, int n);
 int rt_debug_noise(rt_compute cs, const float* xyz, float* out, int n, int density);
+/* rt_debug_sky (ABI 4): the sky of n view directions (xyz interleaved) with the compute's current
+ *   constants (Eye, SunDirection) and tables: 7 floats per direction, getRayleighMieColor's
+ *   (mie.rgb, rayleigh.rgb) (sky.hlsl:83-137) and getSpaceColor (sky.hlsl:26-36). */
+int rt_debug_sky(rt_compute cs, const float* dirs, float* out, int n);
 
 /* ---- IRecorder (Factories/IRecorder.h; RecorderWinAPI.cpp; RecorderFactory.cpp) ----
  * rt_recorder_create   <- RecorderFactory::construct(device, frameRate, fixedSpeed) + create():

@@ -68,13 +68,41 @@ float ro_min(float a, float b)
 }
 static inline float sat(float x) { return ro_min(ro_max(x, 0.0f), 1.0f); }
 static inline float rcp(float x) { return 1.0f / x; }
-static inline float lerp(float a, float b, float t) { return fmaf(t, b - a, a); }
+
+/* Arithmetic conventions of the HLSL-level operations (rules R2, R3, R5).  The default build is
+ * the restatement the GPU matches bit for bit.  Convention VARIANTS (RO_CONV_*, built only as
+ * separate checker libraries by `make -C oracle variants`, never linked into the product) re-evaluate
+ * the same HLSL with another equally valid reading of it, to bound how far the D3D path's
+ * unknowable choices (fxc mad fusion, div, transcendental precision) can move a frame
+ * (scripts/parity_sensitivity.py, profiles/r03/parity_sensitivity.md):
+ *   RO_CONV_UNFUSED  every HLSL a*b+c (mad, lerp, dot, mul, tracing.hlsl:54) as a rounded product
+ *                    and a rounded add;
+ *   RO_CONV_IEEEDIV  a / b as an IEEE division (not a * rcp(b)); normalize(v) = v / length(v);
+ *   RO_CONV_LIBM     pow / exp / exp2 / log2 / sin / cos from the C library (glibc, ~0.5-1 ulp)
+ *                    instead of the R5 polynomials.
+ * MAD(a,b,c) = a*b + c; DIVADD(a,b,c) = a/b + c; DIVR(a,b) = a/b. */
+#ifdef RO_CONV_UNFUSED
+#define MAD(a, b, c) ((a) * (b) + (c))
+#else
+#define MAD(a, b, c) fmaf((a), (b), (c))
+#endif
+#ifdef RO_CONV_IEEEDIV
+#define DIVR(a, b) ((a) / (b))
+#define DIVADD(a, b, c) ((a) / (b) + (c))
+#else
+#define DIVR(a, b) ((a) * rcp(b))
+#define DIVADD(a, b, c) MAD((a), rcp(b), (c))
+#endif
+static inline float lerp(float a, float b, float t) { return MAD(t, b - a, a); }
 
 /* ------------------------------------------------------------------------ */
 /* R5: polynomial transcendentals.  Coefficients are near-minimax fits,
  * written as hex floats so the HIP path can use the identical constants. */
 float ro_exp2(float x)
 {
+#ifdef RO_CONV_LIBM
+    return exp2f(x);
+#endif
     if (x != x) return x;
     if (x >= 128.0f) return INFINITY;
     if (x < -150.0f) return 0.0f;
@@ -92,6 +120,9 @@ float ro_exp2(float x)
 
 float ro_log2(float x)
 {
+#ifdef RO_CONV_LIBM
+    return log2f(x);
+#endif
     if (x != x) return x;
     if (x < 0.0f) return NAN;
     if (x == 0.0f) return -INFINITY;
@@ -116,8 +147,13 @@ float ro_log2(float x)
     return fmaf(f, p, (float)e);
 }
 
+#ifdef RO_CONV_LIBM
+float ro_pow(float x, float y) { return powf(x, y); }
+float ro_exp(float x) { return expf(x); }
+#else
 float ro_pow(float x, float y) { return ro_exp2(y * ro_log2(x)); }
 float ro_exp(float x) { return ro_exp2(x * 0x1.715476p+0f); }
+#endif
 
 static void sincos_red(float x, float* s, float* c)
 {
@@ -139,8 +175,13 @@ static void sincos_red(float x, float* s, float* c)
     default: *s = -cv; *c = sv; break;
     }
 }
+#ifdef RO_CONV_LIBM
+float ro_sin(float x) { return sinf(x); }
+float ro_cos(float x) { return cosf(x); }
+#else
 float ro_sin(float x) { float s, c; if (x != x || isinf(x)) return NAN; sincos_red(x, &s, &c); return s; }
 float ro_cos(float x) { float s, c; if (x != x || isinf(x)) return NAN; sincos_red(x, &s, &c); return c; }
+#endif
 
 void ro_batch_unary(int op, const float* x, float* y, int64_t n)
 {
@@ -171,11 +212,15 @@ void ro_batch_binary(int op, const float* a, const float* b, float* y, int64_t n
 
 /* ------------------------------------------------------------------------ */
 /* R4 vector helpers */
-static inline float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline float dot3(f3 a, f3 b) { return MAD(a.z, b.z, MAD(a.y, b.y, a.x * b.x)); }
 static inline float len3(f3 a) { return sqrtf(dot3(a, a)); }
 static inline f3 sub3(f3 a, f3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline f3 scale3(f3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+#ifdef RO_CONV_IEEEDIV
+static inline f3 norm3(f3 a) { float l = sqrtf(dot3(a, a)); return v3(a.x / l, a.y / l, a.z / l); }
+#else
 static inline f3 norm3(f3 a) { return scale3(a, rcp(sqrtf(dot3(a, a)))); }
+#endif
 
 /* ------------------------------------------------------------------------ */
 /* Noise tables: Graphics/Noise.cpp:6-24 (g3), :39-56 (generate), :58-61,
@@ -223,6 +268,7 @@ static int crt_rand_next(crt_rand* g)
 void ro_noise_generate(ro_noise* out, uint32_t seed, int rand_kind)
 {
     crt_rand g;
+    memset(&g, 0, sizeof(g));
     crt_srand(&g, seed, rand_kind);
     int32_t* p = out->perm;
     for (int x = 0; x < 128; ++x) p[x] = x;
@@ -258,6 +304,7 @@ typedef struct {
     f3 eye, sun;
     float density_factor, step_factor, one_minus_step_factor, min_limit;
     uint64_t noise_calls, density_calls;
+    float pixel_secondary_steps; /* shadow + AO march iterations of the current pixel (parity study) */
 #ifdef RO_STUDY /* scripts/skip_study.c: which pixel / ray the samples belong to */
     int64_t study_pixel;
 #endif
@@ -281,6 +328,7 @@ static void ctx_init(ctx* c, const ro_noise* nz, const ro_frame* fr)
     c->min_limit = (float)((double)0.02f * (double)0.03f);
     c->noise_calls = 0;
     c->density_calls = 0;
+    c->pixel_secondary_steps = 0.0f;
 #ifdef RO_STUDY
     c->study_pixel = -1;
 #endif
@@ -290,11 +338,11 @@ static void ctx_init(ctx* c, const ro_noise* nz, const ro_frame* fr)
 static inline float gradperm(const ctx* c, uint32_t i, float x, float y, float z)
 {
     const float* g = c->nz->grad + (i % 128u) * 4;
-    return fmaf(g[2], z, fmaf(g[1], y, g[0] * x));
+    return MAD(g[2], z, MAD(g[1], y, g[0] * x));
 }
 
 /* noise.hlsl:139-142 */
-static inline float fade(float t) { return ((t * t) * t) * fmaf(t, fmaf(t, 6.0f, -15.0f), 10.0f); }
+static inline float fade(float t) { return ((t * t) * t) * MAD(t, MAD(t, 6.0f, -15.0f), 10.0f); }
 
 /* noise.hlsl:153-179 (the live `#if 1` block) */
 static float noise3d(ctx* c, float px, float py, float pz)
@@ -356,19 +404,19 @@ static float density_nomadplains(ctx* c, f3 p)
     for (int N = 1; (float)N <= detail; ++N) {
         float S = fbm_scale(1.96f, N);
         float n = noise3d(c, q0.x * S, q0.y * (S * 0.35f), q0.z * S);
-        s = fmaf(n, rcp(S), s); /* s += noise/SCALE  (R2, R3) */
+        s = DIVADD(n, S, s); /* s += noise/SCALE  (R2, R3) */
     }
     const float mountains = 0.1f;
     float expo = 0.68f + mountains;
-    s = ro_pow(fabsf(fmaf(s, 30.0f, 1.0f)) * 35.0f, expo); /* s*=30; pow(abs(s+1)*35, .68+m) */
+    s = ro_pow(fabsf(MAD(s, 30.0f, 1.0f)) * 35.0f, expo); /* s*=30; pow(abs(s+1)*35, .68+m) */
     float steep = sat((noise3d(c, p1.x * 0.007138f, p1.z * 0.007138f, 0.0f) - 0.2f) * 6.0f) * 7.5f;
     float floorsize = steep * 1.8f;
     float t;
-    t = sat((p1.y - 13.0f) * steep); s = fmaf(-(t * t), floorsize, s);
-    t = sat((p1.y - 16.0f) * steep); s = fmaf(-(t * t), floorsize, s);
-    t = sat((p1.y - 19.0f) * steep); s = fmaf(-(t * t), floorsize, s);
-    t = sat((p1.y - 22.0f) * steep); s = fmaf(-(t * t), floorsize, s);
-    s = fmaf(ro_pow(sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
+    t = sat((p1.y - 13.0f) * steep); s = MAD(-(t * t), floorsize, s);
+    t = sat((p1.y - 16.0f) * steep); s = MAD(-(t * t), floorsize, s);
+    t = sat((p1.y - 19.0f) * steep); s = MAD(-(t * t), floorsize, s);
+    t = sat((p1.y - 22.0f) * steep); s = MAD(-(t * t), floorsize, s);
+    s = MAD(ro_pow(sat((-p1.y + 10.0f) * 1.6f), 1.5f), 19.0f, s);
     return d + s;
 }
 
@@ -377,7 +425,7 @@ static float density_testing(ctx* c, f3 p)
 {
     (void)c;
     float d = -p.y;
-    return fmaf(ro_sin(p.x * 0.1f) * ro_cos(p.z * 0.1f), 10.0f, d);
+    return MAD(ro_sin(p.x * 0.1f) * ro_cos(p.z * 0.1f), 10.0f, d);
 }
 
 /* Media/simple/shaders/terrain.hlsl:7-48 */
@@ -387,16 +435,16 @@ static float density_simple(ctx* c, f3 p)
     f3 q = scale3(p, 0.006f);
     float n = noise3d(c, q.x * 1.0f, q.y * 0.0f, q.z * 1.0f) * 150.0f;
     f3 q2 = scale3(p, 0.002f);
-    float w2 = ro_min(ro_max(fmaf(-p.y, 1.5f, 50.0f), 0.0f), 36.0f);
-    n = fmaf(-fmaf(noise3d(c, q2.x, q2.y, q2.z), 0.5f, 0.5f), w2, n);
+    float w2 = ro_min(ro_max(MAD(-p.y, 1.5f, 50.0f), 0.0f), 36.0f);
+    n = MAD(-MAD(noise3d(c, q2.x, q2.y, q2.z), 0.5f, 0.5f), w2, n);
     f3 q3 = scale3(p, 0.003f);
-    float w3 = ro_min(ro_max(fmaf(-p.y, 1.5f, 10.0f), 0.0f), 36.0f);
-    n = fmaf(-fmaf(noise3d(c, q3.x, q3.y, q3.z), 0.5f, 0.5f), w3, n);
+    float w3 = ro_min(ro_max(MAD(-p.y, 1.5f, 10.0f), 0.0f), 36.0f);
+    n = MAD(-MAD(noise3d(c, q3.x, q3.y, q3.z), 0.5f, 0.5f), w3, n);
     /* `dist` is computed but unused (terrain.hlsl:37) */
     f3 q4 = scale3(p, 0.06f);
     for (int N = 1; (float)N <= 1.0f; ++N) {
         float S = fbm_scale(1.96f, N);
-        n = fmaf(noise3d(c, q4.x * S, q4.y * (S * 0.35f), q4.z * S), rcp(S), n);
+        n = DIVADD(noise3d(c, q4.x * S, q4.y * (S * 0.35f), q4.z * S), S, n);
     }
     return d + n;
 }
@@ -409,13 +457,13 @@ static float density_greenrocks(ctx* c, f3 p)
     d = d + -p.y;
     f3 pg = scale3(p, 0.01f);
     float g = noise3d(c, pg.x, pg.y, pg.z);
-    f3 noh = v3(1.0f, fmaf(fabsf(g), 1.4f, 0.1f), 1.0f);
+    f3 noh = v3(1.0f, MAD(fabsf(g), 1.4f, 0.1f), 1.0f);
     f3 pc = v3(p.x * 0.011f, p.y * 0.0013f, p.z * 0.011f);
     float g32 = g * 0.32f;
     for (int N = 1; (float)N <= 7.0f; ++N) {
         float S = fbm_scale(2.0f, N);
-        float n = noise3d(c, fmaf(pc.x, S, g32), fmaf(pc.y, S, g32), fmaf(pc.z, S, g32));
-        d = fmaf((fabsf(n) * 210.0f) * g, rcp(S), d);
+        float n = noise3d(c, MAD(pc.x, S, g32), MAD(pc.y, S, g32), MAD(pc.z, S, g32));
+        d = DIVADD((fabsf(n) * 210.0f) * g, S, d);
     }
     d = d - 50.0f;
     f3 p2 = scale3(p, 0.002f);
@@ -423,8 +471,8 @@ static float density_greenrocks(ctx* c, f3 p)
     for (int N = 1; (float)N <= 5.0f; ++N) {
         float S = fbm_scale(2.0f, N);
         float n = noise3d(c, p2n.x * S, p2n.y * S, p2n.z * S);
-        float inner = fmaf(n + 0.1f, 0.5f, 0.5f);
-        d = fmaf(-inner, 220.0f * rcp(S), d);
+        float inner = MAD(n + 0.1f, 0.5f, 0.5f);
+        d = MAD(-inner, DIVR(220.0f, S), d);
     }
     return d;
 }
@@ -450,12 +498,12 @@ static f4 get_fog(ctx* c, f3 p, float dist)
     if (!fog_live(c)) return r;
     float fogd = 0.0f;
     float d = 0.0f;
-    dist = sat(fmaf(-dist, 0.0012f, 1.0f));
-    float falloff = sat(fmaf(-(dist * dist), 0.1f, 1.0f));
+    dist = sat(MAD(-dist, 0.0012f, 1.0f));
+    float falloff = sat(MAD(-(dist * dist), 0.1f, 1.0f));
     if (falloff > 0.0f) {
         d = d + sat((-p.y - 2.0f) * 0.0003f);
         f3 q = scale3(p, 0.1261f);
-        fogd = fmaf(fabsf(noise3d(c, q.x, q.y, q.z)), 0.2f, 0.8f);
+        fogd = MAD(fabsf(noise3d(c, q.x, q.y, q.z)), 0.2f, 0.8f);
     }
     float fc = 0.9f * fogd;
     r.x = (fc * d) * dist;
@@ -478,16 +526,15 @@ static ray_result trace_ray(ctx* c, f3 p, float dist, float enddist, float stepm
     float total = 0.0f;
     float dirLength = len3(dir);
     /* tracing.hlsl:54: the R2 exception (the subtrahend's product is the fused one) */
-    float step = fmaf(-dist, c->one_minus_step_factor, (0.03f * stepmod) * dirLength);
+    float step = MAD(-dist, c->one_minus_step_factor, (0.03f * stepmod) * dirLength);
     float lastStep = step;
-    float il = rcp(dirLength);
-    dir = scale3(dir, il);
+    dir = v3(DIVR(dir.x, dirLength), DIVR(dir.y, dirLength), DIVR(dir.z, dirLength));
     if (calcfog) {
         float hd = dist * 0.5f;
-        f3 mp = v3(fmaf(dir.x * dist, 0.5f, p.x), fmaf(dir.y * dist, 0.5f, p.y), fmaf(dir.z * dist, 0.5f, p.z));
+        f3 mp = v3(MAD(dir.x * dist, 0.5f, p.x), MAD(dir.y * dist, 0.5f, p.y), MAD(dir.z * dist, 0.5f, p.z));
         f4 mf = get_fog(c, mp, hd);
-        f.x = fmaf(mf.x, dist, f.x); f.y = fmaf(mf.y, dist, f.y);
-        f.z = fmaf(mf.z, dist, f.z); f.w = fmaf(mf.w, dist, f.w);
+        f.x = MAD(mf.x, dist, f.x); f.y = MAD(mf.y, dist, f.y);
+        f.z = MAD(mf.z, dist, f.z); f.w = MAD(mf.w, dist, f.w);
     }
     f3 rayp = v3(0.0f, 0.0f, 0.0f);
     int iters = 0;
@@ -495,7 +542,7 @@ static ray_result trace_ray(ctx* c, f3 p, float dist, float enddist, float stepm
         if (max_steps > 0 && iters >= max_steps) break;
         ++iters;
         total = total + 1.0f;
-        rayp = v3(fmaf(dir.x, dist, p.x), fmaf(dir.y, dist, p.y), fmaf(dir.z, dist, p.z));
+        rayp = v3(MAD(dir.x, dist, p.x), MAD(dir.y, dist, p.y), MAD(dir.z, dist, p.z));
         f4 fs = {0.0f, 0.0f, 0.0f, 0.0f};
         d = get_density(c, rayp);
 #ifdef RO_STUDY
@@ -541,14 +588,14 @@ static f3 get_normal(ctx* c, f4 pd)
 static void get_pixel_ray(const ctx* c, float px, float py, f3* outp, f3* outdir)
 {
     const ro_frame* fr = c->fr;
-    float sx = fmaf(px + 0.5f, rcp((float)fr->width), -0.5f) * 2.0f;
-    float sy = fmaf(py + 0.5f, rcp((float)fr->height), -0.5f) * 2.0f;
+    float sx = DIVADD(px + 0.5f, (float)fr->width, -0.5f) * 2.0f;
+    float sy = DIVADD(py + 0.5f, (float)fr->height, -0.5f) * 2.0f;
     sx = sx * fr->projection[5]; /* Projection._22 */
     sy = sy * fr->projection[0]; /* Projection._11 */
     const float* m = fr->view_inverse;
     float r[3];
     for (int j = 0; j < 3; ++j)
-        r[j] = fmaf(1.0f, m[12 + j], fmaf(1.0f, m[8 + j], fmaf(sy, m[4 + j], sx * m[j])));
+        r[j] = MAD(1.0f, m[12 + j], MAD(1.0f, m[8 + j], MAD(sy, m[4 + j], sx * m[j])));
     *outp = v3(r[0], r[1], r[2]);
     *outdir = sub3(*outp, c->eye);
 }
@@ -598,19 +645,19 @@ static float get_space_color(ctx* c, f3 dir)
     dir = mod_ray_dir(dir);
     if (dir.y <= 0.0f) return 0.0f;
     float space = noise3d(c, dir.x * 500.0f, dir.y * 500.0f, dir.z * 500.0f);
-    space = space - fmaf(noise3d(c, dir.x * 150.2f, dir.y * 150.2f, dir.z * 150.2f), 0.5f, 0.13f);
-    space = space - fmaf(noise3d(c, dir.x * 200.2f, dir.y * 200.2f, dir.z * 200.2f), 0.5f, 0.5f);
-    return (space * 1.0f) * sat(fmaf(-c->sun.y, 2.7f, -0.5f));
+    space = space - MAD(noise3d(c, dir.x * 150.2f, dir.y * 150.2f, dir.z * 150.2f), 0.5f, 0.13f);
+    space = space - MAD(noise3d(c, dir.x * 200.2f, dir.y * 200.2f, dir.z * 200.2f), 0.5f, 0.5f);
+    return (space * 1.0f) * sat(MAD(-c->sun.y, 2.7f, -0.5f));
 }
 
 /* sky.hlsl:39-43 */
 static float sky_scale(float fCos)
 {
     float x = 1.0f - fCos;
-    float t = fmaf(x, 5.25f, -6.80f);
-    t = fmaf(x, t, 3.83f);
-    t = fmaf(x, t, 0.459f);
-    t = fmaf(x, t, -0.00287f);
+    float t = MAD(x, 5.25f, -6.80f);
+    t = MAD(x, t, 3.83f);
+    t = MAD(x, t, 0.459f);
+    t = MAD(x, t, -0.00287f);
     return 0.19f * ro_exp(t);
 }
 
@@ -619,30 +666,29 @@ static float sky_scale(float fCos)
 static sky_color get_rayleigh_mie(const ctx* c, const sky_consts* k, f3 org)
 {
     f3 rd = mod_ray_dir(org);
-    float camHeight = fmaf(c->eye.y, 0.001f, 200.0f);
+    float camHeight = MAD(c->eye.y, 0.001f, 200.0f);
     camHeight = ro_max(camHeight, 0.0f);
     float distToTop = k->outerRadius - camHeight;
-    float far = fmaf((1.0f - rd.y) * distToTop, 2.0f, distToTop);
+    float far = MAD((1.0f - rd.y) * distToTop, 2.0f, distToTop);
     f3 start = v3(c->eye.x * 0.001f, camHeight, c->eye.z * 0.001f);
     float depth = ro_exp(k->scaleOverScaleDepth * (200.0f - camHeight));
     float fStartAngle = dot3(rd, norm3(start));
     float fStartOffset = depth * sky_scale(fStartAngle);
-    float sampleLength = far * k->rcp_samples;
+    float sampleLength = DIVR(far, 3.0f); /* far / fSamples; rcp(3.0f) == k->rcp_samples */
     float scaledLength = sampleLength * k->fScale;
     f3 sampleRay = scale3(rd, sampleLength);
-    f3 sp = v3(fmaf(sampleRay.x, 0.5f, start.x), fmaf(sampleRay.y, 0.5f, start.y), fmaf(sampleRay.z, 0.5f, start.z));
+    f3 sp = v3(MAD(sampleRay.x, 0.5f, start.x), MAD(sampleRay.y, 0.5f, start.y), MAD(sampleRay.z, 0.5f, start.z));
     float front[3] = {0.0f, 0.0f, 0.0f};
     for (int i = 0; i < 3; ++i) {
         float height = len3(sp);
         float dep = ro_exp(k->scaleOverScaleDepth * (200.0f - height));
-        float ih = rcp(height);
-        float fLight = dot3(c->sun, sp) * ih;
-        float fCam = dot3(rd, sp) * ih;
-        float fScatter = fmaf(dep, sky_scale(fLight) - sky_scale(fCam), fStartOffset);
+        float fLight = DIVR(dot3(c->sun, sp), height);
+        float fCam = DIVR(dot3(rd, sp), height);
+        float fScatter = MAD(dep, sky_scale(fLight) - sky_scale(fCam), fStartOffset);
         float ds = dep * scaledLength;
         for (int j = 0; j < 3; ++j) {
             float att = ro_exp(-fScatter * k->att_k[j]);
-            front[j] = fmaf(att, ds, front[j]);
+            front[j] = MAD(att, ds, front[j]);
         }
         sp = v3(sp.x + sampleRay.x, sp.y + sampleRay.y, sp.z + sampleRay.z);
     }
@@ -650,20 +696,37 @@ static sky_color get_rayleigh_mie(const ctx* c, const sky_consts* k, f3 org)
     f3 ray = v3(front[0] * k->fKmESun, front[1] * k->fKmESun, front[2] * k->fKmESun);
     f3 t = v3(-rd.x * far, -rd.y * far, -rd.z * far);
     /* applyPhase(rayleigh := mie, mie := ray, camDir := t) */
-    float fCos = dot3(c->sun, t) * rcp(len3(t));
+    float fCos = DIVR(dot3(c->sun, t), len3(t));
     float fCos2 = fCos * fCos;
-    float mphase = (k->mie_a * (1.0f + fCos2)) * rcp(ro_pow(fabsf(fmaf(-k->two_g, fCos, k->one_plus_g2)), 1.5f));
-    float rphase = fmaf(0.75f, fCos2, 0.75f);
+    float mphase = DIVR(k->mie_a * (1.0f + fCos2), ro_pow(fabsf(MAD(-k->two_g, fCos, k->one_plus_g2)), 1.5f));
+    float rphase = MAD(0.75f, fCos2, 0.75f);
     sky_color sc;
     sc.mie = scale3(ray, mphase);
     sc.rayleigh = scale3(mie, rphase);
-    float m = sat(fmaf(org.y, 0.5f, 0.5f) * 4.0f);
+    float m = sat(MAD(org.y, 0.5f, 0.5f) * 4.0f);
     sc.rayleigh = scale3(sc.rayleigh, m);
     float sy = sat(c->sun.y);
-    sc.rayleigh.z = fmaf(0.6f, sy, sc.rayleigh.z);
-    sc.rayleigh.y = fmaf(0.4f, sy, sc.rayleigh.y);
-    sc.rayleigh.x = fmaf(0.3f, sy, sc.rayleigh.x);
+    sc.rayleigh.z = MAD(0.6f, sy, sc.rayleigh.z);
+    sc.rayleigh.y = MAD(0.4f, sy, sc.rayleigh.y);
+    sc.rayleigh.x = MAD(0.3f, sy, sc.rayleigh.x);
     return sc;
+}
+
+/* sky of n view directions for the known-answer tests: (mie.rgb, rayleigh.rgb, space) each */
+void ro_sky(const ro_noise* nz, const ro_frame* fr, const float* dirs, float* out, int64_t n)
+{
+    sky_consts k;
+    sky_init(&k);
+    ctx c;
+    ctx_init(&c, nz, fr);
+    for (int64_t i = 0; i < n; ++i) {
+        f3 d = v3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]);
+        sky_color sc = get_rayleigh_mie(&c, &k, d);
+        float* o = out + 7 * i;
+        o[0] = sc.mie.x; o[1] = sc.mie.y; o[2] = sc.mie.z;
+        o[3] = sc.rayleigh.x; o[4] = sc.rayleigh.y; o[5] = sc.rayleigh.z;
+        o[6] = get_space_color(&c, d);
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -682,25 +745,25 @@ static f3 get_color(ctx* c, f3 p, f3 n, f3 d, float dist, uint64_t* shadow_steps
             f3 q = v3(p.y * 0.5f, p.x * 0.01f, p.z * 0.01f);
             for (int N = 1; (float)N <= 20.0f; ++N) {
                 float S = fbm_scale(2.03f, N);
-                s = fmaf(fabsf(noise3d(c, q.x * S, q.y * S, q.z * S)), rcp(S), s);
+                s = DIVADD(fabsf(noise3d(c, q.x * S, q.y * S, q.z * S)), S, s);
             }
-            for (int i = 0; i < 4; ++i) col[i] = fmaf(-s, 0.5f, col[i]);
+            for (int i = 0; i < 4; ++i) col[i] = MAD(-s, 0.5f, col[i]);
         } else {
             float detail = ro_max(16.0f - ro_pow(dist, 0.33f), 2.0f);
             f3 q = v3(p.y * 0.5f, p.x * 0.01f, p.z * 0.1f);
             for (int N = 1; (float)N <= detail; ++N) {
                 float S = fbm_scale(2.03f, N);
-                s = fmaf(fabsf(noise3d(c, q.x * S, q.y * S, q.z * S)), rcp(S), s);
+                s = DIVADD(fabsf(noise3d(c, q.x * S, q.y * S, q.z * S)), S, s);
             }
-            float w = ro_max((200.0f - dist) * (float)(1.0 / 200.0), 0.0f);
-            for (int i = 0; i < 4; ++i) col[i] = fmaf(-s, w, col[i]);
+            float w = ro_max(DIVR(200.0f - dist, 200.0f), 0.0f);
+            for (int i = 0; i < 4; ++i) col[i] = MAD(-s, w, col[i]);
         }
         col[3] = 0.2f;
         f3 md = v3(-d.x, -d.y, -d.z);
         /* reflect(n, -d) = n - 2*dot(n,-d)*(-d) */
         float t2 = dot3(n, md);
         t2 = t2 + t2;
-        f3 r = v3(fmaf(-t2, md.x, n.x), fmaf(-t2, md.y, n.y), fmaf(-t2, md.z, n.z));
+        f3 r = v3(MAD(-t2, md.x, n.x), MAD(-t2, md.y, n.y), MAD(-t2, md.z, n.z));
         spec_n_dot = dot3(c->sun, r);
     } else if (ls == RO_TESTING) {
         col[0] = 0.6f; col[1] = 0.5f; col[2] = 0.3f; col[3] = 0.1f;
@@ -714,6 +777,7 @@ static f3 get_color(ctx* c, f3 p, f3 n, f3 d, float dist, uint64_t* shadow_steps
     float precision = ro_max((mipf - 3.2f) * 3.0f, 1.0f) * 8.0f;
     ray_result rr = trace_ray(c, p, 0.4f, 100.0f, precision, c->sun, 1, 1, 0);
     *shadow_steps += (uint64_t)rr.steps;
+    c->pixel_secondary_steps += rr.steps;
     if (rr.density > 0.0f) brightness = brightness * 0.1f;
     else brightness = sat(brightness - rr.fcolord.w);
     float specular = sat(ro_pow(ro_max(spec_n_dot, 0.0f), 40.0f)) * col[3];
@@ -722,7 +786,7 @@ static f3 get_color(ctx* c, f3 p, f3 n, f3 d, float dist, uint64_t* shadow_steps
     static const float shc[4] = {0.08f, 0.12f, 0.14f, 0.6f};
     f3 out;
     float m[3];
-    for (int i = 0; i < 3; ++i) m[i] = fmaf(brightness, (float)(1.0 - (double)shc[i]), shc[i]);
+    for (int i = 0; i < 3; ++i) m[i] = MAD(brightness, (float)(1.0 - (double)shc[i]), shc[i]);
     out.x = col[0] * m[0]; out.y = col[1] * m[1]; out.z = col[2] * m[2];
     return out;
 }
@@ -801,6 +865,7 @@ static float ambient_occlusion(ctx* c, f3 p, f3 n, float dist, uint32_t px, uint
     for (int k = 0; k < ao; ++k) {
         ray_result rr = trace_ray(c, p, 0.4f, RO_AO_END, prec, ao_dir(n, px, py, a, (uint32_t)k), 0, 1, 0);
         *ao_steps += (uint64_t)rr.steps;
+        c->pixel_secondary_steps += rr.steps;
         *ao_rays += 1;
         if (rr.density > 0.0f) occ += 1;
     }
@@ -858,9 +923,8 @@ void ro_camerarays_steps(const ro_noise* nz, const ro_frame* fr, float* camera_r
         ctx c;
         ctx_init(&c, nz, fr);
         int tx = i % 32, ty = i / 32;
-        const float r31 = rcp(31.0f);
-        uint32_t pxs = (uint32_t)(((float)tx * r31) * (float)fr->width);
-        uint32_t pys = (uint32_t)(((float)ty * r31) * (float)fr->height);
+        uint32_t pxs = (uint32_t)(DIVR((float)tx, 31.0f) * (float)fr->width);
+        uint32_t pys = (uint32_t)(DIVR((float)ty, 31.0f) * (float)fr->height);
         f3 p, dir;
         get_pixel_ray(&c, (float)pxs, (float)pys, &p, &dir);
         ray_result rr = trace_ray(&c, p, 0.01f, 5000.0f, 2.0f, dir, 0, 1, 0);
@@ -926,6 +990,12 @@ static inline uint8_t unorm8(float v)
 void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_distance, float* rgba32f,
                     uint8_t* rgba8, float* primary_steps, ro_stats* st)
 {
+    ro_tracescreen2(nz, fr, cell_distance, rgba32f, rgba8, primary_steps, NULL, st);
+}
+
+void ro_tracescreen2(const ro_noise* nz, const ro_frame* fr, const float* cell_distance, float* rgba32f,
+                     uint8_t* rgba8, float* primary_steps, float* secondary_steps, ro_stats* st)
+{
     sky_consts k;
     sky_init(&k);
     int W = fr->width, H = fr->height;
@@ -948,11 +1018,12 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
             c.study_pixel = (int64_t)y * W + x;
 #endif
             float pxf = (float)x, pyf = (float)y;
-            float spx = pxf * rcp((float)W), spy = pyf * rcp((float)H);
-            uint32_t cell = (uint32_t)fmaf(floorf(spy * 32.0f), 32.0f, floorf(spx * 32.0f));
+            float spx = DIVR(pxf, (float)W), spy = DIVR(pyf, (float)H);
+            uint32_t cell = (uint32_t)MAD(floorf(spy * 32.0f), 32.0f, floorf(spx * 32.0f));
             float plane_x = cell_distance[2 * cell], plane_y = 5000.0f;
             float col[3] = {0.0f, 0.0f, 0.0f};
             float steps = 0.0f;
+            c.pixel_secondary_steps = 0.0f;
             for (int a = 0; a < aa; ++a) {
                 f3 p, dir;
                 get_pixel_ray(&c, pxf + offs[a][0] * (1.0f / 16.0f), pyf + offs[a][1] * (1.0f / 16.0f), &p, &dir);
@@ -972,8 +1043,7 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
                 }
                 rays += 1;
             }
-            float ia = rcp((float)aa);
-            col[0] *= ia; col[1] *= ia; col[2] *= ia;
+            col[0] = DIVR(col[0], (float)aa); col[1] = DIVR(col[1], (float)aa); col[2] = DIVR(col[2], (float)aa);
             size_t o = (size_t)y * W + x;
             if (rgba32f) {
                 rgba32f[4 * o + 0] = col[0]; rgba32f[4 * o + 1] = col[1];
@@ -984,6 +1054,7 @@ void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_di
                 rgba8[4 * o + 2] = unorm8(col[2]); rgba8[4 * o + 3] = 255;
             }
             if (primary_steps) primary_steps[o] = steps;
+            if (secondary_steps) secondary_steps[o] = c.pixel_secondary_steps;
         }
         noise += c.noise_calls;
         dens += c.density_calls;

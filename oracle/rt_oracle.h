@@ -98,9 +98,17 @@ void ro_set_target_depths(const float* camera_results, float* cell_distance);
  * untouched.  Any output pointer may be NULL. */
 void ro_tracescreen(const ro_noise* nz, const ro_frame* fr, const float* cell_distance,
                     float* rgba32f, uint8_t* rgba8, float* primary_steps, ro_stats* st);
+/* The same with each pixel's shadow + AO march iterations in secondary_steps (W*H, may be NULL). */
+void ro_tracescreen2(const ro_noise* nz, const ro_frame* fr, const float* cell_distance, float* rgba32f,
+                     uint8_t* rgba8, float* primary_steps, float* secondary_steps, ro_stats* st);
 /* Whole frame: prepass + depths + tracescreen. */
 void ro_render_frame(const ro_noise* nz, const ro_frame* fr, float* camera_results, float* cell_distance,
                      float* rgba32f, uint8_t* rgba8, float* primary_steps, ro_stats* st);
+
+/* Sky of n view directions (dirs xyz interleaved) under fr's Eye / SunDirection: 7 floats per
+ * direction, getRayleighMieColor (mie.rgb, rayleigh.rgb; sky.hlsl:83-137) and getSpaceColor
+ * (sky.hlsl:26-36).  Known-answer tests (SURVEY 8c iv) check it against a float64 restatement. */
+void ro_sky(const ro_noise* nz, const ro_frame* fr, const float* dirs, float* out, int64_t n);
 
 /* Output path: RecorderWinAPI::write's conversion of the R8G8B8A8
  * backbuffer rows (RecorderWinAPI.cpp:244-253) into MFVideoFormat_RGB32 DWORDs, and the

@@ -47,12 +47,31 @@ def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR, "all"], check=True)
 
 
+_variants = {}
+
+
+def variant(name):
+    """An arithmetic-convention variant of the checker (oracle/rt_oracle.c RO_CONV_*: "unfused",
+    "ieeediv", "libm", "all"), for the parity-sensitivity study; same API as lib()."""
+    if name not in _variants:
+        path = os.path.join(ORACLE_DIR, "_build", f"librt_oracle_{name}.so")
+        if not os.path.exists(path):
+            subprocess.run(["make", "-s", "-C", ORACLE_DIR, "variants"], check=True)
+        _variants[name] = _configure(C.CDLL(path))
+    return _variants[name]
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = C.CDLL(LIB_PATH)
+        _lib = _configure(C.CDLL(LIB_PATH))
+    return _lib
+
+
+def _configure(L):
+    if True:
         fp = C.POINTER(C.c_float)
         L.ro_noise_generate.argtypes = [C.POINTER(Noise), C.c_uint32, C.c_int]
         for n in ("ro_exp2", "ro_log2", "ro_exp", "ro_sin", "ro_cos"):
@@ -72,12 +91,14 @@ def lib():
         L.ro_set_target_depths.argtypes = [fp, fp]
         L.ro_tracescreen.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.POINTER(C.c_uint8), fp,
                                      C.POINTER(Stats)]
+        L.ro_tracescreen2.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.POINTER(C.c_uint8), fp, fp,
+                                      C.POINTER(Stats)]
         L.ro_render_frame.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, fp, C.POINTER(C.c_uint8), fp,
                                       C.POINTER(Stats)]
         L.ro_bgrx.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        L.ro_sky.argtypes = [C.POINTER(Noise), C.POINTER(Frame), fp, fp, C.c_int64]
         L.ro_sample_times.argtypes = [C.c_int, C.c_int, fp, C.c_int, C.c_void_p, C.c_void_p]
-        _lib = L
-    return _lib
+    return L
 
 
 def bgrx(frame):
@@ -146,6 +167,14 @@ def make_frame(consts, landscape=NOMADPLAINS, aa=1, recording=0, max_steps=0, ro
     return fr
 
 
+def sky(nz, fr, dirs):
+    """(n, 7) float32: getRayleighMieColor (mie rgb, rayleigh rgb) and getSpaceColor per direction."""
+    d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    out = np.empty((len(d), 7), np.float32)
+    lib().ro_sky(C.byref(nz), C.byref(fr), _fp(d), _fp(out), len(d))
+    return out
+
+
 def density(nz, fr, xyz):
     xyz = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
     out = np.empty(len(xyz), np.float32)
@@ -153,8 +182,10 @@ def density(nz, fr, xyz):
     return out
 
 
-def render(nz, fr):
-    """Full frame (prepass + setTargetDepths + tracescreen). Returns dict of arrays + stats."""
+def render(nz, fr, L=None):
+    """Full frame (prepass + setTargetDepths + tracescreen). Returns dict of arrays + stats.
+    L: a variant() library instead of the checker."""
+    L = L or lib()
     W, H = fr.width, fr.height
     cr = np.zeros(1024 * 4, np.float32)
     cd = np.zeros(1024 * 2, np.float32)
@@ -162,24 +193,27 @@ def render(nz, fr):
     rgba8 = np.zeros((H, W, 4), np.uint8)
     steps = np.zeros((H, W), np.float32)
     st = Stats()
-    lib().ro_render_frame(C.byref(nz), C.byref(fr), _fp(cr), _fp(cd), _fp(rgba),
+    L.ro_render_frame(C.byref(nz), C.byref(fr), _fp(cr), _fp(cd), _fp(rgba),
                           rgba8.ctypes.data_as(C.POINTER(C.c_uint8)), _fp(steps), C.byref(st))
     return {"camera_results": cr.reshape(1024, 4), "cell_distance": cd.reshape(1024, 2), "rgba32f": rgba,
             "rgba8": rgba8, "primary_steps": steps, "stats": st.as_dict()}
 
 
-def render_rows(nz, fr):
+def render_rows(nz, fr, L=None, steps=None, secondary_steps=None):
     """Prepass + setTargetDepths + tracescreen on fr's rows (row_begin::row_step) only.
     Returns (rgba32f, rgba8, camera_results, cell_distance, stats); rows outside the sample
-    stay zero."""
+    stay zero.  L: a variant() library; steps / secondary_steps: (H, W) float32 arrays that
+    receive each pixel's primary / shadow + AO march iterations."""
+    L = L or lib()
     W, H = fr.width, fr.height
     cr = np.zeros(1024 * 4, np.float32)
     cd = np.zeros(1024 * 2, np.float32)
     rgba = np.zeros((H, W, 4), np.float32)
     rgba8 = np.zeros((H, W, 4), np.uint8)
     st = Stats()
-    lib().ro_camerarays(C.byref(nz), C.byref(fr), _fp(cr), C.byref(st))
-    lib().ro_set_target_depths(_fp(cr), _fp(cd))
-    lib().ro_tracescreen(C.byref(nz), C.byref(fr), _fp(cd), _fp(rgba), rgba8.ctypes.data_as(C.POINTER(C.c_uint8)),
-                         None, C.byref(st))
+    L.ro_camerarays(C.byref(nz), C.byref(fr), _fp(cr), C.byref(st))
+    L.ro_set_target_depths(_fp(cr), _fp(cd))
+    L.ro_tracescreen2(C.byref(nz), C.byref(fr), _fp(cd), _fp(rgba), rgba8.ctypes.data_as(C.POINTER(C.c_uint8)),
+                      _fp(steps) if steps is not None else None,
+                      _fp(secondary_steps) if secondary_steps is not None else None, C.byref(st))
     return rgba, rgba8, cr.reshape(1024, 4), cd.reshape(1024, 2), st.as_dict()
