@@ -68,3 +68,29 @@ def test_native_server_empty_registry_and_unknown_variable():
     finally:
         G.VariableManager.stop()
     G.VariableManager.stop()  # idempotent
+
+
+def test_native_server_survives_malformed_clients():
+    """Untrusted bytes on the live-tweak port (VariableManager.cpp:144-185 reads a name length byte,
+    the name and the variable's bytes): random and truncated packets, zero-length and maximal names,
+    clients that vanish mid-packet.  The server must close such clients and keep serving; run under
+    ASan + UBSan by scripts/sanitize_cpu.sh."""
+    import gpgpuraytrace_amd as G
+    rng = np.random.default_rng(7)
+    port = _free_port()
+    G.VariableManager.start(port)
+    try:
+        payloads = [b"", bytes([0]), bytes([255]), bytes([255]) + b"A" * 255, bytes([200]) + b"x" * 10,
+                    bytes([4]) + b"Nope", bytes([12]) + b"SunDirection"]
+        payloads += [rng.integers(0, 256, size=int(n), dtype=np.uint8).tobytes() for n in rng.integers(1, 600, 24)]
+        for p in payloads:
+            s = socket.create_connection(("127.0.0.1", port), timeout=5.0)
+            s.sendall(p)
+            s.close()
+        # still serving: a well-formed client is accepted and gets its (empty) registry
+        cl = VC.VariableClient("127.0.0.1", port)
+        cl.sock.settimeout(2.0)
+        cl.close()
+        assert G.VariableManager.count() == 0
+    finally:
+        G.VariableManager.stop()
