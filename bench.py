@@ -280,19 +280,18 @@ def main():
     plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass)
     coll = P.Collectives(dist, backend, rank, world)
     dev_str = f"cuda:{local}"
-    bufs = {}
+    # a batch's devices share its stream (FrameRing): every op of a batch rides on it
+    bufs = {g: {"stream": torch.cuda.ExternalStream(ring.slots[g * B][0].stream(), device=dev_str)}
+            for g in range(ring.depth)}
     if world > 1:
         pre_group = dist.new_group(backend=backend) if plan.split_prepass else None
         for g in range(ring.depth):
-            first_dev = ring.slots[g * B][0]
-            bufs[g] = {
-                # a batch's devices share its stream (FrameRing): every op of a batch rides on it
-                "stream": torch.cuda.ExternalStream(first_dev.stream(), device=dev_str),
+            bufs[g].update({
                 "packed": torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device=dev_str),
                 "gathered": [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device=dev_str)
                              for _ in range(world)] if rank == 0 else None,
                 "cams": torch.zeros(plan.camera_floats(), dtype=torch.float32, device=dev_str),
-            }
+            })
 
     class DeviceOps:
         """run_batch's actions on this GPU: HIP kernels through the C-ABI, RCCL collectives."""
@@ -335,8 +334,21 @@ def main():
             for d in self.devs:
                 d.present()
 
-    def batch_step(n):
-        P.run_batch(plan, rank, DeviceOps(n), frames=n)
+    timed_marks, timed_t0 = [], []  # per timed batch: run_batch's phase marks (HIP events) and its stream's t0
+
+    def batch_step(n, timed=False):
+        ops = DeviceOps(n)
+        mark = None
+        if timed:
+            marks, stream = [], ops.b["stream"]
+
+            def mark(name):
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(stream)
+                marks.append((name, ev))
+            timed_marks.append(marks)
+            timed_t0.append(t0_events[ops.g])
+        P.run_batch(plan, rank, ops, frames=n, mark=mark)
         ring.frame += B
 
     progress(rank, "warmup")
@@ -347,9 +359,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     progress(rank, f"timed: {len(sizes)} batches")
+    # the timed region's start on every batch stream (the phase marks' time base)
+    t0_events = []
+    for g in range(ring.depth):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(bufs[g]["stream"])
+        t0_events.append(ev)
     t0 = time.perf_counter()
     for n in sizes:
-        batch_step(n)
+        batch_step(n, timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -439,10 +457,17 @@ def main():
             "ms_per_frame": round(dt / a.steps * 1e3, 4), "rays_per_frame": rc["rays"],
             "how": "--config ref: the same frames and batching, uncapped march (tracing.hlsl:68), no AO"}
 
+    # this rank's phases of the timed batches (HIP events on each batch's stream, from the common
+    # start barrier) and its tracescreen launch time; rank 0 reports every rank's (config.per_rank)
+    phases = P.phase_summary(timed_marks, lambda x, y: x.elapsed_time(y), t0=timed_t0)
+    phases.update({"rank": rank, "tracescreen_kernel_ms": round(k_avg_ms, 4)})
+    per_rank = [phases]
     if world > 1:
         t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=dev_str if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, latency_ms = float(t[0].item()), float(t[1].item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, phases)
 
     ms_per_frame = elapsed / a.steps * 1e3
     value = rays_per_frame * a.steps / elapsed / 1e6
@@ -489,6 +514,12 @@ def main():
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
                               else "direct launches",
                 "frame_latency_ms": round(latency_ms, 4),  # one batch of B frames at a time
+                # per rank: mean / max ms per timed batch of each run_batch phase on the batch's stream
+                # (prepass, all_gather, trace, pack, gather, unpack; waits for the other batch in flight
+                # included), each batch's trace start from the common start barrier, and the rank's
+                # tracescreen launch (roofline pass); trace_start_skew_ms = per batch max - min over ranks
+                "per_rank": per_rank,
+                **({"trace_start_skew_ms": P.start_skew(per_rank)} if world > 1 else {}),
                 **companions,
                 **({"verify": f"all {sizes[-1]} frames of the last timed batch equal a whole-frame render on one "
                               f"device" if not verify else {"MISMATCH": verify}}

@@ -137,28 +137,77 @@ class BatchPlan:
         return [(src, f, self.shard(src, f), self.pack_offset(f)) for src in range(1, self.world) for f in range(n)]
 
 
-def run_batch(plan, rank, ops, frames=None):
+def run_batch(plan, rank, ops, frames=None, mark=None):
     """One batch on this rank.  `ops` supplies the actions (bench.py: HIP + RCCL; tests: numpy
     + gloo): prepass(first, count), all_gather_cameras(), trace(), render() (prepass + trace of
     every frame, the unsplit path), pack_batch([(f, shard, offset)]) (this rank's frames; one
     rt_shard_pack_batch launch on the GPU), gather(), unpack_batch([(src, f, shard, offset)])
     (rank 0: every other rank's frames in one rt_shard_unpack_batch launch), present().
-    `frames` < plan.batch renders a partial batch (its first frames)."""
+    `frames` < plan.batch renders a partial batch (its first frames).
+    mark(name), if given, is called at the start ("start") and after each phase ("prepass",
+    "all_gather", "trace", "pack", "gather", "unpack"): bench.py records a HIP event on the
+    batch's stream there (PHASES; phase_summary turns the marks into per-phase times)."""
     n = plan.batch if frames is None else int(frames)
+    mark = mark or (lambda name: None)
+    mark("start")
     if plan.split_prepass:
         first, count = plan.prepass_range(rank)
         count = max(0, min(count, n - first))
         ops.prepass(first, count)
+        mark("prepass")
         ops.all_gather_cameras()
+        mark("all_gather")
         ops.trace()
     else:
         ops.render()
+    mark("trace")
     if plan.world > 1:
         ops.pack_batch(plan.packs(rank, n))
+        mark("pack")
         ops.gather()
+        mark("gather")
         if rank == 0:
             ops.unpack_batch(plan.unpacks(n))
+            mark("unpack")
     ops.present()
+
+
+PHASES = ("prepass", "all_gather", "trace", "pack", "gather", "unpack")
+
+
+def phase_summary(batches, elapsed_ms, t0=None):
+    """Per-phase times of one rank's batches.  batches: per batch the [(name, clock)] marks of
+    run_batch (a HIP event or a host time); elapsed_ms(a, b): ms from clock a to clock b; t0: the
+    clock the timed region started at (per batch, or one for all), for each batch's trace start.
+    Returns {"batches", "phase_ms" (mean per batch), "phase_ms_max", "trace_start_ms" (per batch,
+    from t0: the prepass + all-gather end; the batch start when the prepass is not split)}.  A
+    phase's time is from the previous mark: it includes any wait of the batch's stream for the
+    other batch in flight (the co-scheduling DESIGN.md section 7 describes)."""
+    per = {p: [] for p in PHASES}
+    starts = []
+    for i, marks in enumerate(batches):
+        for (_, a), (name, b) in zip(marks, marks[1:]):
+            per[name].append(elapsed_ms(a, b))
+        if t0 is not None:
+            z = t0[i] if isinstance(t0, (list, tuple)) else t0
+            names = [m[0] for m in marks]
+            at = marks[names.index("all_gather")][1] if "all_gather" in names else marks[0][1]
+            starts.append(elapsed_ms(z, at))
+    out = {"batches": len(batches),
+           "phase_ms": {p: round(float(sum(v) / len(v)), 4) for p, v in per.items() if v},
+           "phase_ms_max": {p: round(float(max(v)), 4) for p, v in per.items() if v}}
+    if t0 is not None:
+        out["trace_start_ms"] = [round(float(x), 4) for x in starts]
+    return out
+
+
+def start_skew(per_rank):
+    """Per batch: the spread (max - min over ranks) of the trace start, from the ranks'
+    phase_summary()s (their t0 is the common barrier that starts the timed region)."""
+    starts = [r["trace_start_ms"] for r in per_rank if "trace_start_ms" in r]
+    if not starts:
+        return []
+    return [round(max(c) - min(c), 4) for c in zip(*starts)]
 
 
 class Collectives:

@@ -3,6 +3,7 @@ runs on N GPUs: tile-cyclic ownership, per-rank packing, ONE gather to rank 0,
 unpack, and the max-over-ranks timing reduction.  The GPU pack/unpack kernels
 implement the same mapping (checked on the GPU in test_gpu_parity.py)."""
 import os
+import time
 import socket
 
 import numpy as np
@@ -170,11 +171,19 @@ def _batch_worker(rank, world, port, w, h, batch, frames, split, q):
         coll = P.Collectives(dist, "gloo", rank, world)
         group = dist.new_group(backend="gloo") if plan.split_prepass else None
         ops = HostOps(plan, rank, coll, w, h, frames, group)
-        P.run_batch(plan, rank, ops, frames=frames)
+        # bench.py's per-rank phase report, with host clocks in place of HIP events
+        dist.barrier()
+        t0 = time.perf_counter()
+        marks = []
+        P.run_batch(plan, rank, ops, frames=frames, mark=lambda name: marks.append((name, time.perf_counter())))
+        phases = P.phase_summary([marks], lambda a, b: (b - a) * 1e3, t0=t0)
+        phases["rank"] = rank
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, phases)
         if rank == 0:
             ok = all(np.array_equal(ops.frames[f], synthetic_batch_frame(w, h, f, synthetic_cameras(f)))
                      for f in range(frames))
-            q.put((ok, ops.log))
+            q.put((ok, ops.log, per_rank, P.start_skew(per_rank)))
     finally:
         dist.destroy_process_group()
 
@@ -202,7 +211,7 @@ def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
     for p in procs:
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    ok, log = q.get(timeout=10)
+    ok, log, per_rank, skew = q.get(timeout=10)
     assert ok
     from gpgpuraytrace_amd import parallel as P
     plan = P.BatchPlan(w, h, batch, world, split_prepass=split)
@@ -212,6 +221,15 @@ def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
         assert log[0] == ("render",)
     # rank 0: one pack of its frames, one unpack of every other rank's (one launch each on the GPU)
     assert ("pack_batch", frames) in log and ("unpack_batch", (world - 1) * frames) in log
+    # bench.py's config.per_rank / trace_start_skew_ms (make the first 8-GPU run diagnosable)
+    assert [r["rank"] for r in per_rank] == list(range(world))
+    want = (["prepass", "all_gather"] if plan.split_prepass else []) + ["trace", "pack", "gather"]
+    for r in per_rank:
+        keys = want + (["unpack"] if r["rank"] == 0 else [])
+        assert sorted(r["phase_ms"]) == sorted(keys) and sorted(r["phase_ms_max"]) == sorted(keys)
+        assert all(v >= 0.0 for v in r["phase_ms"].values()) and r["batches"] == 1
+        assert len(r["trace_start_ms"]) == 1 and r["trace_start_ms"][0] >= 0.0
+    assert len(skew) == 1 and skew[0] >= 0.0
 
 
 def test_batch_plan_bookkeeping():
