@@ -91,8 +91,10 @@ def parse():
                          "at N>1)")
     ap.add_argument("--cpu-row-step", type=int, default=None, help="CPU baseline (all cores): every n-th row")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = the host's share)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02", "traffic.json"),
-                    help="PMC-derived HBM bytes per tracescreen launch (from rocprofv3 --pmc), if present")
+    ap.add_argument("--traffic", choices=["pmc", "off"], default="pmc",
+                    help="pmc (N=1): measure roofline.traffic in this run, two rocprofv3 --pmc passes (FETCH_SIZE, "
+                         "WRITE_SIZE) over one B-frame tracescreen launch in child processes; off: null")
+    ap.add_argument("--traffic-child", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
     preset = CONFIGS[a.config]
     for key in ("width", "height", "max_steps", "ao"):
@@ -175,6 +177,74 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
     return out, parity
 
 
+TRAFFIC_KERNELS = ("k_order", "k_trace", "k_shade_pre", "k_shadow", "k_finish")
+
+
+def traffic_child(a):
+    """--traffic-child: what the PMC passes profile: two B-frame batches, one in flight (the first
+    warms up; the second is the launch measured)."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    euler = G.camera.INITIAL_ROTATION_EULER if a.pose == "reset" else G.camera.LOOKDOWN_ROTATION_EULER
+    B = max(1, min(16, a.batch))
+    ring = E.FrameRing(a.width, a.height, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
+                       time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
+    for _ in range(2):
+        ring.render_batch()
+    ring.synchronize()
+    ring.destroy()
+
+
+def measure_traffic(a, B):
+    """HBM bytes of one B-frame tracescreen launch, measured now: rocprofv3 --pmc FETCH_SIZE and
+    --pmc WRITE_SIZE (separate passes: the two do not fit the 4 TCC slots of one) over
+    `bench.py --traffic-child` child processes (children, never an exec of this GPU process), the
+    uninstrumented tracescreen kernels of the second (measured) launch, 2 * FETCH_SIZE + WRITE_SIZE
+    (MI355X_MICROARCH.md HBM: gfx950 FETCH_SIZE tallies half the bytes of these loads;
+    profiles/r02/hbm_counter_calibration.txt).  Returns (bytes or None, note)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    work = tempfile.mkdtemp(prefix="bench_traffic_", dir="/tmp")
+    child = [sys.executable, os.path.abspath(__file__), "--traffic-child", "--config", a.config, "--width", str(a.width),
+             "--height", str(a.height), "--landscape", a.landscape, "--pose", a.pose, "--max-steps", str(a.max_steps),
+             "--ao", str(a.ao), "--batch", str(B), "--graph", str(a.graph)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    kib = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(work, counter)
+            r = subprocess.run([prof, "--pmc", counter, "--output-format", "csv", "-d", out, "-o", "run", "--"] + child,
+                               cwd="/tmp", env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=180)
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} rc={r.returncode}: {r.stderr.decode(errors='replace')[-200:]}"
+            per = {}
+            for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
+                for row in csv.DictReader(open(f)):
+                    name = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+                    key = (int(row["Dispatch_Id"]), name)
+                    per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
+            orders = sorted(d for d, n in per if n.startswith("k_order"))
+            if len(orders) < 2:
+                return None, f"rocprofv3 --pmc {counter}: {len(orders)} tracescreen launches in the trace"
+            last = orders[len(orders) // 2]  # k_order of the second (measured) launch; one workgroup per frame
+            kib[counter] = sum(v for (d, n), v in per.items()
+                               if d >= last and n.startswith(TRAFFIC_KERNELS) and "true" not in n)
+    except (subprocess.TimeoutExpired, OSError, KeyError, ValueError) as e:
+        return None, f"traffic pass failed: {type(e).__name__}: {e}"
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+    return int((2.0 * kib["FETCH_SIZE"] + kib["WRITE_SIZE"]) * 1024), (
+        f"measured in this run: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes over one {B}-frame launch "
+        f"({' + '.join(TRAFFIC_KERNELS)}), 2 * FETCH_SIZE + WRITE_SIZE = {2 * kib['FETCH_SIZE'] / 1024:.1f} + "
+        f"{kib['WRITE_SIZE'] / 1024:.1f} MiB")
+
+
 def progress(rank, msg):
     """One progress line on stderr (the JSON line stays alone on stdout)."""
     print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
@@ -182,6 +252,8 @@ def progress(rank, msg):
 
 def main():
     a = parse()
+    if a.traffic_child:
+        return traffic_child(a)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -473,15 +545,11 @@ def main():
     value = rays_per_frame * a.steps / elapsed / 1e6
     batch_noise = counts["batch_noise"]
     achieved = batch_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
-    traffic = None  # measured for whole frames (one GPU); a rank's shard launch has no entry
-    if world == 1 and os.path.exists(a.traffic_json):
-        try:
-            with open(a.traffic_json) as f:
-                tj = json.load(f)
-            key = f"{W}x{H}_{a.landscape}_{a.pose}_ms{a.max_steps}_ao{a.ao}_b{B}"
-            traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = None
+    traffic, traffic_how = None, "not measured (N>1: a rank's launch traces a shard; or --traffic off)"
+    if world == 1 and a.traffic == "pmc":
+        progress(rank, "traffic: rocprofv3 FETCH_SIZE / WRITE_SIZE passes")
+        traffic, traffic_how = measure_traffic(a, B)
+        progress(rank, f"traffic: {traffic}")
 
     if rank == 0:
         preset = CONFIGS[a.config]
@@ -528,6 +596,8 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_FP32_VECTOR_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_VECTOR_TFLOPS, 4), "traffic": traffic,
+                "traffic_how": traffic_how,
+                **({"traffic_per_frame_vs_rgba8": round(traffic / B / (W * H * 4), 2)} if traffic else {}),
                 "kernel": TRACESCREEN_KERNELS, "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
                 "timing": "HIP events per launch on its stream, one batch in flight (the last "
                           f"{kn} tracescreen launches of the run; one launch = {B} frames)",

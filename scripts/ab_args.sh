@@ -9,7 +9,7 @@ fi
 n=0
 for args in "$@"; do
   n=$((n+1))
-  timeout -k 10 200 python3 bench.py --no-cpu-baseline $args > gpurun_out/aba/b$n.json 2> gpurun_out/aba/b$n.err || { echo "bench $n failed"; exit 1; }
+  timeout -k 10 200 python3 bench.py --no-cpu-baseline --traffic off $args > gpurun_out/aba/b$n.json 2> gpurun_out/aba/b$n.err || { echo "bench $n failed"; exit 1; }
   python3 - "$args" gpurun_out/aba/b$n.json <<'PY'
 import json, sys
 b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/abb
 n=0
 for setting in "$@"; do
   n=$((n+1))
-  env $setting timeout -k 10 200 python3 scripts/with_variant.py bench.py --no-cpu-baseline --no-companions $BENCH_ARGS > gpurun_out/abb/b$n.json 2> gpurun_out/abb/b$n.err || { echo "bench $n failed"; tail -3 gpurun_out/abb/b$n.err; exit 1; }
+  env $setting timeout -k 10 200 python3 scripts/with_variant.py bench.py --no-cpu-baseline --traffic off --no-companions $BENCH_ARGS > gpurun_out/abb/b$n.json 2> gpurun_out/abb/b$n.err || { echo "bench $n failed"; tail -3 gpurun_out/abb/b$n.err; exit 1; }
   python3 - "$setting" gpurun_out/abb/b$n.json <<'PY'
 import json, re, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -12,6 +12,6 @@ bash scripts/profile_round.sh > gpurun_out/profile_round.log 2>&1 || { tail -5 g
 tail -3 gpurun_out/profile_round.log
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -s KILL 120 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE \
-  --output-format csv -d gpurun_out/icache -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+  --output-format csv -d gpurun_out/icache -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --traffic off \
   --frames-in-flight 1 > gpurun_out/icache.log 2>&1
 echo "icache pass rc=$?"

@@ -6,9 +6,9 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/pmcab; rm -rf $O; mkdir -p $O
 for v in "$@"; do
   tag=${v:-default}
-  RT_LIB_VARIANT=$v timeout -k 10 200 python3 scripts/with_variant.py bench.py --no-cpu-baseline > $O/$tag.json 2> $O/$tag.err || { echo "bench $tag failed"; exit 1; }
+  RT_LIB_VARIANT=$v timeout -k 10 200 python3 scripts/with_variant.py bench.py --no-cpu-baseline --traffic off > $O/$tag.json 2> $O/$tag.err || { echo "bench $tag failed"; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
-    RT_LIB_VARIANT=$v timeout -k 10 200 rocprofv3 --pmc $c --output-format csv -d $O/$tag-$c -o run -- python3 scripts/with_variant.py bench.py --steps 3 --warmup 1 --no-cpu-baseline --frames-in-flight 1 > $O/$tag-$c.log 2>&1 || { echo "pmc $tag $c failed"; exit 1; }
+    RT_LIB_VARIANT=$v timeout -k 10 200 rocprofv3 --pmc $c --output-format csv -d $O/$tag-$c -o run -- python3 scripts/with_variant.py bench.py --steps 3 --warmup 1 --no-cpu-baseline --traffic off --frames-in-flight 1 > $O/$tag-$c.log 2>&1 || { echo "pmc $tag $c failed"; exit 1; }
   done
   python3 - $O $tag <<'PY'
 import csv, glob, json, sys, collections

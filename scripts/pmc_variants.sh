@@ -8,7 +8,7 @@ O=gpurun_out/pmcv; rm -rf $O; mkdir -p $O
 for v in "$@"; do
   tag=${v:-default}
   RT_LIB_VARIANT=$v timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
-    --output-format csv -d $O/$tag -o run -- python3 scripts/with_variant.py bench.py --steps 12 --warmup 1 --no-cpu-baseline --no-companions --frames-in-flight 1 > $O/$tag.log 2>&1 || { echo "pmc $tag failed"; exit 1; }
+    --output-format csv -d $O/$tag -o run -- python3 scripts/with_variant.py bench.py --steps 12 --warmup 1 --no-cpu-baseline --traffic off --no-companions --frames-in-flight 1 > $O/$tag.log 2>&1 || { echo "pmc $tag failed"; exit 1; }
   python3 - $O/$tag $tag <<'PY'
 import csv, glob, sys, collections
 per = collections.defaultdict(lambda: collections.defaultdict(float))

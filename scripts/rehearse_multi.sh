@@ -7,7 +7,7 @@ export RT_BENCH_SAME_GPU=1 RT_DIST_BACKEND=gloo RT_BENCH_WATCHDOG=60
 PORT=29500
 run() { local n=$1; shift; PORT=$((PORT + 1))
   timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
-    --master-port $PORT bench.py --gpus $n --verify --no-cpu-baseline "$@" > gpurun_out/reh/$PORT.json \
+    --master-port $PORT bench.py --gpus $n --verify --no-cpu-baseline --traffic off "$@" > gpurun_out/reh/$PORT.json \
     2> >(tee gpurun_out/reh/$PORT.err | grep --line-buffered -E "bench rank|Thread|File" >&2) \
     || { echo "n=$n failed"; tail -20 gpurun_out/reh/$PORT.err; return 1; }
   tail -1 gpurun_out/reh/$PORT.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['n_gpus'], d['config']['parallelism'], '->', d['config'].get('verify'))"
