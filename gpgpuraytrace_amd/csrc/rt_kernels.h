@@ -5,8 +5,8 @@
 
 #include "rt_types.h"
 
-// work counters (one 64-byte block, zeroed per launch)
-enum { RT_CTR_PRIMARY = 0, RT_CTR_HITS = 1, RT_CTR_SHADE = 2, RT_CTR_FINISH = 3, RT_CTR_SHADOW = 4, RT_CTR_LONG = 5 };
+// work counters (one 64-byte block, zeroed by k_order before every k_trace)
+enum { RT_CTR_PRIMARY = 0 };
 #define RT_CTR_BYTES 64
 
 // A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by
@@ -35,9 +35,13 @@ struct RtLaunch {
     // per-sample buffers, rt_split_samples() entries per frame (sample t, see rt_kernels.hip)
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
     float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
-    uint32_t* hitlist;        // compacted sample ids of primary hits
-    float4* shrec;            // 3 float4 per long ray on the global list: march state + sample id + type
-    uint32_t long_cap;        // entries shrec holds
+    // k_trace's per-block spill rings (HBM): what does not fit a block's LDS rings, consumed by the
+    // same block; capacities per block (rt_spill_caps: the bound on a block's queued work)
+    uint32_t* spill_hits;     // hit sample ids, hit_spill_cap per block
+    float4* spill_long;       // long-ray records (3 float4), long_spill_cap per block
+    uint32_t hit_spill_cap, long_spill_cap;
+    int cells_from_cam;       // k_order derives CellDistance from CameraResults (setTargetDepths) first
+    int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS rings hold 64 entries
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word
     int ao_samples;           // AO rays per primary hit (0 = off)
@@ -50,10 +54,9 @@ struct RtLaunch {
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);
-void rt_launch_cell_depths(hipStream_t s, const float4* camera_results, float2* cells);
-// the prepass and setTargetDepths of every frame of a.frames (CameraResults -> CellDistance)
+// the prepass of every frame of a.frames (-> CameraResults); with a.cells_from_cam the
+// tracescreen launch derives CellDistance from them first (setTargetDepths, in k_order)
 void rt_launch_camerarays_batch(const RtLaunch& a);
-void rt_launch_cell_depths_batch(const RtLaunch& a);
 // Trace the region [off, off+ext) in 32x32-pixel tiles of every frame of a.frames (cells and
 // outputs from the table), tile-cyclic sharding: a single frame traces the tiles t (row-major
 // over the region) with t % tile_stride == tile_first; in a batch of n > 1 frames with
@@ -62,6 +65,15 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, ui
                            uint32_t tile_first, uint32_t tile_stride);
 
 #define RT_TILE 32
+// k_trace's spill capacities per block (1024 threads = 16 waves).  A wave starts a primary unit only
+// while fewer than 64 hits are queued and starts shading only while fewer than 128 long rays are
+// (k_trace's work priority), so a block never queues more than 64 + 16 * 64 * aa hits or
+// 128 + 16 * 64 * (1 + ao) long rays plus 16 compaction hand-backs of < 64: the rings cannot fill.
+inline void rt_spill_caps(int aa, int ao, uint32_t* hits, uint32_t* longs)
+{
+    *hits = 64u * (uint32_t)aa * 17u + 64u;
+    *longs = 64u * 16u * (uint32_t)(ao + 2) + 256u;
+}
 // samples the split pipeline addresses for a w x h frame: whole 32x32 tiles x AA
 inline size_t rt_split_samples(int w, int h, int aa)
 {

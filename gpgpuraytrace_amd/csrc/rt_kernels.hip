@@ -1,10 +1,10 @@
 // rt_kernels.hip -- HIP kernels for gfx950 (MI355X).
 //
 //   k_camerarays   <- Media/common/shaders/camerarays.hlsl:12-21
-//   k_cell_depths  <- Graphics/Terrain.cpp:356-439 (setTargetDepths: host code in
+//   k_order        <- Graphics/Terrain.cpp:356-439 (setTargetDepths: host code in
 //                     the reference; on the device here so a frame needs no
 //                     GPU->CPU->GPU round trip)
-//   k_order, k_trace, k_shade_pre, k_shadow, k_finish
+//   k_order (+ the longest-first tile order), k_trace, k_finish
 //                  <- Media/common/shaders/tracescreen.hlsl:16-76 (split pipeline below)
 //   k_shard_copy   -- tile-cyclic shard pack/unpack for the multi-GPU gather
 //
@@ -228,15 +228,12 @@ __device__ __forceinline__ float cd_interp(const float* d, int x, int y)
     return cd_get_depth(d, x, y);
 }
 
-__global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__ cam, float2* __restrict__ cells,
-                                                     const FrameTable* __restrict__ ft)
+// setTargetDepths of one frame by a 1024-thread block (thread = cell), depth scratch in LDS
+__device__ __forceinline__ void cell_depths_frame(const float4* __restrict__ cam, float2* __restrict__ cells,
+                                                  float* s_d)
 {
-    if (ft) { // frame blockIdx.x of a batch
-        cam = ft->cam[blockIdx.x];
-        cells = ft->cells[blockIdx.x];
-    }
-    __shared__ float s_d[RT_CAMERA_RES * RT_CAMERA_RES];
-    int i = threadIdx.x;
+    const int i = threadIdx.x;
+    __syncthreads(); // s_d's previous frame is no longer read
     s_d[i] = cam[i].w;
     __syncthreads();
     int xpos = i % RT_CAMERA_RES, ypos = i / RT_CAMERA_RES;
@@ -261,7 +258,6 @@ __global__ void __launch_bounds__(1024) k_cell_depths(const float4* __restrict__
 //   k_order     : longest-first 32x32 tile order per frame (scheduling only).
 //   k_trace     : persistent; primary march (tracing.hlsl:47-105) per 8x8 unit, the hit
 //                 shading + first shadow step, the long shadow / AO rays (LDS rings).
-//   k_shade_pre + k_shadow: drain what did not fit k_trace's rings (empty = instant exit).
 //   k_finish    : sky colour of the misses + in-order AA average + UNORM8.
 // Sample t = (u*64 + j)*AA + a: AA sample a of lane-slot j of 8x8 unit u.
 // A batch of n_frames frames: unit g of the launch is unit g % n_units of frame g / n_units
@@ -272,6 +268,7 @@ struct UnitMap {
     uint32_t n_frames, frame_samples;
     uint32_t frame_rot; // 1: frame f of a batch traces shard (tile_first + f) % tile_stride
     uint32_t order_batch; // k_order: 1 one longest-first order over the batch, 0 one per frame (frame-major)
+    uint32_t cells_from_cam; // k_order first derives each frame's CellDistance from its CameraResults
 };
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
@@ -356,11 +353,20 @@ __device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, 
 constexpr uint32_t kOrderLdsBuckets = 144u * 1024u;
 constexpr uint32_t kOrderBatchUnitsPerWave = 4u;
 __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
-                                                uint32_t* __restrict__ order)
+                                                uint32_t* __restrict__ order, uint32_t* __restrict__ counters)
 {
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
     __shared__ uint8_t s_b[kOrderLdsBuckets];
+    // k_trace's work counters start at zero (k_trace follows on the stream)
+    if (blockIdx.x == 0 && threadIdx.x < RT_CTR_BYTES / 4) counters[threadIdx.x] = 0u;
+    // setTargetDepths (Terrain.cpp:398-439) of this workgroup's frames first: the device path's
+    // CellDistance comes from the prepass's CameraResults (one launch fewer than a separate kernel)
+    if (m.cells_from_cam) {
+        const uint32_t c0 = m.order_batch ? 0u : blockIdx.x, c1 = m.order_batch ? m.n_frames : blockIdx.x + 1u;
+        for (uint32_t f = c0; f < c1; ++f) cell_depths_frame(ft->cam[f], ft->cells[f], s_key);
+        __syncthreads(); // the cells are stored before load_keys reads them (same workgroup)
+    }
     if (threadIdx.x < 64) s_hist[threadIdx.x] = 0;
     const uint32_t n_tiles = m.n_units >> 4;
     const bool cached = n_tiles * m.n_frames <= kOrderLdsBuckets;
@@ -726,156 +732,6 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
     }
 }
 
-// Shading of the hits a fused k_trace could not keep on its CU (hitlist, counter
-// RT_CTR_HITS): finish the short shadows, append the long ones to the global list.
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_shade_pre(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
-                                                    const uint32_t* __restrict__ perm2d,
-                                                    const float4* __restrict__ grad, UnitMap m,
-                                                    const float4* __restrict__ res,
-                                                    const uint32_t* __restrict__ hitlist,
-                                                    float4* __restrict__ samples, float4* __restrict__ fin,
-                                                    float4* __restrict__ shrec, uint32_t long_cap,
-                                                    uint32_t* __restrict__ counters, RtStats* stats)
-{
-    // hits k_trace could not queue on its CU (hit ring full)
-    const uint32_t n_hits = __builtin_amdgcn_readfirstlane(counters[RT_CTR_HITS]);
-    if (n_hits == 0u) return; // everything was shaded inside k_trace
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords];
-    load_noise_lds(lds, perm2d, grad, k);
-    const uint32_t lane = threadIdx.x & 63u;
-    Ctx c = make_ctx(k, lds);
-    const uint32_t n_units = (n_hits + 63u) / 64u;
-    float ssteps = 0.0f;
-    for (;;) {
-        uint32_t u = wave_fetch(&counters[RT_CTR_SHADE], lane);
-        if (u >= n_units) break;
-        const uint32_t i = u * 64u + lane;
-        const bool valid = i < n_hits;
-        bool more = false;
-        uint32_t t = 0;
-        March<L, true> st;
-        ShadeHit h;
-        if (valid) t = hitlist[i];
-        per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
-            const Ctx cf = frame_ctx(c, ft, f);
-            h = shade_hit<L, false>(cf, m, res, t, t - f * m.frame_samples, st);
-            c.nz.calls = cf.nz.calls;
-            more = h.more;
-            if (!more) {
-                sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
-                if constexpr (STATS) ssteps += (float)st.iters;
-            } else {
-                fin_store<L>(fin, t, h);
-            }
-        });
-        const uint64_t lb = __ballot(more);
-        if (lb) {
-            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(lb));
-            const uint32_t j = b + lane_rank(lb);
-            if (more && j < long_cap) long_pack(st, t, RT_LONG_SHADOW, shrec + (size_t)kShadowRec * j);
-        }
-        // AO extension: every AO ray of every hit goes to the long list
-        const uint64_t vb = __ballot(valid);
-        for (int kk = 0; kk < k->ao_samples; ++kk) {
-            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, (uint32_t)__popcll(vb));
-            const uint32_t j = b + lane_rank(vb);
-            if (valid && j < long_cap) {
-                March<L, true> ao;
-                ao_begin(c, h, (uint32_t)kk, ao);
-                long_pack(ao, t, RT_LONG_AO, shrec + (size_t)kShadowRec * j);
-            }
-        }
-    }
-    if constexpr (STATS) {
-        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        stats_noise(stats, c.nz.calls);
-    }
-}
-
-// The long shadow rays on the global list (counter RT_CTR_LONG) with lane refill:
-// each lane takes the next ray as soon as its own ends.  A retiring lane finishes
-// its sample from fin[t].
-template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
-                                                 UnitMap m,
-                                                 const uint32_t* __restrict__ perm2d,
-                                                 const float4* __restrict__ grad, const float4* __restrict__ shrec,
-                                                 const float4* __restrict__ fin, float4* __restrict__ samples,
-                                                 uint32_t* __restrict__ aocc, uint32_t long_cap,
-                                                 uint32_t* __restrict__ counters, RtStats* stats)
-{
-    const uint32_t n_long = min(__builtin_amdgcn_readfirstlane(counters[RT_CTR_LONG]), long_cap);
-    if (n_long == 0u) return; // every long shadow ray was marched inside k_trace
-    __shared__ __attribute__((aligned(16))) uint32_t lds[kNoiseLdsWords + sizeof(FrameRays) / 4];
-    FrameRays& s_fr = *reinterpret_cast<FrameRays*>(lds + kNoiseLdsWords);
-    frame_rays_load(s_fr, ft, m.n_frames);
-    load_noise_lds(lds, perm2d, grad, k);
-    const uint32_t lane = threadIdx.x & 63u;
-    Ctx c = make_ctx(k, lds); // c.eye: the lane's ray's frame (set on refill)
-    March<L, true> st;
-    st.d = 0.0f;
-    st.iters = 0;
-    bool live = false;
-    uint32_t t = 0, type = RT_LONG_SHADOW;
-    uint32_t pool = 0, pool_left = 0; // wave-uniform
-    bool drained = false;
-    float ssteps = 0.0f, aosteps = 0.0f;
-    for (;;) {
-        // 1. retire rays that left the loop: finish their samples
-        if (live && !march_live<L, true, true>(c, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
-            long_finish<L, false>(k, fin, samples, aocc, t, type, st);
-            live = false;
-            if constexpr (STATS) {
-                if (type == RT_LONG_AO) aosteps += (float)st.iters;
-                else ssteps += (float)st.iters;
-            }
-        }
-        // 2. refill idle lanes from the wave's pool of long-list indices
-        if (!drained) {
-            uint64_t idle = __ballot(!live);
-            if ((uint32_t)__popcll(idle) >= kRefillIdle) {
-                while (idle) {
-                    if (pool_left == 0u) {
-                        uint32_t b = wave_fetch(&counters[RT_CTR_SHADOW], lane, 64u);
-                        if (b >= n_long) {
-                            drained = true;
-                            break;
-                        }
-                        pool = b;
-                        pool_left = (n_long - b) < 64u ? (n_long - b) : 64u;
-                    }
-                    const uint32_t take = (uint32_t)__popcll(idle) < pool_left ? (uint32_t)__popcll(idle) : pool_left;
-                    const uint32_t rank = lane_rank(idle);
-                    const bool mine = ((idle >> lane) & 1ull) && rank < take;
-                    if (mine) {
-                        const float4* r = shrec + (size_t)kShadowRec * (pool + rank);
-                        t = long_unpack(r[0], r[1], r[2], rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
-                        const float* fr = s_fr.v[frame_of(m, t)];
-                        c.eye = rtm::mk(fr[0], fr[1], fr[2]);
-                        if (type == RT_LONG_SHADOW) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
-                        live = true; // AO rays start live; shadow rays were live when stored
-                    }
-                    idle &= ~__ballot(mine);
-                    pool += take;
-                    pool_left -= take;
-                }
-            }
-        }
-        // 3. one shadow-march step on every live lane
-        if (__ballot(live) == 0ull) {
-            if (drained) break;
-            continue;
-        }
-        if (live) march_step<L, true, true>(c, st);
-    }
-    if constexpr (STATS) {
-        atomicAdd(&stats->shadow_steps, (unsigned long long)ssteps);
-        atomicAdd(&stats->ao_steps, (unsigned long long)aosteps);
-        stats_noise(stats, c.nz.calls);
-    }
-}
-
 // ===========================================================================
 // Fused trace (default pipeline): the primary march, the hit shading and the long
 // shadow rays in ONE persistent kernel, so the latency-bound shading phases run in
@@ -890,7 +746,8 @@ __global__ void __launch_bounds__(1024) k_shadow(const RtConsts* __restrict__ k,
 // per-block LDS lock for a few instructions.  Every hand-off stays on one CU: the
 // producer's global stores (res / fin) complete (s_waitcnt) before the ring push,
 // and the consumer reads them with L1-bypassing loads from the XCD's L2.  A full
-// ring spills to the global lists, which k_shade_pre / k_shadow drain afterwards.
+// ring spills to the block's spill ring in HBM (the same block consumes it, so the hand-off stays
+// on one CU like the LDS rings' own): a block never hands work to another kernel.
 constexpr uint32_t kHitRing = 512;
 constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
 #ifndef RT_LONG_BATCH // A/B: make variant FLAGS=-DRT_LONG_BATCH=n
@@ -917,6 +774,8 @@ struct TraceQueues {
     uint32_t active;  // waves inside a primary unit or a shading batch (they may still push)
     uint32_t drained; // the global unit queue is exhausted
     uint32_t pad;
+    uint32_t hs_head, hs_tail; // the block's hit spill ring (HBM), when the LDS hit ring is full
+    uint32_t ls_head, ls_tail; // the block's long-ray spill ring (HBM)
     uint32_t hits[kHitRing];
     float4 longs[kLongRing * kShadowRec];
 };
@@ -969,11 +828,12 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 UnitMap m, const uint32_t* __restrict__ order,
                                                 uint64_t* __restrict__ hitmask,
                                                 float4* __restrict__ res, float4* __restrict__ samples,
-                                                float4* __restrict__ fin, uint32_t* __restrict__ hitlist,
-                                                float4* __restrict__ shrec, uint32_t long_cap,
+                                                float4* __restrict__ fin, uint32_t* __restrict__ spill_hits,
+                                                float4* __restrict__ spill_long, uint32_t hit_spill_cap,
+                                                uint32_t long_spill_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live)
+                                                uint32_t compact_live, uint32_t hit_ring_cap, uint32_t long_ring_cap)
 {
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
@@ -990,6 +850,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         q.l_head = q.l_tail = 0;
         q.active = 0;
         q.drained = 0;
+        q.hs_head = q.hs_tail = 0;
+        q.ls_head = q.ls_tail = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     load_noise_lds(lds, perm2d, grad, k);
@@ -998,6 +860,12 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     if constexpr (STATS) c.nz.lds_calls = (__attribute__((address_space(3))) unsigned long long*)&s_st.v[BlockStats::NOISE];
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
+    // this block's spill rings (records hit_spill_cap / long_spill_cap per block)
+    uint32_t* const hspill = spill_hits + (size_t)blockIdx.x * hit_spill_cap;
+    float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
+    // queued work of the block: LDS ring + spill ring
+    auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_tail) - vload(q.ls_head); };
+    auto queued_hits = [&]() { return vload(q.h_tail) - vload(q.h_head) + vload(q.hs_tail) - vload(q.hs_head); };
     // STATS: march steps and hits go to the block's LDS counters (no VGPRs held across the loops)
     auto stat = [&](int i, uint32_t v) {
         if constexpr (STATS) atomicAdd(&s_st.v[i], (unsigned long long)v);
@@ -1007,24 +875,24 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     // loop iterations, long rays finished (lane), max long-ray iters (lane), last iteration, max primary iters (lane)
     WT(unsigned long long wt[RT_WT_FIELDS] = {}; wt[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
-    // push the lanes' long rays (shadow continuations or AO starts) to the ring, or
-    // to the global list when the ring is full
+    // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
+    // block's spill ring when the LDS ring is full (stored before the tail publishes them)
     auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t type) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
         const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
-        const bool fits = lt - lh + n <= kLongRing;
-        if (fits) {
+        if (lt - lh + n <= long_ring_cap) {
             if (want) long_pack(st, t, type, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
+        } else {
+            const uint32_t stl = vload(q.ls_tail);
+            if (want) long_pack(st, t, type, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) q.ls_tail = stl + n;
         }
         q_unlock(&q.lock, lane);
-        if (!fits) {
-            const uint32_t b = wave_fetch(&counters[RT_CTR_LONG], lane, n);
-            if (want && b + rank < long_cap) long_pack(st, t, type, shrec + (size_t)kShadowRec * (b + rank));
-        }
     };
 
     // ---- a batch of long rays, lane refill from the ring ----
@@ -1045,20 +913,33 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= refill_idle && vload(q.l_tail) != vload(q.l_head)) {
+            if (nidle >= refill_idle && queued_long() != 0u) {
                 q_lock(&q.lock, lane);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
+                // the block's spill ring tops up what the LDS ring cannot give
+                const uint32_t sh = vload(q.ls_head), sl = vload(q.ls_tail);
+                const uint32_t more = (sl - sh) < nidle - take ? (sl - sh) : nidle - take;
                 const uint32_t rank = lane_rank(idle);
-                if (((idle >> lane) & 1ull) && rank < take) {
-                    const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
-                    t = long_unpack(r[0], r[1], r[2], rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
+                const bool mine = ((idle >> lane) & 1ull) && rank < take + more;
+                auto take_ray = [&](float4 r0, float4 r1, float4 r2) {
+                    t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
                     const float* fr = s_fr.v[frame_of(m, t)];
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                     if (type == RT_LONG_SHADOW) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     live = true;
+                };
+                if (mine && rank < take) {
+                    const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
+                    take_ray(r[0], r[1], r[2]);
+                } else if (mine) {
+                    const float4* r = lspill + (size_t)((sh + rank - take) % long_spill_cap) * kShadowRec;
+                    take_ray(ld_fresh(r), ld_fresh(r + 1), ld_fresh(r + 2));
                 }
-                if (lane == 0) q.l_head = head + take;
+                if (lane == 0) {
+                    q.l_head = head + take;
+                    q.ls_head = sh + more;
+                }
                 q_unlock(&q.lock, lane);
             }
             const uint64_t lv = __ballot(live);
@@ -1069,8 +950,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
-            if ((uint32_t)__popcll(lv) < compact_live && vload(q.l_tail) == vload(q.l_head) &&
-                vload(q.drained) == 0u) {
+            if ((uint32_t)__popcll(lv) < compact_live && queued_long() == 0u && vload(q.drained) == 0u) {
                 push_long(live, st, t, type);
                 c.nz.calls = cl.nz.calls;
                 return;
@@ -1091,10 +971,20 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     auto do_shade = [&]() {
         q_lock(&q.lock, lane);
         const uint32_t head = vload(q.h_head), tail = vload(q.h_tail);
-        const uint32_t take = (tail - head) < 64u ? (tail - head) : 64u;
+        uint32_t take = (tail - head) < 64u ? (tail - head) : 64u;
         uint32_t t = 0;
         if (lane < take) t = q.hits[(head + lane) % kHitRing];
         if (lane == 0) q.h_head = head + take;
+        // the block's spill ring tops the batch up
+        const uint32_t sh = vload(q.hs_head), sl = vload(q.hs_tail);
+        const uint32_t spilled = (sl - sh) < 64u - take ? (sl - sh) : 64u - take;
+        if (spilled) {
+            if (lane >= take && lane < take + spilled)
+                t = __builtin_nontemporal_load(hspill + (sh + lane - take) % hit_spill_cap);
+            if (lane == 0) q.hs_head = sh + spilled;
+            take += spilled;
+            __builtin_amdgcn_s_waitcnt(0); // read before the slots can be reused
+        }
         q_unlock(&q.lock, lane);
         March<L, true> st;
         bool more = false;
@@ -1196,16 +1086,16 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 __builtin_amdgcn_s_waitcnt(0); // res[t] is in L2 before the hit is visible
                 q_lock(&q.lock, lane);
                 const uint32_t hh = vload(q.h_head), ht = vload(q.h_tail);
-                const bool fits = ht - hh + n <= kHitRing;
-                if (fits) {
+                if (ht - hh + n <= hit_ring_cap) {
                     if (hit) q.hits[(ht + rank) % kHitRing] = t;
                     if (lane == 0) q.h_tail = ht + n;
+                } else { // the LDS ring is full: the block's spill ring, stored before the tail publishes it
+                    const uint32_t sl = vload(q.hs_tail);
+                    if (hit) hspill[(sl + rank) % hit_spill_cap] = t;
+                    __builtin_amdgcn_s_waitcnt(0);
+                    if (lane == 0) q.hs_tail = sl + n;
                 }
                 q_unlock(&q.lock, lane);
-                if (!fits) {
-                    const uint32_t b = wave_fetch(&counters[RT_CTR_HITS], lane, n);
-                    if (hit) hitlist[b + rank] = t;
-                }
             }
         }
         c.nz.calls = cf.nz.calls;
@@ -1219,8 +1109,8 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     bool first_unit = true;
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
-        const uint32_t lp = vload(q.l_tail) - vload(q.l_head);
-        const uint32_t hp = vload(q.h_tail) - vload(q.h_head);
+        const uint32_t lp = queued_long();
+        const uint32_t hp = queued_hits();
         const bool drained = vload(q.drained) != 0u;
         WT(const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); wt[12]++;
            wt[15] = t0;)
@@ -1250,7 +1140,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             continue;
         }
         // drained and nothing queued: leave once no wave of the block can still push
-        if (vload(q.active) == 0u && vload(q.l_tail) == vload(q.l_head) && vload(q.h_tail) == vload(q.h_head)) break;
+        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) break;
         __builtin_amdgcn_s_sleep(2);
         WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
     }
@@ -1289,7 +1179,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
 // w + n_waves, ...): the per-unit work is so short that a shared queue atomic would serialise it.
 __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                  UnitMap m, const uint64_t* __restrict__ hitmask,
-                                                 const float4* __restrict__ samples, const uint32_t* __restrict__ aocc)
+                                                 const float4* __restrict__ samples, uint32_t* __restrict__ aocc)
 {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
@@ -1317,9 +1207,18 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
                 const float ao = ao_factor(ao_occluded(aocc, t), k->ao_samples);
                 v = make_float4(v.x * ao, v.y * ao, v.z * ao, v.w);
             }
+
             c0 = c0 + v.x;
             c1 = c1 + v.y;
             c2 = c2 + v.z;
+        }
+        // the next launch on these buffers counts from zero: every counted sample is read above, and
+        // the words are cleared once all of them are (a word's other samples belong to this lane or to
+        // lanes of this unit, whose reads in the same loop iterations precede these stores), so no
+        // per-launch memset of the counts precedes k_trace
+        if (k->ao_samples > 0) {
+            const uint32_t t0 = f * m.frame_samples + (u * 64u + lane) * aa;
+            for (uint32_t w = t0 >> 2; w <= (t0 + aa - 1u) >> 2; ++w) aocc[w] = 0u;
         }
         float ia = rtm::rcp((float)aa);
         c0 = c0 * ia;
@@ -1464,21 +1363,17 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     // k_finish holds no LDS: up to 2 blocks per CU
     uint32_t fblocks = need < 2u * blocks ? need : 2u * blocks;
     dim3 blk(1024);
-    (void)hipMemsetAsync(a.queue, 0, RT_CTR_BYTES, a.stream);
-    if (a.ao_samples > 0)
-        (void)hipMemsetAsync(a.aocc, 0, ((size_t)m.frame_samples * m.n_frames + 3) / 4 * sizeof(uint32_t), a.stream);
-    hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order);
-    // primary + shading + long rays; what did not fit the CU's rings goes to the global lists
+    m.cells_from_cam = (uint32_t)a.cells_from_cam;
+    // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
+    hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue);
+    // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill rings
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
         hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m,
-                           a.order, a.hitmask, a.res, a.samples, a.fin, a.hitlist, a.shrec, a.long_cap, a.aocc, a.queue,
-                           a.stats, kLongBatch, kRefillIdle, kCompactLive);
-        hipLaunchKernelGGL((k_shade_pre<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m, a.res,
-                           a.hitlist, a.samples, a.fin, a.shrec, a.long_cap, a.queue, a.stats);
-        hipLaunchKernelGGL((k_shadow<L, S>), dim3(blocks), blk, 0, a.stream, k0, a.frames, m, a.perm2d, a.grad, a.shrec,
-                           a.fin, a.samples, a.aocc, a.long_cap, a.queue, a.stats);
+                           a.order, a.hitmask, a.res, a.samples, a.fin, a.spill_hits, a.spill_long, a.hit_spill_cap,
+                           a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
+                           a.small_rings ? 64u : kHitRing, a.small_rings ? 64u : kLongRing);
         hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});
@@ -1505,16 +1400,6 @@ void rt_launch_camerarays_batch(const RtLaunch& a)
     case RT_GREENROCKS: launch_camerarays_l<RT_GREENROCKS>(a, nullptr, a.frames, a.n_frames); break;
     default: launch_camerarays_l<RT_NOMADPLAINS>(a, nullptr, a.frames, a.n_frames); break;
     }
-}
-
-void rt_launch_cell_depths(hipStream_t s, const float4* cam, float2* cells)
-{
-    hipLaunchKernelGGL(k_cell_depths, dim3(1), dim3(1024), 0, s, cam, cells, nullptr);
-}
-
-void rt_launch_cell_depths_batch(const RtLaunch& a)
-{
-    hipLaunchKernelGGL(k_cell_depths, dim3(a.n_frames), dim3(1024), 0, a.stream, nullptr, nullptr, a.frames);
 }
 
 void rt_launch_tracescreen(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, uint32_t ey, uint32_t first,

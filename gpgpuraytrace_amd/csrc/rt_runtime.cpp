@@ -118,14 +118,14 @@ struct rt_device_s {
     int num_cus = 256;
     float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
     float4* res = nullptr;
-    uint32_t* hitlist = nullptr;
+    uint32_t* spill_hits = nullptr; // k_trace's per-block spill rings (rt_spill_caps per block)
+    float4* spill_long = nullptr;
+    size_t spill_hits_n = 0, spill_long_n = 0; // entries allocated (all blocks)
     uint32_t* order = nullptr;
     uint64_t* hitmask = nullptr; // per unit and AA sample: the primary-hit ballot (k_trace -> k_finish)
-    float4* shrec = nullptr;
     float4* fin = nullptr;
     uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
-    size_t long_cap = 0; // entries of the global long-ray list (shrec)
     // dominant-kernel timing (rt_device_set_profiling)
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
@@ -444,11 +444,13 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.num_cus = dev->num_cus;
     a.samples = dev->samples;
     a.res = dev->res;
-    a.hitlist = dev->hitlist;
     a.order = dev->order;
     a.hitmask = dev->hitmask;
-    a.shrec = dev->shrec;
-    a.long_cap = (uint32_t)std::min<size_t>(dev->long_cap, 0xffffffffu);
+    a.spill_hits = dev->spill_hits;
+    a.spill_long = dev->spill_long;
+    rt_spill_caps(s->aa, s->ao, &a.hit_spill_cap, &a.long_spill_cap);
+    a.cells_from_cam = 0;
+    a.small_rings = (dev->flags & RT_DEVICE_DEBUG_SMALL_RINGS) ? 1 : 0;
     a.fin = dev->fin;
     a.aocc = dev->aocc;
     a.ao_samples = s->ao;
@@ -488,39 +490,47 @@ int check_texture(Shader* s)
 // (48 B each).
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
+    // k_trace's spill rings: rt_spill_caps per block, one block per CU
+    uint32_t hcap, lcap;
+    rt_spill_caps(aa, ao, &hcap, &lcap);
+    const size_t hs_need = (size_t)dev->num_cus * hcap, ls_need = (size_t)dev->num_cus * lcap;
+    if (hs_need > dev->spill_hits_n || ls_need > dev->spill_long_n) {
+        HIP_TRY(hipStreamSynchronize(dev->stream));
+        if (dev->spill_hits) HIP_TRY(hipFree(dev->spill_hits));
+        if (dev->spill_long) HIP_TRY(hipFree(dev->spill_long));
+        dev->spill_hits = nullptr;
+        dev->spill_long = nullptr;
+        dev->spill_hits_n = dev->spill_long_n = 0;
+        HIP_TRY(hipMalloc(&dev->spill_hits, hs_need * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
+        dev->spill_hits_n = hs_need;
+        dev->spill_long_n = ls_need;
+    }
     size_t need = rt_split_samples(dev->width, dev->height, aa) * (size_t)n_frames;
-    size_t long_need = need * (size_t)(1 + ao);
-    if (need <= dev->samples_cap && long_need <= dev->long_cap) return RT_OK;
-    need = std::max(need, dev->samples_cap);
-    long_need = std::max(long_need, dev->long_cap);
+    if (need <= dev->samples_cap) return RT_OK;
     HIP_TRY(hipStreamSynchronize(dev->stream));
     if (dev->samples) HIP_TRY(hipFree(dev->samples));
     if (dev->res) HIP_TRY(hipFree(dev->res));
-    if (dev->hitlist) HIP_TRY(hipFree(dev->hitlist));
     if (dev->order) HIP_TRY(hipFree(dev->order));
     if (dev->hitmask) HIP_TRY(hipFree(dev->hitmask));
-    if (dev->shrec) HIP_TRY(hipFree(dev->shrec));
     if (dev->fin) HIP_TRY(hipFree(dev->fin));
     if (dev->aocc) HIP_TRY(hipFree(dev->aocc));
-    dev->shrec = nullptr;
     dev->fin = nullptr;
     dev->aocc = nullptr;
     dev->samples = nullptr;
     dev->res = nullptr;
-    dev->hitlist = nullptr;
     dev->order = nullptr;
     dev->hitmask = nullptr;
     dev->samples_cap = 0;
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->hitlist, need * sizeof(uint32_t)));
-    HIP_TRY(hipMalloc(&dev->shrec, long_need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->aocc, (need + 3) / 4 * sizeof(uint32_t))); // a byte per sample (ao_count)
+    // AO counts, a byte per sample (ao_count): zero once here; k_finish clears what it reads
+    HIP_TRY(hipMalloc(&dev->aocc, (need + 3) / 4 * sizeof(uint32_t)));
+    HIP_TRY(hipMemsetAsync(dev->aocc, 0, (need + 3) / 4 * sizeof(uint32_t), dev->stream));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * RT_MAX_BATCH * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->hitmask, need / 64 * sizeof(uint64_t)));
     dev->samples_cap = need;
-    dev->long_cap = long_need;
     return RT_OK;
 }
 
@@ -595,7 +605,7 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)res, (void*)hitlist, (void*)order, (void*)hitmask, (void*)shrec, (void*)fin, (void*)aocc,
+                    (void*)res, (void*)spill_hits, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
@@ -1122,8 +1132,9 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
     const uint64_t v[] = {(uint64_t)(uintptr_t)a.stream, (uint64_t)a.landscape, (uint64_t)(uintptr_t)a.consts,
                           (uint64_t)(uintptr_t)a.perm2d, (uint64_t)(uintptr_t)a.grad, (uint64_t)(uintptr_t)a.stats,
                           (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
-                          (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.hitlist,
-                          (uint64_t)(uintptr_t)a.shrec, (uint64_t)a.long_cap, (uint64_t)(uintptr_t)a.fin,
+                          (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.spill_hits,
+                          (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_spill_cap, (uint64_t)a.long_spill_cap,
+                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)(uintptr_t)a.fin,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));
@@ -1307,9 +1318,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     la_cam.frames = la_scr.frames = dev->table.d;
     la_cam.frames_host = la_scr.frames_host = ft;
     la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
+    // setTargetDepths runs at the start of the tracescreen launch (k_order), from the CameraResults
+    la_scr.cells_from_cam = 1;
     auto pre = [&] {
         if (phases & PH_PRE) rt_launch_camerarays_batch(la_cam);
-        rt_launch_cell_depths_batch(la_cam);
     };
     if (graphs) {
         // the constant / table uploads stay outside: they precede the replay on this stream

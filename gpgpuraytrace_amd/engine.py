@@ -157,10 +157,13 @@ class Compute:
 class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
-    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False):
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False):
+        """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS rings hold 64 entries,
+        so queued work takes the per-block spill rings; same bits)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
-                      | (_native.RT_DEVICE_GRAPH if graph else 0))
+                      | (_native.RT_DEVICE_GRAPH if graph else 0)
+                      | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0))
         self._h = None
 
     def create(self):

@@ -46,14 +46,18 @@ enum {
     RT_DEVICE_STATS = 2u,
     RT_DEVICE_GRAPH = 4u,
     RT_DEVICE_SEG_TAIL_OFF = 8u,
-    RT_DEVICE_SEG_TAIL_ON = 16u
+    RT_DEVICE_SEG_TAIL_ON = 16u,
+    RT_DEVICE_DEBUG_SMALL_RINGS = 32u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
  * every frame; a changed launch argument (shader swap, buffers, shard, stats) re-captures.
  * No reference counterpart (the D3D frame loop re-records its dispatches every frame).
  * RT_DEVICE_SEG_TAIL_OFF / _ON: reserved (ABI <= 3 selected a trace-kernel tail variant that
- * ABI 4 removed; both are accepted and have no effect).  Setting both fails with RT_ERR_INVALID. */
+ * ABI 4 removed; both are accepted and have no effect).  Setting both fails with RT_ERR_INVALID.
+ * RT_DEVICE_DEBUG_SMALL_RINGS (ABI 4, diagnostic): the trace kernel's per-CU LDS work rings hold 64
+ * entries instead of 512 / 528, so most queued work takes the per-block spill rings in HBM (the
+ * parity tests run frames through that path); same bits, slower. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };

@@ -27,19 +27,29 @@ def main():
     ap.add_argument("--max-steps", type=int, default=512)
     ap.add_argument("--ao", type=int, default=1)
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--batch", type=int, default=1, help="frames per launch (rt_terrain_render_batch)")
     a = ap.parse_args()
     import numpy as np
     import gpgpuraytrace_amd as G
     W, H = 1920, 1080
-    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=0)
-    ter = G.Terrain(dev, "nomadplains", max_steps=a.max_steps, ao_samples=a.ao)
-    ter.create()
-    assert ter.reload()
-    ter.set_camera(G.Camera(W, H))
-    ter.set_time_of_day(0.3)
+    devs, ters = [], []
+    for _ in range(a.batch):
+        d = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=0)
+        t = G.Terrain(d, "nomadplains", max_steps=a.max_steps, ao_samples=a.ao)
+        t.create()
+        assert t.reload()
+        t.set_camera(G.Camera(W, H))
+        t.set_time_of_day(0.3)
+        devs.append(d)
+        ters.append(t)
+    dev = devs[0]
     for _ in range(3):
-        ter.render_device(a.rank, a.n)
-    dev.synchronize()
+        if a.batch > 1:
+            G.engine.render_batch(ters, a.rank, a.n)
+        else:
+            ters[0].render_device(a.rank, a.n)
+    for d in devs:
+        d.synchronize()
     L = G.lib()
     L.rt_debug_wave_trace.argtypes = [C.c_void_p, C.c_int]
     nw = 256 * 16
@@ -74,9 +84,20 @@ def main():
         sums[k_] = sums.get(k_, 0.0) + b
     v = np.array(list(sums.values()))
     print(f"per-SIMD busy (sum over its waves): mean {v.mean():.1f} us  max {v.max():.1f} us  p99 {np.percentile(v, 99):.1f}")
+    # when each SIMD's last wave left, and each SIMD's live-wave count over time: the launch's tail
+    last = {}
+    for k_, e in zip(key, end):
+        last[k_] = max(last.get(k_, 0.0), e)
+    le = np.array(sorted(last.values()))
+    span = end.max()
+    print(f"SIMD idle-after-last-wave: p10 {np.percentile(le, 10):.1f}  p50 {np.percentile(le, 50):.1f}  "
+          f"p90 {np.percentile(le, 90):.1f}  max {span:.1f} us; SIMD-time after its last wave = "
+          f"{(span - le).sum() / (len(le) * span):.2%} of the launch")
+    print(f"wave-slot time after the wave left = {(span - end).sum() / (len(end) * span):.2%} of the launch")
     # longest single activity
     print(f"longest single unit (wave total/units, max): {(tot(2) / np.maximum(t[:, 5], 1)).max():.1f} us")
-    dev.destroy()
+    for d in devs:
+        d.destroy()
 
 
 if __name__ == "__main__":

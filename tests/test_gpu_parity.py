@@ -31,10 +31,10 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         ao=0, graph=False):
+         ao=0, graph=False, small_rings=False):
     import gpgpuraytrace_amd as G
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
-                                    stats=stats, graph=graph)
+                                    stats=stats, graph=graph, small_rings=small_rings)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -169,15 +169,17 @@ def test_density_bitexact(land):
 
 
 # --- whole frames vs the golden oracle frames ----------------------------------------------
-@pytest.mark.parametrize("kernels", ["stats", "product"])
+@pytest.mark.parametrize("kernels", ["stats", "product", "spill"])
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_frame_bitexact_device_path(spec, kernels):
     """stats: the instrumented kernels (their counts equal the oracle's too); product: the
-    uninstrumented kernels the bench times."""
+    uninstrumented kernels the bench times; spill: the product kernels with 64-entry LDS rings
+    (RT_DEVICE_DEBUG_SMALL_RINGS), so queued hits and long rays go through the per-block spill rings."""
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
-    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=kernels == "stats", ao=ao)
+    dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=kernels == "stats", ao=ao,
+                    small_rings=kernels == "spill")
     ter.render_device()
     dev.present()
     img, img8 = dev.readback_float(), dev.readback()
@@ -426,15 +428,16 @@ def test_other_landscapes_720p_rows_bitexact(land, ao):
     dev.destroy()
 
 
-@pytest.mark.parametrize("name", ["c2", "c3"])
-def test_baseline_config_batch_rows_bitexact(name):
+@pytest.mark.parametrize("name,small_rings", [("c2", False), ("c3", False), ("c3", True)])
+def test_baseline_config_batch_rows_bitexact(name, small_rings):
     """The bench's entry point: one rt_terrain_render_batch of 4 frames (reset, look-down,
-    reset, look-down) at the config's size; every frame equals the oracle on its row sample."""
+    reset, look-down) at the config's size; every frame equals the oracle on its row sample.
+    small_rings: the C3 batch with 64-entry LDS rings, so most queued work spills to HBM."""
     from gpgpuraytrace_amd import engine as E
     w, h, ms, ao, step = BASELINE_CONFIGS[name]
     poses = ["reset", "lookdown", "reset", "lookdown"]
     refs = {p: _config_rows(name, p, 3) for p in ("reset", "lookdown")}
-    frames = [make(refs[p][0], max_steps=ms, ao=ao) for p in poses]
+    frames = [make(refs[p][0], max_steps=ms, ao=ao, small_rings=small_rings) for p in poses]
     E.render_batch([t for _, t in frames])
     for (dev, _), p in zip(frames, poses):
         _, (ref, ref8, _, _, _), rows = refs[p]
