@@ -21,8 +21,8 @@ ref_semantics the same machinery at the reference's own semantics (uncapped, no 
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
 scaling: the frame is fixed); parallel.BatchPlan / run_batch hold the per-batch sequence
-(split prepass + CameraResults all-gather, shard rotation, pack, one RCCL gather to rank 0,
-unpack), which tests/test_dist.py drives with host ops over gloo.
+(every rank's prepass of the batch, or with --split-prepass 1 a B/N share + CameraResults
+all-gather; shard rotation, pack, one RCCL gather to rank 0, unpack), which tests/test_dist.py drives with host ops over gloo.
 
 Prints ONE JSON line on rank 0 (driver contract), with "roofline" for the dominant
 kernel (tracescreen, timed by HIP events on its own stream in a pass with one batch in
@@ -55,7 +55,7 @@ CONFIGS = {
     "ref": {"width": 1920, "height": 1080, "max_steps": 0, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 16,
             "name": "1920x1080, reference semantics (uncapped march, shadow, no AO)"},
 }
-TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_shade_pre + k_shadow + k_finish"
+TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_finish"
 
 
 def parse():
@@ -76,9 +76,12 @@ def parse():
     ap.add_argument("--batch", type=int, default=12,
                     help="max frames per rt_terrain_render_batch launch sequence (1..16); the --steps frames are "
                          "split into ceil(steps / batch) batches of near-equal size")
-    ap.add_argument("--split-prepass", type=int, default=1,
-                    help="N>1: each rank runs the prepass of B/N frames of a batch and one all-gather shares them "
-                         "(0 = every rank runs every frame's prepass)")
+    ap.add_argument("--split-prepass", type=int, default=0,
+                    help="N>1: 1 = each rank runs the prepass of B/N frames of a batch and an all-gather shares "
+                         "them (a second collective and a cross-rank barrier per batch); 0 (default, SURVEY 8e and "
+                         "north_star's single gather) = every rank runs every frame's prepass.  The barrier model "
+                         "(scripts/batch_shard_sim.py --barrier-model, profiles/r03/batch_shard_barrier.log) puts "
+                         "the split's gain at <= 2%% (N=8)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
@@ -177,7 +180,7 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
     return out, parity
 
 
-TRAFFIC_KERNELS = ("k_order", "k_trace", "k_shade_pre", "k_shadow", "k_finish")
+TRAFFIC_KERNELS = ("k_order", "k_trace", "k_finish")
 
 
 def traffic_child(a):

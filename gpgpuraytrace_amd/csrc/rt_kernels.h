@@ -34,14 +34,13 @@ struct RtLaunch {
     int num_cus;              // compute units (persistent grid size)
     // per-sample buffers, rt_split_samples() entries per frame (sample t, see rt_kernels.hip)
     float4* samples;          // saturated colour of hit samples (written by S, read by R)
-    float4* res;              // 3 float4 per sample: primary RayResult (pd, fcolord, density)
-    // k_trace's per-block spill rings (HBM): what does not fit a block's LDS rings, consumed by the
-    // same block; capacities per block (rt_spill_caps: the bound on a block's queued work)
-    uint32_t* spill_hits;     // hit sample ids, hit_spill_cap per block
-    float4* spill_long;       // long-ray records (3 float4), long_spill_cap per block
-    uint32_t hit_spill_cap, long_spill_cap;
+    // k_trace's per-block queues in HBM, consumed by the same block; capacities per block
+    // (rt_spill_caps: the bound on a block's queued work)
+    float4* hitq;             // hit queue: primary hit records (1 float4, 3 with fog), hit_cap per block
+    float4* spill_long;       // long-ray records (3 float4) the LDS ring cannot hold, long_spill_cap per block
+    uint32_t hit_cap, long_spill_cap;
     int cells_from_cam;       // k_order derives CellDistance from CameraResults (setTargetDepths) first
-    int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS rings hold 64 entries
+    int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS long ring holds 64 entries
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word
     int ao_samples;           // AO rays per primary hit (0 = off)
@@ -65,10 +64,11 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, ui
                            uint32_t tile_first, uint32_t tile_stride);
 
 #define RT_TILE 32
-// k_trace's spill capacities per block (1024 threads = 16 waves).  A wave starts a primary unit only
-// while fewer than 64 hits are queued and starts shading only while fewer than 128 long rays are
-// (k_trace's work priority), so a block never queues more than 64 + 16 * 64 * aa hits or
-// 128 + 16 * 64 * (1 + ao) long rays plus 16 compaction hand-backs of < 64: the rings cannot fill.
+// k_trace's queue capacities per block (1024 threads = 16 waves): the hit queue and the long-ray
+// spill ring.  A wave starts a primary unit only while fewer than 64 hits are queued and starts
+// shading only while fewer than 128 long rays are (k_trace's work priority), so a block never
+// queues more than 64 + 16 * 64 * aa hits or 128 + 16 * 64 * (1 + ao) long rays plus 16 compaction
+// hand-backs of < 64: the rings cannot fill.
 inline void rt_spill_caps(int aa, int ao, uint32_t* hits, uint32_t* longs)
 {
     *hits = 64u * (uint32_t)aa * 17u + 64u;

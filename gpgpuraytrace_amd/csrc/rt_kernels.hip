@@ -315,24 +315,29 @@ __device__ __forceinline__ uint32_t first_unit_index()
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * gridDim.x + blockIdx.x;
 }
 
-// A hit's RayResult, the shading input (misses store none).  With fog live (greenrocks): 3 float4
-// per sample (pd + dist, fcolord, density).  Without, fcolord is 0 and is not stored, and the hit
-// position is not either: the shading re-derives it from the pixel's ray and the last sample's
-// distance (march_result's fma).  (sd, dist, density) as 3 floats at a 12-byte stride: 12 B per hit
-// instead of 48, in one contiguous record.
+// A hit's record in its block's hit queue (the shading input; misses store none): the primary
+// RayResult and the sample id t.  With fog live (greenrocks): 3 float4 (pd + dist, fcolord,
+// (density, steps, -, t)).  Without, fcolord is 0 and is not stored, and the hit position is not
+// either: the shading re-derives it from the pixel's ray and the last sample's distance
+// (march_result's fma), so the record is one float4 (sd, dist, density, t).  The queue is a stack
+// per block (hits shade in any order), written densely at its top: the few KiB near the top are
+// rewritten over and over and stay in the XCD's L2 (write-back), instead of a sample-indexed array
+// whose sparsely written lines (the hit lanes of each unit) each cost a write-back and a re-fetch,
+// or a ring whose whole capacity cycles through the L2 (scripts/ubench_l2wb.hip: 16 KiB rewritten
+// per block stays in L2, 64 KiB per block is written back on every pass).
 template <int L>
-__device__ __forceinline__ void store_ray(float4* __restrict__ res, uint32_t n, uint32_t t, const RayResult& rr)
+struct HitRec {
+    static constexpr uint32_t N = FogLive<L>::value ? 3u : 1u; // float4 per record
+};
+template <int L>
+__device__ __forceinline__ void hit_store(float4* __restrict__ r, uint32_t t, const RayResult& rr)
 {
     if constexpr (FogLive<L>::value) {
-        res[3u * t + 0u] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
-        res[3u * t + 1u] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
-        res[3u * t + 2u] = make_float4(rr.density, rr.steps, 0.0f, 0.0f);
+        r[0] = make_float4(rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w);
+        r[1] = make_float4(rr.fc.x, rr.fc.y, rr.fc.z, rr.fc.w);
+        r[2] = make_float4(rr.density, rr.steps, 0.0f, __uint_as_float(t));
     } else {
-        (void)n;
-        float* r = reinterpret_cast<float*>(res) + 3u * t;
-        r[0] = rr.sd;
-        r[1] = rr.pd.w;
-        r[2] = rr.density;
+        r[0] = make_float4(rr.sd, rr.pd.w, rr.density, __uint_as_float(t));
     }
 }
 
@@ -587,10 +592,10 @@ __device__ __forceinline__ void frame_rays_load(FrameRays& s, const FrameTable* 
     }
 }
 
-// tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.  t: the global
-// sample id (buffers), tl: the sample within its frame (pixel).
-template <int L, bool FRESH>
-__device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, const float4* __restrict__ res,
+// tracescreen.hlsl:22-35 (hit branch) through the first shadow-march step.  r0..r2: the hit's
+// record (hit_store), t: the global sample id (buffers), tl: the sample within its frame (pixel).
+template <int L>
+__device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, float4 r0, float4 r1, float4 r2,
                                               uint32_t t, uint32_t tl, March<L, true>& st)
 {
     const RtConsts* k = c.k;
@@ -598,15 +603,14 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, co
     ShadeHit h;
     float4 pdw, dn;
     if constexpr (FogLive<L>::value) {
-        pdw = FRESH ? ld_fresh(res + 3u * t) : res[3u * t];
-        dn = FRESH ? ld_fresh(res + 3u * t + 2u) : res[3u * t + 2u];
-        h.fog = FRESH ? ld_fresh(res + 3u * t + 1u) : res[3u * t + 1u];
-    } else { // store_ray's fog-free layout; fcolord is 0
-        const float* r = reinterpret_cast<const float*>(res) + 3u * t;
-        const float2 sdw = make_float2(FRESH ? ld_fresh1(r) : r[0], FRESH ? ld_fresh1(r + 1) : r[1]);
-        const float* dp = r + 2;
-        pdw = make_float4(sdw.x, 0.0f, 0.0f, sdw.y); // (sd, -, -, dist) until the position is re-derived
-        dn = make_float4(FRESH ? ld_fresh1(dp) : *dp, 0.0f, 0.0f, 0.0f);
+        pdw = r0;
+        h.fog = r1;
+        dn = r2;
+    } else { // hit_store's fog-free layout; fcolord is 0
+        (void)r1;
+        (void)r2;
+        pdw = make_float4(r0.x, 0.0f, 0.0f, r0.y); // (sd, -, -, dist) until the position is re-derived
+        dn = make_float4(r0.z, 0.0f, 0.0f, 0.0f);
         h.fog = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     uint32_t px, py, a;
@@ -736,20 +740,20 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
 // Fused trace (default pipeline): the primary march, the hit shading and the long
 // shadow rays in ONE persistent kernel, so the latency-bound shading phases run in
 // the shadow of the VALU-bound primary march instead of after it.  Each CU keeps
-// two block-local rings in LDS, fed and drained by its own 16 waves:
-//   hits  : sample ids of primary hits (pushed by a wave when it finishes a unit);
+// two block-local queues, fed and drained by its own 16 waves:
+//   hits  : the records of primary hits (hit_store; pushed by a wave when it finishes a unit),
+//           a stack per block in HBM (its top lines live in the XCD's L2);
 //   longs : march state of shadow rays still live after their first step (pushed
-//           by a wave when it finishes a shading batch).
+//           by a wave when it finishes a shading batch), a ring in LDS.
 // A wave's next job, in priority order: march long shadows (lane refill from the
 // ring) when enough are queued; shade a batch of 64 queued hits; march the next
-// primary unit from the global longest-first queue.  Ring operations hold a
-// per-block LDS lock for a few instructions.  Every hand-off stays on one CU: the
-// producer's global stores (res / fin) complete (s_waitcnt) before the ring push,
-// and the consumer reads them with L1-bypassing loads from the XCD's L2.  A full
-// ring spills to the block's spill ring in HBM (the same block consumes it, so the hand-off stays
-// on one CU like the LDS rings' own): a block never hands work to another kernel.
-constexpr uint32_t kHitRing = 512;
-constexpr uint32_t kLongRing = 528; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + rings
+// primary unit from the global longest-first queue.  Queue operations hold a
+// per-block LDS lock.  Every hand-off stays on one CU: the producer's global stores
+// (hit records, fin) complete (s_waitcnt) before the push publishes them, and the consumer
+// reads them with L1-bypassing loads from the XCD's L2.  A full long ring spills to the block's
+// spill ring in HBM (the same block consumes it, so the hand-off stays on one CU like the LDS
+// ring's own): a block never hands work to another kernel.
+constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + the ring
 #ifndef RT_LONG_BATCH // A/B: make variant FLAGS=-DRT_LONG_BATCH=n
 #define RT_LONG_BATCH 128
 #endif
@@ -769,14 +773,13 @@ struct BlockStats {
 
 struct TraceQueues {
     uint32_t lock;
-    uint32_t h_head, h_tail;
+    uint32_t h_top, pad0; // the block's hit stack (HBM, hit_cap records): records [0, h_top) are queued
     uint32_t l_head, l_tail;
     uint32_t active;  // waves inside a primary unit or a shading batch (they may still push)
     uint32_t drained; // the global unit queue is exhausted
     uint32_t pad;
-    uint32_t hs_head, hs_tail; // the block's hit spill ring (HBM), when the LDS hit ring is full
     uint32_t ls_head, ls_tail; // the block's long-ray spill ring (HBM)
-    uint32_t hits[kHitRing];
+    uint32_t pad2[2];
     float4 longs[kLongRing * kShadowRec];
 };
 
@@ -826,14 +829,13 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
                                                 UnitMap m, const uint32_t* __restrict__ order,
-                                                uint64_t* __restrict__ hitmask,
-                                                float4* __restrict__ res, float4* __restrict__ samples,
-                                                float4* __restrict__ fin, uint32_t* __restrict__ spill_hits,
-                                                float4* __restrict__ spill_long, uint32_t hit_spill_cap,
+                                                uint64_t* __restrict__ hitmask, float4* __restrict__ samples,
+                                                float4* __restrict__ fin, float4* __restrict__ hitq,
+                                                float4* __restrict__ spill_long, uint32_t hit_cap,
                                                 uint32_t long_spill_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live, uint32_t hit_ring_cap, uint32_t long_ring_cap)
+                                                uint32_t compact_live, uint32_t long_ring_cap)
 {
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
@@ -846,11 +848,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     frame_rays_load(s_fr, ft, m.n_frames);
     if (threadIdx.x == 0) {
         q.lock = 0;
-        q.h_head = q.h_tail = 0;
+        q.h_top = 0;
         q.l_head = q.l_tail = 0;
         q.active = 0;
         q.drained = 0;
-        q.hs_head = q.hs_tail = 0;
         q.ls_head = q.ls_tail = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
@@ -860,12 +861,13 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     if constexpr (STATS) c.nz.lds_calls = (__attribute__((address_space(3))) unsigned long long*)&s_st.v[BlockStats::NOISE];
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
-    // this block's spill rings (records hit_spill_cap / long_spill_cap per block)
-    uint32_t* const hspill = spill_hits + (size_t)blockIdx.x * hit_spill_cap;
+    // this block's hit stack and long-ray spill ring (hit_cap / long_spill_cap records per block)
+    constexpr uint32_t HR = HitRec<L>::N;
+    float4* const hq = hitq + (size_t)blockIdx.x * hit_cap * HR;
     float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
-    // queued work of the block: LDS ring + spill ring
+    // queued work of the block: long rays in the LDS ring + spill ring, hits in the hit queue
     auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_tail) - vload(q.ls_head); };
-    auto queued_hits = [&]() { return vload(q.h_tail) - vload(q.h_head) + vload(q.hs_tail) - vload(q.hs_head); };
+    auto queued_hits = [&]() { return vload(q.h_top); };
     // STATS: march steps and hits go to the block's LDS counters (no VGPRs held across the loops)
     auto stat = [&](int i, uint32_t v) {
         if constexpr (STATS) atomicAdd(&s_st.v[i], (unsigned long long)v);
@@ -970,22 +972,21 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     // ---- a batch of up to 64 queued hits: shading + first shadow step ----
     auto do_shade = [&]() {
         q_lock(&q.lock, lane);
-        const uint32_t head = vload(q.h_head), tail = vload(q.h_tail);
-        uint32_t take = (tail - head) < 64u ? (tail - head) : 64u;
-        uint32_t t = 0;
-        if (lane < take) t = q.hits[(head + lane) % kHitRing];
-        if (lane == 0) q.h_head = head + take;
-        // the block's spill ring tops the batch up
-        const uint32_t sh = vload(q.hs_head), sl = vload(q.hs_tail);
-        const uint32_t spilled = (sl - sh) < 64u - take ? (sl - sh) : 64u - take;
-        if (spilled) {
-            if (lane >= take && lane < take + spilled)
-                t = __builtin_nontemporal_load(hspill + (sh + lane - take) % hit_spill_cap);
-            if (lane == 0) q.hs_head = sh + spilled;
-            take += spilled;
-            __builtin_amdgcn_s_waitcnt(0); // read before the slots can be reused
+        const uint32_t top = vload(q.h_top);
+        const uint32_t take = top < 64u ? top : 64u;
+        float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0;
+        if (lane < take) {
+            const float4* r = hq + (size_t)(top - take + lane) * HR;
+            r0 = ld_fresh(r);
+            if constexpr (HR == 3u) {
+                r1 = ld_fresh(r + 1);
+                r2 = ld_fresh(r + 2);
+            }
         }
+        __builtin_amdgcn_s_waitcnt(0); // read before the slots can be reused
+        if (lane == 0) q.h_top = top - take;
         q_unlock(&q.lock, lane);
+        const uint32_t t = __float_as_uint(HR == 3u ? r2.w : r0.w);
         March<L, true> st;
         bool more = false;
         const bool valid = lane < take;
@@ -993,7 +994,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
             Ctx cf = frame_ctx(c, ft, f);
             cf.nz.phase = RT_PHASE_SHADE;
-            h = shade_hit<L, true>(cf, m, res, t, t - f * m.frame_samples, st);
+            h = shade_hit<L>(cf, m, r0, r1, r2, t, t - f * m.frame_samples, st);
             c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
@@ -1062,12 +1063,11 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             __builtin_amdgcn_s_setprio(0);
             const bool hit = valid && st.d > 0.0f;
             WT(if (valid) wp_maxit = max(wp_maxit, (uint32_t)st.iters);)
+            RayResult rr;
             if (valid) {
-                RayResult rr = march_result(st);
+                rr = march_result(st);
                 stat(BlockStats::PRIMARY, (uint32_t)st.iters);
-                if (hit) {
-                    store_ray<L>(res, m.frame_samples * m.n_frames, t, rr); // the shading input
-                } else {
+                if (!hit) {
                     const float4 v = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
                     if (aa == 1u) { // the pixel is final (k_finish's sum of one sample times rcp(1) is v itself)
                         const size_t o = (size_t)py * W + px;
@@ -1081,20 +1081,17 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             const uint64_t hb = __ballot(hit);
             if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = hb; // k_finish skips the misses
             if (hb) {
+                // the hits' records go on the block's hit stack in rank order (dense lines), stored
+                // before the top publishes them.  The stack never overflows: a wave starts a unit
+                // only while fewer than 64 hits are queued, so at most 63 + 16 waves x 64 x aa are
+                // (rt_spill_caps' hit_cap).
                 const uint32_t n = (uint32_t)__popcll(hb), rank = lane_rank(hb);
                 if (hit) stat(BlockStats::HITS, 1u);
-                __builtin_amdgcn_s_waitcnt(0); // res[t] is in L2 before the hit is visible
                 q_lock(&q.lock, lane);
-                const uint32_t hh = vload(q.h_head), ht = vload(q.h_tail);
-                if (ht - hh + n <= hit_ring_cap) {
-                    if (hit) q.hits[(ht + rank) % kHitRing] = t;
-                    if (lane == 0) q.h_tail = ht + n;
-                } else { // the LDS ring is full: the block's spill ring, stored before the tail publishes it
-                    const uint32_t sl = vload(q.hs_tail);
-                    if (hit) hspill[(sl + rank) % hit_spill_cap] = t;
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (lane == 0) q.hs_tail = sl + n;
-                }
+                const uint32_t top = vload(q.h_top);
+                if (hit) hit_store<L>(hq + (size_t)(top + rank) * HR, t, rr);
+                __builtin_amdgcn_s_waitcnt(0);
+                if (lane == 0) q.h_top = top + n;
                 q_unlock(&q.lock, lane);
             }
         }
@@ -1371,9 +1368,9 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
         hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m,
-                           a.order, a.hitmask, a.res, a.samples, a.fin, a.spill_hits, a.spill_long, a.hit_spill_cap,
+                           a.order, a.hitmask, a.samples, a.fin, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
-                           a.small_rings ? 64u : kHitRing, a.small_rings ? 64u : kLongRing);
+                           a.small_rings ? 64u : kLongRing);
         hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});

@@ -117,10 +117,9 @@ struct rt_device_s {
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
     float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
-    float4* res = nullptr;
-    uint32_t* spill_hits = nullptr; // k_trace's per-block spill rings (rt_spill_caps per block)
+    float4* hitq = nullptr;       // k_trace's per-block hit queues and long-ray spill rings (rt_spill_caps per block)
     float4* spill_long = nullptr;
-    size_t spill_hits_n = 0, spill_long_n = 0; // entries allocated (all blocks)
+    size_t hitq_n = 0, spill_long_n = 0; // records allocated (all blocks)
     uint32_t* order = nullptr;
     uint64_t* hitmask = nullptr; // per unit and AA sample: the primary-hit ballot (k_trace -> k_finish)
     float4* fin = nullptr;
@@ -443,12 +442,11 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.queue = dev->queue;
     a.num_cus = dev->num_cus;
     a.samples = dev->samples;
-    a.res = dev->res;
     a.order = dev->order;
     a.hitmask = dev->hitmask;
-    a.spill_hits = dev->spill_hits;
+    a.hitq = dev->hitq;
     a.spill_long = dev->spill_long;
-    rt_spill_caps(s->aa, s->ao, &a.hit_spill_cap, &a.long_spill_cap);
+    rt_spill_caps(s->aa, s->ao, &a.hit_cap, &a.long_spill_cap);
     a.cells_from_cam = 0;
     a.small_rings = (dev->flags & RT_DEVICE_DEBUG_SMALL_RINGS) ? 1 : 0;
     a.fin = dev->fin;
@@ -482,35 +480,32 @@ int check_texture(Shader* s)
     return RT_OK;
 }
 
-// Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded
-// colour (16 B; 12 B used with one sample per pixel), one primary RayResult (48 B; 12 B used
-// without fog), one hit-list slot (4 B), the shading inputs of a long shadow ray (48 B; 32 B used
-// without fog), an AO occlusion count (1 B) and a hit bit (the 64-lane ballot per 8x8 unit and
-// AA sample); the global long-ray list holds up to one shadow ray plus `ao` AO rays per sample
-// (48 B each).
+// Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded colour (16 B; 12 B used
+// with one sample per pixel), the shading inputs of a long shadow ray (48 B; 32 B used without
+// fog), an AO occlusion count (1 B) and a hit bit (the 64-lane ballot per 8x8 unit and AA sample).
+// Per block (one per CU): k_trace's hit queue (hit records of up to 48 B) and long-ray spill ring
+// (48 B records), rt_spill_caps records each.
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
-    // k_trace's spill rings: rt_spill_caps per block, one block per CU
     uint32_t hcap, lcap;
     rt_spill_caps(aa, ao, &hcap, &lcap);
-    const size_t hs_need = (size_t)dev->num_cus * hcap, ls_need = (size_t)dev->num_cus * lcap;
-    if (hs_need > dev->spill_hits_n || ls_need > dev->spill_long_n) {
+    const size_t hq_need = (size_t)dev->num_cus * hcap, ls_need = (size_t)dev->num_cus * lcap;
+    if (hq_need > dev->hitq_n || ls_need > dev->spill_long_n) {
         HIP_TRY(hipStreamSynchronize(dev->stream));
-        if (dev->spill_hits) HIP_TRY(hipFree(dev->spill_hits));
+        if (dev->hitq) HIP_TRY(hipFree(dev->hitq));
         if (dev->spill_long) HIP_TRY(hipFree(dev->spill_long));
-        dev->spill_hits = nullptr;
+        dev->hitq = nullptr;
         dev->spill_long = nullptr;
-        dev->spill_hits_n = dev->spill_long_n = 0;
-        HIP_TRY(hipMalloc(&dev->spill_hits, hs_need * sizeof(uint32_t)));
+        dev->hitq_n = dev->spill_long_n = 0;
+        HIP_TRY(hipMalloc(&dev->hitq, hq_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
-        dev->spill_hits_n = hs_need;
+        dev->hitq_n = hq_need;
         dev->spill_long_n = ls_need;
     }
     size_t need = rt_split_samples(dev->width, dev->height, aa) * (size_t)n_frames;
     if (need <= dev->samples_cap) return RT_OK;
     HIP_TRY(hipStreamSynchronize(dev->stream));
     if (dev->samples) HIP_TRY(hipFree(dev->samples));
-    if (dev->res) HIP_TRY(hipFree(dev->res));
     if (dev->order) HIP_TRY(hipFree(dev->order));
     if (dev->hitmask) HIP_TRY(hipFree(dev->hitmask));
     if (dev->fin) HIP_TRY(hipFree(dev->fin));
@@ -518,12 +513,10 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     dev->fin = nullptr;
     dev->aocc = nullptr;
     dev->samples = nullptr;
-    dev->res = nullptr;
     dev->order = nullptr;
     dev->hitmask = nullptr;
     dev->samples_cap = 0;
     HIP_TRY(hipMalloc(&dev->samples, need * sizeof(float4)));
-    HIP_TRY(hipMalloc(&dev->res, need * 3 * sizeof(float4)));
     HIP_TRY(hipMalloc(&dev->fin, need * 3 * sizeof(float4)));
     // AO counts, a byte per sample (ao_count): zero once here; k_finish clears what it reads
     HIP_TRY(hipMalloc(&dev->aocc, (need + 3) / 4 * sizeof(uint32_t)));
@@ -605,7 +598,7 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)res, (void*)spill_hits, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
+                    (void*)hitq, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
@@ -1132,8 +1125,8 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
     const uint64_t v[] = {(uint64_t)(uintptr_t)a.stream, (uint64_t)a.landscape, (uint64_t)(uintptr_t)a.consts,
                           (uint64_t)(uintptr_t)a.perm2d, (uint64_t)(uintptr_t)a.grad, (uint64_t)(uintptr_t)a.stats,
                           (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
-                          (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.res, (uint64_t)(uintptr_t)a.spill_hits,
-                          (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_spill_cap, (uint64_t)a.long_spill_cap,
+                          (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.hitq,
+                          (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_cap, (uint64_t)a.long_spill_cap,
                           (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)(uintptr_t)a.fin,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};

@@ -96,7 +96,7 @@ class BatchPlan:
 
     CAMERA_FLOATS = 1024 * 4  # CameraResults of one frame: float4[1024]
 
-    def __init__(self, width, height, batch, world, split_prepass=True):
+    def __init__(self, width, height, batch, world, split_prepass=False):
         if not 1 <= batch <= 16:
             raise ValueError("batch must be 1..16 frames (RT_MAX_BATCH)")
         self.width, self.height, self.batch, self.world = int(width), int(height), int(batch), int(world)

@@ -3,6 +3,17 @@ time rank r's share (tile-cyclic, rt_terrain_render_batch(.., r, N)) of B-frame 
 batches in flight (engine.FrameRing(depth=D, batch=B)), steady state.  The N-GPU frame time is
 bounded below by max_r of these (plus the gather), so t(N=1) / max_r t(r, N) is the ceiling.
 Usage: python scripts/batch_shard_sim.py [--batches 1,4,8] [--depth 2] [--ns 1,2,4,8]
+
+--barrier-model: the split prepass's all-gather couples the ranks every batch.
+Per rank and batch, one batch at a time on the card (synchronised), it times the rank's prepass
+chunk P_r(b), the full B-frame prepass P(b) and the rank's trace T_r(b) (setTargetDepths +
+tracescreen of its shard), and models
+  recompute (no collective before the trace):  max_r sum_b (P(b) + T_r(b))
+  split, no barrier (the earlier, optimistic reading):     max_r sum_b (P_r(b) + T_r(b))
+  split + all-gather barrier:  sum_b [max_r (T_r(b-1) + P_r(b)) + L]
+(rank r's prepass chunk of batch b runs when its trace of batch b-1 ends, since k_trace holds every
+CU; batch b's trace starts on every rank once the slowest rank's chunk is in and the all-gather,
+L = --gather-us, has run), each divided by the frames.
 """
 import argparse
 import json
@@ -28,7 +39,12 @@ def main():
                     help="1: rank r runs only its ceil(B/N) frames' prepass (bench.py --split-prepass; the "
                          "all-gather is not simulated: the other frames' CameraResults come from a full prepass "
                          "run once before timing)")
+    ap.add_argument("--barrier-model", action="store_true")
+    ap.add_argument("--gather-us", type=float, default=40.0,
+                    help="modelled all-gather latency per batch (16 KiB per frame over xGMI)")
     a = ap.parse_args()
+    if a.barrier_model:
+        return barrier_model(a)
     import torch
     import gpgpuraytrace_amd as G
     W, H = a.width, a.height
@@ -72,6 +88,63 @@ def main():
                 base = worst
             print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
+        ring.destroy()
+
+
+def barrier_model(a):
+    import torch
+    import gpgpuraytrace_amd as G
+    W, H = a.width, a.height
+    cam = G.Camera(W, H)
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3
+
+    for B in [int(x) for x in a.batches.split(",")]:
+        ring = G.FrameRing(W, H, depth=1, batch=B, camera=cam, time_of_day=0.3, max_steps=a.max_steps,
+                           ao_samples=a.ao)
+        ters = [t for _, t in ring.slots[:B]]
+        buf = torch.zeros(B * 1024 * 4, dtype=torch.float32, device="cuda:0")
+        nb = max(2, a.frames // B)
+        for n in [int(x) for x in a.ns.split(",")]:
+            chunk = -(-B // n)
+            P, Pr, T = [], [], []  # P[b], Pr[r][b], T[r][b] in ms
+            for r in range(n):
+                lo, cnt = min(r * chunk, B), max(0, min(B - r * chunk, chunk))
+                pr, tr = [], []
+                for b in range(nb + 1):  # the first batch warms up
+                    if r == 0:
+                        p = timed(lambda: G.engine.prepass_batch(ters, 0, B, buf.data_ptr()))
+                        if b:
+                            P.append(p)
+                    else:
+                        G.engine.prepass_batch(ters, 0, B, buf.data_ptr())
+                    p = timed(lambda: G.engine.prepass_batch(ters, lo, cnt, buf.data_ptr())) if cnt else 0.0
+                    t = timed(lambda: G.engine.trace_batch(ters, r, n, buf.data_ptr()))
+                    if b:
+                        pr.append(p)
+                        tr.append(t)
+                Pr.append(pr)
+                T.append(tr)
+            frames = nb * B
+            recompute = max(sum(P[b] + T[r][b] for b in range(nb)) for r in range(n)) / frames
+            split_free = max(sum(Pr[r][b] + T[r][b] for b in range(nb)) for r in range(n)) / frames
+            L = a.gather_us / 1e3 if n > 1 else 0.0
+            # batch 0's chunk starts at time 0 on every rank; batch b's chunk after the rank's trace of b-1
+            split_barrier = (max(Pr[r][0] for r in range(n)) + L
+                             + sum(max(T[r][b - 1] + Pr[r][b] for r in range(n)) + L for b in range(1, nb))
+                             + max(T[r][nb - 1] for r in range(n))) / frames
+            print(json.dumps({"batch": B, "n": n, "batches": nb, "gather_us": a.gather_us,
+                              "ms_per_frame": {"recompute": round(recompute, 4), "split_no_barrier": round(split_free, 4),
+                                               "split_barrier": round(split_barrier, 4)},
+                              "prepass_full_ms": round(sum(P) / len(P), 4),
+                              "prepass_chunk_ms": [round(sum(x) / len(x), 4) for x in Pr],
+                              "trace_ms": [round(sum(x) / len(x), 4) for x in T],
+                              "trace_spread_ms": [round(max(x) - min(x), 4) for x in T]}), flush=True)
         ring.destroy()
 
 

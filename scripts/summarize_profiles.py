@@ -15,7 +15,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-TRACESCREEN = ("k_order", "k_trace", "k_primary", "k_shade", "k_shadow", "k_finish", "k_march")
+TRACESCREEN = ("k_order", "k_trace", "k_finish")
 
 
 def instrumented(name):
@@ -58,7 +58,7 @@ def main(src, dst):
                     f"{float(r['TotalDurationNs']) / 1e6:.3f} |\n")
         plain = {short(r["Name"]): float(r["AverageNs"]) / 1e6 for r in rows}
         ts = sum(v for k, v in plain.items() if any(k.startswith(t) for t in TRACESCREEN) and not instrumented(k))
-        f.write(f"\ntracescreen (uninstrumented k_order + k_trace + k_shade_pre + k_shadow + k_finish) avg sum: {ts:.4f} ms\n")
+        f.write(f"\ntracescreen (uninstrumented k_order + k_trace + k_finish) avg sum: {ts:.4f} ms\n")
         f.write(f"\nbench line of the same run:\n\n```\n{bench}\n```\n")
     # the bench's roofline pass = its last K tracescreen launches (one frame in flight): per-kernel
     # means and the launch span (k_order start -> k_finish end) over exactly those dispatches
@@ -114,7 +114,7 @@ def main(src, dst):
     tr[key] = {"hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024),
                "fetch_size_kib": fetch, "write_size_kib": write,
                "tcc_ea0_rdreq": rd, "tcc_ea0_wrreq": wr,
-               "kernels": "tracescreen launch: k_order + k_trace + k_shade_pre + k_shadow + k_finish (uninstrumented)",
+               "kernels": "tracescreen launch: k_order + k_trace + k_finish (uninstrumented)",
                "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section)"}
     if fetch == 0.0 and write == 0.0:  # a kernel-trace-only profile (PMC=0): no traffic to record
         print(open(os.path.join(dst, "kernels.md")).read())

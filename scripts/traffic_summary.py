@@ -24,7 +24,7 @@ for f in glob.glob(src + "/**/*counter_collection.csv", recursive=True):
             tot[name][c].append(v)
 s = 0.0
 for k in sorted(tot):
-    if any(k.startswith(x) for x in ("k_trace", "k_finish", "k_shade", "k_shadow", "k_order")):
+    if any(k.startswith(x) for x in ("k_trace", "k_finish", "k_order")):
         d = {c: sum(v) / len(v) for c, v in tot[k].items()}
         b = (2 * d.get("FETCH_SIZE", 0) + d.get("WRITE_SIZE", 0)) * 1024
         s += b
@@ -39,13 +39,13 @@ if len(sys.argv) > 3:
     key = (f"{cf['width']}x{cf['height']}_{cf['landscape']}_{cf['pose']}_ms{cf['max_steps']}_ao{cf.get('ao_samples', 0)}"
            f"_b{cf.get('batch', 1)}")
     fetch = sum(sum(v) / len(v) for k, cs in tot.items() for c, v in cs.items() if c == "FETCH_SIZE"
-                and any(k.startswith(x) for x in ("k_trace", "k_finish", "k_shade", "k_shadow", "k_order")))
+                and any(k.startswith(x) for x in ("k_trace", "k_finish", "k_order")))
     write = sum(sum(v) / len(v) for k, cs in tot.items() for c, v in cs.items() if c == "WRITE_SIZE"
-                and any(k.startswith(x) for x in ("k_trace", "k_finish", "k_shade", "k_shadow", "k_order")))
+                and any(k.startswith(x) for x in ("k_trace", "k_finish", "k_order")))
     tj = json.load(open(sys.argv[3])) if os.path.exists(sys.argv[3]) else {}
     tj[key] = {"hbm_bytes_per_launch": int(2 * fetch * 1024 + write * 1024), "fetch_size_kib": fetch,
                "write_size_kib": write,
-               "kernels": "tracescreen launch: k_order + k_trace + k_shade_pre + k_shadow + k_finish (uninstrumented)",
+               "kernels": "tracescreen launch: k_order + k_trace + k_finish (uninstrumented)",
                "rule": "2*FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md HBM section; calibrated, "
                        "profiles/r02/hbm_counter_calibration.txt)"}
     json.dump(tj, open(sys.argv[3], "w"), indent=1)
