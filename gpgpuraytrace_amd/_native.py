@@ -19,7 +19,7 @@ RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
 RT_DEVICE_SEG_TAIL_OFF = 8  # reserved since ABI 4 (no effect)
 RT_DEVICE_SEG_TAIL_ON = 16  # reserved since ABI 4 (no effect)
-RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's LDS rings hold 64 entries (spill-path tests)
+RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
 ABI_VERSION = 4  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3

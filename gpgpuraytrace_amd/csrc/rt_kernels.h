@@ -40,8 +40,9 @@ struct RtLaunch {
     float4* spill_long;       // long-ray records (3 float4) the LDS ring cannot hold, long_spill_cap per block
     uint32_t hit_cap, long_spill_cap;
     int cells_from_cam;       // k_order derives CellDistance from CameraResults (setTargetDepths) first
-    int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS long ring holds 64 entries
+    int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS long ring holds 64 entries, its fin pool 8
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
+    float4* finpool;          // the same per block in a pool of RT_FIN_SLOTS slots of 3 float4 (fin is the fallback)
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
@@ -64,6 +65,7 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, ui
                            uint32_t tile_first, uint32_t tile_stride);
 
 #define RT_TILE 32
+#define RT_FIN_SLOTS 1536 // k_trace's fin pool slots per block
 // k_trace's queue capacities per block (1024 threads = 16 waves): the hit queue and the long-ray
 // spill ring.  A wave starts a primary unit only while fewer than 64 hits are queued and starts
 // shading only while fewer than 128 long rays are (k_trace's work priority), so a block never

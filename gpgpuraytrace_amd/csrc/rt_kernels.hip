@@ -505,8 +505,17 @@ __device__ __forceinline__ float4 ld_fresh(const float4* p)
 // finished where their march ends) and every sample k_finish reads is a hit, so the record is the
 // colour alone: 12 B (a float3 array over the same buffer); with AA, misses are stored too and w
 // marks the hits (16 B).
+// An opaque copy of a lane value: address arithmetic on it cannot be hoisted above this point, so a
+// store's 64-bit address is formed where the store is (one VGPR live before it, not two).
+__device__ __forceinline__ uint32_t late(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 __device__ __forceinline__ void sample_store(const RtConsts* k, float4* __restrict__ samples, uint32_t t, float4 v)
 {
+    t = late(t);
     if (k->aa_samples == 1) { // 3 floats at 12-byte stride (a float3 vector type would pad to 16)
         float* c = reinterpret_cast<float*>(samples) + 3u * t;
         c[0] = v.x;
@@ -537,7 +546,6 @@ struct ShadeHit {
     uint32_t px, py, a;
 };
 
-enum { RT_LONG_SHADOW = 0, RT_LONG_AO = 1 };
 
 // frame f's context (f wave-uniform): its constant block (camera, sun) as cf.kf, its Eye and
 // SunDirection in scalar registers; the launch's block c.k stays the source of every
@@ -626,13 +634,20 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, fl
         const float sd = pdw.x;
         pdw = make_float4(fma(md.x, sd, p.x), fma(md.y, sd, p.y), fma(md.z, sd, p.z), pdw.w);
     }
+    f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
+    h.hp = hp;
+    // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): the first step,
+    // taken before the normal and the colour (it needs neither; precision is the hit distance's),
+    // so the colour's FBM and the step's density never hold their live values at the same time
+    h.prec = shade_precision(pdw.w);
+    march_begin(c, st, hp, 0.4f, h.prec, c.sun);
+    if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
+    h.more = march_live<L, true, true>(c, st, 100.0f, 0);
     f3 pdn = rtm::normalize(dir);
     float skyAmount = pdw.w * 0.0005f;
     skyAmount = rtm::sat(skyAmount * skyAmount);
     f4 pd = {pdw.x, pdw.y, pdw.z, dn.x}; // getNormal(float4(rr.pd.xyz, rr.density)) :31
     f3 n = get_normal<L>(c, pd);
-    f3 hp = rtm::mk(pdw.x, pdw.y, pdw.z);
-    h.hp = hp;
     h.n = n;
     ShadePre sp = shade_pre<L>(c, hp, n, pdn, pdw.w);
     // color.hlsl:63-66: the specular term does not depend on the shadow
@@ -640,43 +655,41 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, fl
     SkyColor scat = get_rayleigh_mie(c, pdn);
     h.cb = make_float4(sp.col[0] + specular, sp.col[1] + specular, sp.col[2] + specular, sp.brightness);
     h.ray = make_float4(scat.rayleigh.x, scat.rayleigh.y, scat.rayleigh.z, skyAmount);
-    h.prec = sp.precision;
-    // color.hlsl:51 traceRay(p, 0.4, 100, precision, SunDirection, fog, skiprefine): first step
-    march_begin(c, st, hp, 0.4f, sp.precision, c.sun);
-    if (march_live<L, true, true>(c, st, 100.0f, 0)) march_step<L, true, true>(c, st);
-    h.more = march_live<L, true, true>(c, st, 100.0f, 0);
     return h;
 }
 
-// Long-ray record (48 B): (p, dist), (step, lastStep, iters | type << 31, t),
-// (shadow fog | AO dir; a fog-free landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
-// length(SunDirection) (tracing.hlsl:60-61) for every ray; an AO ray carries its own
-// (normalised) direction in the fog slot, since AO rays march without fog.  The
-// density d is not kept: a stored ray is live, so its next step overwrites d before
-// anything reads it.
+// A long ray's `aux` word: an AO ray (kAuxAO), or a shadow ray whose finishing inputs (fin_store)
+// sit in its block's fin pool slot aux (< kFinSlots), or at fin[t] when the pool was empty (kAuxFinT).
+constexpr uint32_t kAuxAO = 0xffffffffu, kAuxFinT = 0xfffffffeu;
+
+// Long-ray record (48 B): (p, dist), (step, aux, iters, t), (shadow fog | AO dir; a fog-free
+// landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
+// length(SunDirection) (tracing.hlsl:60-61) for every ray; an AO ray carries its own (normalised)
+// direction in the fog slot, since AO rays march without fog.  The density d is not kept: a stored
+// ray is live, so its next step overwrites d before anything reads it; nor is lastStep, which only
+// the refinement after a hit reads (tracing.hlsl:76-79) and SKIPREFINE rays break before it.
 template <int L>
-__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t type, float4* r)
+__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t aux, float4* r)
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
-    r[1] = make_float4(st.step, st.lastStep, __uint_as_float((uint32_t)st.iters | (type << 31)), __uint_as_float(t));
-    if (type == RT_LONG_AO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
+    r[1] = make_float4(st.step, __uint_as_float(aux), __uint_as_float((uint32_t)st.iters), __uint_as_float(t));
+    if (aux == kAuxAO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
     else if constexpr (March<L, true>::FOG) r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
     // no fog: a shadow ray's f is +0 throughout (march_step), so r2 is neither written nor read
 }
 
 template <int L>
 __device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1, const float4 r2, f3 sun_dir,
-                                                March<L, true>& st, uint32_t* type)
+                                                March<L, true>& st, uint32_t* aux)
 {
-    const uint32_t it = __float_as_uint(r1.z);
-    *type = it >> 31;
+    *aux = __float_as_uint(r1.y);
     st.p = rtm::mk(r0.x, r0.y, r0.z);
     st.dist = r0.w;
     st.step = r1.x;
-    st.lastStep = r1.y;
+    st.lastStep = 0.0f; // not read (SKIPREFINE)
     st.d = 0.0f;
-    st.iters = (int)(it & 0x7fffffffu);
-    if (*type == RT_LONG_AO) {
+    st.iters = (int)__float_as_uint(r1.z);
+    if (*aux == kAuxAO) {
         st.dir = rtm::mk(r2.x, r2.y, r2.z);
         st.f = {0.0f, 0.0f, 0.0f, 0.0f};
         st.fog = false;
@@ -699,40 +712,40 @@ __device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32
 }
 
 // The inputs a long shadow ray needs to finish its sample: (albedo + specular, brightness), fcolord
-// (fog-live landscapes only; 0 otherwise) and (rayleigh, skyAmount).
+// (fog-live landscapes only; 0 otherwise) and (rayleigh, skyAmount): FinRec<L>::N float4 at f, a
+// slot of the block's fin pool or fin[t].
 template <int L>
-__device__ __forceinline__ void fin_store(float4* __restrict__ fin, uint32_t t, const ShadeHit& h)
+struct FinRec {
+    static constexpr uint32_t N = FogLive<L>::value ? 3u : 2u;
+};
+template <int L>
+__device__ __forceinline__ void fin_store(float4* __restrict__ f, const ShadeHit& h)
 {
     if constexpr (FogLive<L>::value) {
-        fin[3u * t + 0u] = h.cb;
-        fin[3u * t + 1u] = h.fog;
-        fin[3u * t + 2u] = h.ray;
+        f[0] = h.cb;
+        f[1] = h.fog;
+        f[2] = h.ray;
     } else {
-        fin[2u * t + 0u] = h.cb;
-        fin[2u * t + 1u] = h.ray;
+        f[0] = h.cb;
+        f[1] = h.ray;
     }
 }
 
-// A long ray left its loop: a shadow ray finishes its sample from fin[t]; an AO ray
+// A long ray left its loop: a shadow ray finishes its sample from its fin record; an AO ray
 // counts its occlusion for k_finish.
-template <int L, bool FRESH>
+template <int L>
 __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __restrict__ fin,
-                                            float4* __restrict__ samples, uint32_t* __restrict__ aocc, uint32_t t,
-                                            uint32_t type, const March<L, true>& st)
+                                            const float4* __restrict__ finp, float4* __restrict__ samples,
+                                            uint32_t* __restrict__ aocc, uint32_t t, uint32_t aux,
+                                            const March<L, true>& st)
 {
-    if (type == RT_LONG_AO) {
+    if (aux == kAuxAO) {
         if (st.d > 0.0f) ao_count(aocc, t);
     } else {
-        if constexpr (FogLive<L>::value) {
-            const float4* f = fin + 3u * t;
-            sample_store(k, samples, t, FRESH ? shade_finish(k, ld_fresh(f), ld_fresh(f + 1), ld_fresh(f + 2), st.d, st.f.w)
-                                              : shade_finish(k, f[0], f[1], f[2], st.d, st.f.w));
-        } else { // fin_store's fog-free layout
-            const float4* f = fin + 2u * t;
-            const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            sample_store(k, samples, t, FRESH ? shade_finish(k, ld_fresh(f), zero, ld_fresh(f + 1), st.d, st.f.w)
-                                              : shade_finish(k, f[0], zero, f[1], st.d, st.f.w));
-        }
+        constexpr uint32_t FR = FinRec<L>::N;
+        const float4* f = aux == kAuxFinT ? fin + (size_t)FR * t : finp + (size_t)FR * aux;
+        const float4 fog = FogLive<L>::value ? ld_fresh(f + 1) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        sample_store(k, samples, t, shade_finish(k, ld_fresh(f), fog, ld_fresh(f + FR - 1u), st.d, st.f.w));
     }
 }
 
@@ -754,6 +767,11 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __r
 // spill ring in HBM (the same block consumes it, so the hand-off stays on one CU like the LDS
 // ring's own): a block never hands work to another kernel.
 constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + the ring
+// A block's fin pool: slots of FinRec<L>::N float4 in HBM for the finishing inputs of its long
+// shadow rays, handed out from a LIFO free list in LDS, so the few hundred slots in use at a time
+// are the same lines over and over and stay in the XCD's L2 (fin[t] instead: a sparse write and a
+// re-fetch per long shadow).  An empty pool falls back to fin[t].
+constexpr uint32_t kFinSlots = RT_FIN_SLOTS;
 #ifndef RT_LONG_BATCH // A/B: make variant FLAGS=-DRT_LONG_BATCH=n
 #define RT_LONG_BATCH 128
 #endif
@@ -779,8 +797,9 @@ struct TraceQueues {
     uint32_t drained; // the global unit queue is exhausted
     uint32_t pad;
     uint32_t ls_head, ls_tail; // the block's long-ray spill ring (HBM)
-    uint32_t pad2[2];
+    uint32_t f_top, pad2;      // free slots of the block's fin pool: fin_free[0, f_top)
     float4 longs[kLongRing * kShadowRec];
+    uint16_t fin_free[kFinSlots];
 };
 
 // A fresh read of a ring field another wave may have written: a relaxed workgroup-scope atomic
@@ -824,18 +843,33 @@ __device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
 #define WT(...)
 #endif
 
+// k_trace's block: 16 waves (4 per SIMD, 128 VGPRs each) for the fog-free landscapes; the fog-live
+// one (greenrocks: fog state in every march and record) and simple (its two-plane density) need
+// more than 128 VGPRs and run 12 waves (3 per SIMD, up to 168 VGPRs) instead of spilling.
+#ifndef RT_TRACE_WAVES_FAST // A/B: make variant FLAGS=-DRT_TRACE_WAVES_FAST=12
+#define RT_TRACE_WAVES_FAST 16
+#endif
+#ifndef RT_TRACE_WAVES_WIDE // A/B: make variant FLAGS=-DRT_TRACE_WAVES_WIDE=16
+#define RT_TRACE_WAVES_WIDE 12
+#endif
+template <int L>
+struct TraceThreads {
+    static constexpr uint32_t value = 64u * ((L == RT_GREENROCKS || L == RT_SIMPLE) ? RT_TRACE_WAVES_WIDE : RT_TRACE_WAVES_FAST);
+};
+
 template <int L, bool STATS>
-__global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
+__global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
                                                 UnitMap m, const uint32_t* __restrict__ order,
                                                 uint64_t* __restrict__ hitmask, float4* __restrict__ samples,
-                                                float4* __restrict__ fin, float4* __restrict__ hitq,
+                                                float4* __restrict__ fin, float4* __restrict__ finpool,
+                                                float4* __restrict__ hitq,
                                                 float4* __restrict__ spill_long, uint32_t hit_cap,
                                                 uint32_t long_spill_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live, uint32_t long_ring_cap)
+                                                uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots)
 {
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
@@ -853,8 +887,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         q.active = 0;
         q.drained = 0;
         q.ls_head = q.ls_tail = 0;
+        q.f_top = fin_slots;
         if constexpr (STATS) s_st = BlockStats{};
     }
+    for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
     load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = __lane_id(); // v_mbcnt of constants: rematerialisable (threadIdx & 63 spilled)
     Ctx c = make_ctx(k, lds); // k: frame-invariant constants (per-frame ones: frame_ctx / s_fr)
@@ -864,6 +900,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
     // this block's hit stack and long-ray spill ring (hit_cap / long_spill_cap records per block)
     constexpr uint32_t HR = HitRec<L>::N;
     float4* const hq = hitq + (size_t)blockIdx.x * hit_cap * HR;
+    float4* const finp = finpool + (size_t)blockIdx.x * kFinSlots * FinRec<L>::N;
     float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
     // queued work of the block: long rays in the LDS ring + spill ring, hits in the hit queue
     auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_tail) - vload(q.ls_head); };
@@ -879,22 +916,36 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
     // block's spill ring when the LDS ring is full (stored before the tail publishes them)
-    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t type) {
+    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
         const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
         if (lt - lh + n <= long_ring_cap) {
-            if (want) long_pack(st, t, type, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
+            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
         } else {
             const uint32_t stl = vload(q.ls_tail);
-            if (want) long_pack(st, t, type, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
+            if (want) long_pack(st, t, aux, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
             __builtin_amdgcn_s_waitcnt(0);
             if (lane == 0) q.ls_tail = stl + n;
         }
         q_unlock(&q.lock, lane);
+    };
+
+    // the fin pool slots of finished shadow rays (idle lanes whose aux is a slot) go back to the free
+    // list; the lock is held
+    auto free_fin_locked = [&](bool live, uint32_t& aux) {
+        const bool pend = !live && aux < kFinSlots;
+        const uint64_t pb = __ballot(pend);
+        if (!pb) return;
+        const uint32_t top = vload(q.f_top);
+        if (pend) {
+            q.fin_free[top + lane_rank(pb)] = (uint16_t)aux;
+            aux = kAuxAO;
+        }
+        if (lane == 0) q.f_top = top + (uint32_t)__popcll(pb);
     };
 
     // ---- a batch of long rays, lane refill from the ring ----
@@ -903,20 +954,21 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         st.d = 0.0f;
         st.iters = 0;
         bool live = false;
-        uint32_t t = 0, type = RT_LONG_SHADOW;
+        uint32_t t = 0, aux = kAuxAO; // aux: the lane's ray (long_pack); on an idle lane, a fin slot to free
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
-            if (live && !march_live<L, true, true>(cl, st, type == RT_LONG_AO ? RT_AO_END : 100.0f, 0)) {
-                long_finish<L, true>(k, fin, samples, aocc, t, type, st);
+            if (live && !march_live<L, true, true>(cl, st, aux == kAuxAO ? RT_AO_END : 100.0f, 0)) {
+                long_finish<L>(k, fin, finp, samples, aocc, t, aux, st);
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 live = false;
-                stat(type == RT_LONG_AO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                stat(aux == kAuxAO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
             if (nidle >= refill_idle && queued_long() != 0u) {
                 q_lock(&q.lock, lane);
+                free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
                 // the block's spill ring tops up what the LDS ring cannot give
@@ -925,10 +977,10 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 const uint32_t rank = lane_rank(idle);
                 const bool mine = ((idle >> lane) & 1ull) && rank < take + more;
                 auto take_ray = [&](float4 r0, float4 r1, float4 r2) {
-                    t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &type);
+                    t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
                     const float* fr = s_fr.v[frame_of(m, t)];
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
-                    if (type == RT_LONG_SHADOW) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                    if (aux != kAuxAO) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     live = true;
                 };
                 if (mine && rank < take) {
@@ -945,15 +997,18 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
                 q_unlock(&q.lock, lane);
             }
             const uint64_t lv = __ballot(live);
-            if (lv == 0ull) {
-                c.nz.calls = cl.nz.calls;
-                return;
-            }
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
-            if ((uint32_t)__popcll(lv) < compact_live && queued_long() == 0u && vload(q.drained) == 0u) {
-                push_long(live, st, t, type);
+            const bool hand_back = lv != 0ull && (uint32_t)__popcll(lv) < compact_live && queued_long() == 0u &&
+                                   vload(q.drained) == 0u;
+            if (lv == 0ull || hand_back) {
+                if (__ballot(!live && aux < kFinSlots)) {
+                    q_lock(&q.lock, lane);
+                    free_fin_locked(live, aux);
+                    q_unlock(&q.lock, lane);
+                }
+                if (hand_back) push_long(live, st, t, aux);
                 c.nz.calls = cl.nz.calls;
                 return;
             }
@@ -989,6 +1044,7 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
         const uint32_t t = __float_as_uint(HR == 3u ? r2.w : r0.w);
         March<L, true> st;
         bool more = false;
+        uint32_t aux = kAuxAO;
         const bool valid = lane < take;
         ShadeHit h;
         per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
@@ -1000,19 +1056,30 @@ __global__ void __launch_bounds__(1024) k_trace(const RtConsts* __restrict__ k, 
             if (!more) {
                 sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
                 stat(BlockStats::SHADOW, (uint32_t)st.iters);
-            } else {
-                fin_store<L>(fin, t, h);
+            }
+            // the long shadows' finishing inputs: a fin pool slot each (this frame's lanes are the
+            // active ones: the first of them takes the lock), fin[t] when the pool is empty
+            const uint64_t mb = __ballot(more);
+            if (mb) {
+                const uint32_t lead = (uint32_t)__builtin_ctzll(__ballot(1));
+                q_lock(&q.lock, lane - lead);
+                const uint32_t top = vload(q.f_top), n = (uint32_t)__popcll(mb), rank = lane_rank(mb);
+                const uint32_t got = n < top ? n : top;
+                if (more) aux = rank < got ? (uint32_t)q.fin_free[top - 1u - rank] : kAuxFinT;
+                if (lane == lead) q.f_top = top - got;
+                q_unlock(&q.lock, lane - lead);
+                if (more) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
             }
         });
         if (__ballot(more)) {
-            __builtin_amdgcn_s_waitcnt(0); // fin[t] is in L2 before the ray is visible
-            push_long(more, st, t, RT_LONG_SHADOW);
+            __builtin_amdgcn_s_waitcnt(0); // the fin record is in L2 before the ray is visible
+            push_long(more, st, t, aux);
         }
         // AO extension: the hit's AO rays start as long rays
         for (int kk = 0; kk < k->ao_samples; ++kk) {
             March<L, true> ao;
             if (valid) ao_begin(c, h, (uint32_t)kk, ao);
-            push_long(valid, ao, t, RT_LONG_AO);
+            push_long(valid, ao, t, kAuxAO);
         }
     };
 
@@ -1367,10 +1434,11 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), blk, 0, a.stream, k0, a.frames, a.perm2d, a.grad, m,
-                           a.order, a.hitmask, a.samples, a.fin, a.hitq, a.spill_long, a.hit_cap,
+        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
+                           a.perm2d, a.grad, m,
+                           a.order, a.hitmask, a.samples, a.fin, a.finpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
-                           a.small_rings ? 64u : kLongRing);
+                           a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots);
         hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});

@@ -123,6 +123,7 @@ struct rt_device_s {
     uint32_t* order = nullptr;
     uint64_t* hitmask = nullptr; // per unit and AA sample: the primary-hit ballot (k_trace -> k_finish)
     float4* fin = nullptr;
+    float4* finpool = nullptr; // k_trace's per-block fin pools (RT_FIN_SLOTS slots of 3 float4 per block)
     uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
@@ -450,6 +451,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.cells_from_cam = 0;
     a.small_rings = (dev->flags & RT_DEVICE_DEBUG_SMALL_RINGS) ? 1 : 0;
     a.fin = dev->fin;
+    a.finpool = dev->finpool;
     a.aocc = dev->aocc;
     a.ao_samples = s->ao;
     a.aa = s->aa;
@@ -483,8 +485,8 @@ int check_texture(Shader* s)
 // Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded colour (16 B; 12 B used
 // with one sample per pixel), the shading inputs of a long shadow ray (48 B; 32 B used without
 // fog), an AO occlusion count (1 B) and a hit bit (the 64-lane ballot per 8x8 unit and AA sample).
-// Per block (one per CU): k_trace's hit queue (hit records of up to 48 B) and long-ray spill ring
-// (48 B records), rt_spill_caps records each.
+// Per block (one per CU): k_trace's hit stack (hit records of up to 48 B) and long-ray spill ring
+// (48 B records), rt_spill_caps records each, and its fin pool (RT_FIN_SLOTS records of up to 48 B).
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
     uint32_t hcap, lcap;
@@ -494,11 +496,14 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         HIP_TRY(hipStreamSynchronize(dev->stream));
         if (dev->hitq) HIP_TRY(hipFree(dev->hitq));
         if (dev->spill_long) HIP_TRY(hipFree(dev->spill_long));
+        if (dev->finpool) HIP_TRY(hipFree(dev->finpool));
         dev->hitq = nullptr;
         dev->spill_long = nullptr;
+        dev->finpool = nullptr;
         dev->hitq_n = dev->spill_long_n = 0;
         HIP_TRY(hipMalloc(&dev->hitq, hq_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
+        HIP_TRY(hipMalloc(&dev->finpool, (size_t)dev->num_cus * RT_FIN_SLOTS * 3 * sizeof(float4)));
         dev->hitq_n = hq_need;
         dev->spill_long_n = ls_need;
     }
@@ -598,7 +603,7 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)hitq, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
+                    (void*)hitq, (void*)finpool, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
@@ -1127,7 +1132,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.hitq,
                           (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_cap, (uint64_t)a.long_spill_cap,
-                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)(uintptr_t)a.fin,
+                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));

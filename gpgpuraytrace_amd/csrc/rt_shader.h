@@ -822,6 +822,13 @@ __device__ __forceinline__ SkyColor get_rayleigh_mie(const Ctx& c, f3 org)
 // getColor up to (not including) the shadow march: albedo, brightness and the
 // shadow-ray step modifier.  Media/nomadplains/shaders/color.hlsl:8-50,
 // testing/color.hlsl:12-22, simple/color.hlsl:8-52, greenrocks/color.hlsl:12-22.
+// color.hlsl:47-49: the shadow ray's stepmod from the hit distance (mip level)
+__device__ __forceinline__ float shade_precision(float dist)
+{
+    float mipf = rtm::max(0.5f * rtm::log2_nonneg(dist), 0.0f);
+    return rtm::max((mipf - 3.2f) * 3.0f, 1.0f) * 8.0f;
+}
+
 struct ShadePre {
     float col[3];   // albedo rgb (color.a handled via spec_k)
     float spec_k;   // color.a
@@ -878,8 +885,7 @@ __device__ __forceinline__ ShadePre shade_pre(const Ctx& c, f3 p, f3 n, f3 d, fl
         r.spec_dot = rtm::dot(rtm::mk(-d.x, -d.y, -d.z), n);
     }
     r.brightness = rtm::dot(n, c.sun);
-    float mipf = rtm::max(0.5f * rtm::log2_nonneg(dist), 0.0f);
-    r.precision = rtm::max((mipf - 3.2f) * 3.0f, 1.0f) * 8.0f;
+    r.precision = shade_precision(dist);
     return r;
 }
 

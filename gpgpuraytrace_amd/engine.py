@@ -158,8 +158,9 @@ class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
     def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False):
-        """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS rings hold 64 entries,
-        so queued work takes the per-block spill rings; same bits)."""
+        """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
+        entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
+        shadows the fin[t] fallback; same bits)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
                       | (_native.RT_DEVICE_GRAPH if graph else 0)

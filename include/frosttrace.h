@@ -55,9 +55,10 @@ enum {
  * No reference counterpart (the D3D frame loop re-records its dispatches every frame).
  * RT_DEVICE_SEG_TAIL_OFF / _ON: reserved (ABI <= 3 selected a trace-kernel tail variant that
  * ABI 4 removed; both are accepted and have no effect).  Setting both fails with RT_ERR_INVALID.
- * RT_DEVICE_DEBUG_SMALL_RINGS (ABI 4, diagnostic): the trace kernel's per-CU LDS work rings hold 64
- * entries instead of 512 / 528, so most queued work takes the per-block spill rings in HBM (the
- * parity tests run frames through that path); same bits, slower. */
+ * RT_DEVICE_DEBUG_SMALL_RINGS (ABI 4, diagnostic): the trace kernel's per-CU LDS long-ray ring holds
+ * 64 entries instead of 570 and its fin pool 8 slots instead of 1536, so queued long rays take the
+ * per-block spill rings in HBM and most long shadows the fin[t] fallback (the parity tests run
+ * frames through those paths); same bits, slower. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };

@@ -173,8 +173,9 @@ def test_density_bitexact(land):
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_frame_bitexact_device_path(spec, kernels):
     """stats: the instrumented kernels (their counts equal the oracle's too); product: the
-    uninstrumented kernels the bench times; spill: the product kernels with 64-entry LDS rings
-    (RT_DEVICE_DEBUG_SMALL_RINGS), so queued hits and long rays go through the per-block spill rings."""
+    uninstrumented kernels the bench times; spill: the product kernels with a 64-entry LDS long ring
+    and an 8-slot fin pool (RT_DEVICE_DEBUG_SMALL_RINGS), so queued long rays go through the
+    per-block spill rings and long shadows through the fin[t] fallback."""
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
