@@ -16,7 +16,8 @@ Frames are rendered in BATCHES (rt_terrain_render_batch: one launch sequence tra
 with D batches in flight (engine.FrameRing).  Exactly --steps frames are timed: the steps are
 split into ceil(steps / B) batches of near-equal size.  Every frame is computed in full and
 independently; value / ms_per_step are the steady-state frame rate; config.frame_latency_ms is
-one batch at a time, config.single_frame one frame at a time (B = 1), and (C3) config.
+one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
+in flight, config.single_frame_serial one frame at a time with no overlap, and (C3) config.
 ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
@@ -497,7 +498,7 @@ def main():
     ring.set_profiling(False)
     k_avg_ms = kms / max(1, kn)  # one launch = a batch of B frames
 
-    # --- companions (N=1): one frame at a time (B = 1) on slot 0 ---
+    # --- companions (N=1): frames rendered one per launch sequence (B = 1) ---
     companions = {}
     if world == 1 and not a.no_companions:
         d0, ter0 = group0[0]
@@ -507,12 +508,34 @@ def main():
             ter0.render_device()
             d0.present()
         d0.synchronize()
+        dt_serial = time.perf_counter() - ts
+    ring.destroy()
+    if world == 1 and not a.no_companions:
+        # B = 1 with three frames in flight (D3D11's default maximum frame latency, the reference
+        # frame loop's own queue depth): each frame is its own prepass -> k_order -> k_trace ->
+        # k_finish on its slot's stream, and the next frame's prepass overlaps this one's tail
+        sring = E.FrameRing(W, H, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
+                            max_steps=a.max_steps, ao_samples=a.ao, batch=1)
+        for _ in range(sring.depth + 1):
+            sring.render_batch()
+        sring.synchronize()
+        ts = time.perf_counter()
+        for _ in range(a.steps):
+            sring.render_batch()
+        sring.synchronize()
         dt = time.perf_counter() - ts
+        sring.destroy()
+        ps = W * H + hits + 1024  # primary + shadow (+ prepass), as config.primary_plus_shadow_mrays
         companions["single_frame"] = {
             "value": round(rays_per_frame * a.steps / dt / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt / a.steps * 1e3, 4),
-            "how": f"rt_terrain_render, one frame at a time on one stream (B=1), {a.steps} frames"}
-    ring.destroy()
+            "primary_plus_shadow_mrays": round(ps * a.steps / dt / 1e6, 3),
+            "how": f"B=1 (one frame per launch sequence), 3 frames in flight on 3 streams, {a.steps} frames"}
+        companions["single_frame_serial"] = {
+            "value": round(rays_per_frame * a.steps / dt_serial / 1e6, 3), "unit": "Mray/s",
+            "ms_per_frame": round(dt_serial / a.steps * 1e3, 4),
+            "primary_plus_shadow_mrays": round(ps * a.steps / dt_serial / 1e6, 3),
+            "how": f"rt_terrain_render, one frame at a time on one stream (B=1, no overlap), {a.steps} frames"}
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)
