@@ -7,15 +7,19 @@ cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 ROUND=${ROUND:-r03}
 # STEPS/WARMUP: the bench command profiled (STEPS=20 WARMUP=5: the driver's, two 10-frame launches);
-# PMC=0 skips the counter passes (kernel trace only)
+# PMC=0 skips the counter passes (kernel trace only), PMC=only skips the kernel trace
 STEPS=${STEPS:-24}; WARMUP=${WARMUP:-2}; PMC=${PMC:-1}
 O=gpurun_out/prof_$ROUND${TAG:+_$TAG}; rm -rf $O; mkdir -p $O
 BENCH="bench.py --steps $STEPS --warmup $WARMUP --no-cpu-baseline --traffic off --no-companions"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $BENCH > $O/kt_bench.json 2> $O/kt.log || exit 1
-echo "kernel trace ok"
+if [ "$PMC" != "only" ]; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o run -- python3 $BENCH > $O/kt_bench.json 2> $O/kt.log || exit 1
+  echo "kernel trace ok"
+fi
 [ "$PMC" = "0" ] && exit 0
+# PMC passes: every tracescreen launch of the run is one 10-frame batch (the driver's), one in
+# flight, so the per-kernel means are per 10-frame launch
 pmc() { local n=$1; shift
-  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $O/$n -o run -- python3 bench.py --steps 12 --warmup 1 --no-cpu-baseline --traffic off --no-companions --frames-in-flight 1 > $O/$n.log 2>&1; local rc=$?; echo "pmc $n rc=$rc"; return $rc; }
+  timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $O/$n -o run -- python3 bench.py --steps 10 --warmup 10 --batch 10 --no-cpu-baseline --traffic off --no-companions --frames-in-flight 1 > $O/$n.log 2>&1; local rc=$?; echo "pmc $n rc=$rc"; return $rc; }
 pmc fetch FETCH_SIZE && pmc write WRITE_SIZE && pmc ea TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum && \
 pmc sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE && \
 pmc sq2 SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS

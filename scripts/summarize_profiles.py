@@ -47,7 +47,9 @@ def main(src, dst):
     shutil.copy(ks[0], os.path.join(dst, "kernel_stats.csv"))
     bench = open(os.path.join(src, "kt_bench.json")).read().strip().splitlines()[-1]
     with open(os.path.join(dst, "kernels.md"), "w") as f:
-        f.write("# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps 24 --warmup 2 --no-cpu-baseline --no-companions`\n\n"
+        bj = json.loads(bench)
+        f.write(f"# rocprofv3 --kernel-trace --stats: `python3 bench.py --steps {bj['steps']} --warmup {bj['warmup']} "
+                "--no-cpu-baseline --traffic off --no-companions`\n\n"
                 "All launches of the run.  The timed loop keeps several batches of frames in flight, so those\n"
                 "launches share the GPU and each one spans longer than it would alone; the per-launch cost the\n"
                 "roofline uses is the bench's one-batch-in-flight pass, tabulated at the end from the same trace.\n"
@@ -92,8 +94,8 @@ def main(src, dst):
     m = pmc_means(src)
     with open(os.path.join(dst, "pmc.md"), "w") as f:
         f.write("# rocprofv3 --pmc per-kernel means (one pass per counter group, "
-                "`bench.py --frames-in-flight 1`: the counters are chip-wide, so no batch may overlap; "
-                "one launch = one batch of frames)\n\n")
+                "`bench.py --steps 10 --warmup 10 --batch 10 --frames-in-flight 1`: the counters are chip-wide, so no "
+                "batch may overlap; every tracescreen launch is one 10-frame batch)\n\n")
         for k in sorted(m):
             f.write(f"## {k}\n\n")
             for c in sorted(m[k]):
