@@ -835,7 +835,7 @@ __device__ unsigned long long g_live_hist[65];
 #endif
 
 #ifdef RT_WAVE_TRACE
-#define RT_WT_FIELDS 18
+#define RT_WT_FIELDS 21
 #define RT_WT_MAX_WAVES 8192
 __device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
 #define WT(...) __VA_ARGS__
@@ -1177,7 +1177,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         const uint32_t hp = queued_hits();
         const bool drained = vload(q.drained) != 0u;
         WT(const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); wt[12]++;
-           wt[15] = t0;)
+           wt[15] = t0; if (drained && wt[18] == 0) { wt[18] = t0; wt[19] = lp; wt[20] = hp; })
         if (lp >= long_batch || (drained && lp > 0u)) {
             do_shadow();
             WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)

@@ -17,7 +17,7 @@ import with_variant  # noqa: E402
 
 with_variant.apply()
 
-F = 18
+F = 21
 
 
 def main():
@@ -56,6 +56,7 @@ def main():
     buf = np.zeros(nw * F, np.uint64)
     assert L.rt_debug_wave_trace(buf.ctypes.data, nw) == F
     t = buf.reshape(nw, F).astype(np.int64)
+    slot = np.nonzero(t[:, 0] > 0)[0]
     t = t[t[:, 0] > 0]
     t0 = t[:, 0].min()
     us = lambda x: x * 0.01  # 100 MHz realtime clock -> us
@@ -96,6 +97,31 @@ def main():
     print(f"wave-slot time after the wave left = {(span - end).sum() / (len(end) * span):.2%} of the launch")
     # longest single activity
     print(f"longest single unit (wave total/units, max): {(tot(2) / np.maximum(t[:, 5], 1)).max():.1f} us")
+    # per block: when the unit queue ran dry for it (first wave to see it), its backlog then
+    # (long rays, hits), and when its last wave left
+    blk = slot // 16
+    rows = []
+    for b in np.unique(blk):
+        m = blk == b
+        dr = t[m, 18]
+        seen = dr > 0
+        if not seen.any():
+            continue
+        i0 = np.argmin(np.where(seen, dr, np.iinfo(np.int64).max))
+        rows.append((us(dr[i0] - t0), t[m, 19][i0], t[m, 20][i0], end[m].max()))
+    if rows:
+        r = np.array(rows, float)
+        print(f"blocks: drain seen p50 {np.percentile(r[:, 0], 50):.1f} us (p10 {np.percentile(r[:, 0], 10):.1f}, "
+              f"p90 {np.percentile(r[:, 0], 90):.1f}); block end p50 {np.percentile(r[:, 3], 50):.1f}, max "
+              f"{r[:, 3].max():.1f} us")
+        print(f"  backlog at drain: long rays p50 {np.percentile(r[:, 1], 50):.0f} p90 {np.percentile(r[:, 1], 90):.0f} "
+              f"max {r[:, 1].max():.0f}; hits p50 {np.percentile(r[:, 2], 50):.0f} max {r[:, 2].max():.0f}")
+        late = np.argsort(-r[:, 3])[:8]
+        print("  last blocks: end  drain-seen  long-backlog  hit-backlog")
+        for i in late:
+            print(f"    {r[i, 3]:8.1f}  {r[i, 0]:8.1f}  {r[i, 1]:6.0f}  {r[i, 2]:6.0f}")
+        c = np.corrcoef(r[:, 1] + r[:, 2], r[:, 3] - r[:, 0])[0, 1] if len(r) > 2 else 0.0
+        print(f"  corr(backlog, end - drain) = {c:.2f}")
     for d in devs:
         d.destroy()
 
