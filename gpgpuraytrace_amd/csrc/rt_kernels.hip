@@ -780,6 +780,20 @@ constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a w
 #define RT_COMPACT_LIVE 56
 #endif
 constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
+// After the unit queue drains (nomadplains): a long-ray wave left with at most kSegHandBack live rays
+// and an empty ring hands them back, and a wave that finds at most kSegQueue rays queued marches them
+// as segments of kSegLanes lanes per ray (density_nomadplains_seg: the octaves spread over the
+// segment), cutting the per-step latency that sets a launch's last few hundred microseconds.
+#ifndef RT_SEG_LANES // A/B: make variant FLAGS=-DRT_SEG_LANES=n (0: off)
+#define RT_SEG_LANES 8
+#endif
+#ifndef RT_SEG_HANDBACK
+#define RT_SEG_HANDBACK 16
+#endif
+#ifndef RT_SEG_QUEUE
+#define RT_SEG_QUEUE 64
+#endif
+constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSegQueue = RT_SEG_QUEUE;
 
 // STATS kernels: a k_trace block's march-step and hit counters (LDS atomics; the block's last wave
 // adds them to the frame statistics)
@@ -1000,8 +1014,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
-            const bool hand_back = lv != 0ull && (uint32_t)__popcll(lv) < compact_live && queued_long() == 0u &&
-                                   vload(q.drained) == 0u;
+            const bool drained_now = vload(q.drained) != 0u;
+            bool hand_back = lv != 0ull && (uint32_t)__popcll(lv) < compact_live && queued_long() == 0u && !drained_now;
+            if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) // after the drain: few rays go to segment waves
+                hand_back = hand_back || (drained_now && lv != 0ull && (uint32_t)__popcll(lv) <= kSegHandBack &&
+                                          queued_long() == 0u);
             if (lv == 0ull || hand_back) {
                 if (__ballot(!live && aux < kFinSlots)) {
                     q_lock(&q.lock, lane);
@@ -1021,6 +1038,85 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             }
 #endif
             if (live) march_step<L, true, true>(cl, st);
+        }
+    };
+
+    // ---- after the drain: up to 64 / kSegLanes queued long rays, a segment of lanes per ray ----
+    auto do_shadow_seg = [&]() {
+        if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
+            constexpr uint32_t LPR = kSegLanes, RPW = 64u / kSegLanes;
+            // late(): the segment's lane values (and the octave scales derived from them) are formed
+            // here, not hoisted into the kernel's prologue where they would stay live throughout
+            const uint32_t lid = late(lane);
+            const uint32_t j = lid & (LPR - 1u), grp = lid / LPR, base = lid & ~(LPR - 1u);
+            March<L, true> st;
+            st.d = 0.0f;
+            st.iters = 0;
+            uint32_t t = 0, aux = kAuxAO;
+            bool live = false;
+            Ctx cl = c;
+            cl.nz.phase = RT_PHASE_LONG;
+            q_lock(&q.lock, lane);
+            const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
+            const uint32_t take = (tail - head) < RPW ? (tail - head) : RPW;
+            const uint32_t sh = vload(q.ls_head), sl = vload(q.ls_tail);
+            const uint32_t more = (sl - sh) < RPW - take ? (sl - sh) : RPW - take;
+            if (grp < take + more) { // every lane of the segment unpacks the same record
+                float4 r0, r1, r2;
+                if (grp < take) {
+                    const float4* r = &q.longs[((head + grp) % kLongRing) * kShadowRec];
+                    r0 = r[0];
+                    r1 = r[1];
+                    r2 = r[2];
+                } else {
+                    const float4* r = lspill + (size_t)((sh + grp - take) % long_spill_cap) * kShadowRec;
+                    r0 = ld_fresh(r);
+                    r1 = ld_fresh(r + 1);
+                    r2 = ld_fresh(r + 2);
+                }
+                t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
+                const float* fr = s_fr.v[frame_of(m, t)];
+                cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
+                if (aux != kAuxAO) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                live = true;
+            }
+            __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
+            if (lane == 0) {
+                q.l_head = head + take;
+                q.ls_head = sh + more;
+            }
+            q_unlock(&q.lock, lane);
+            const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
+            for (;;) {
+                if (live && !march_live<L, true, true>(cl, st, aux == kAuxAO ? RT_AO_END : 100.0f, 0)) {
+                    if (j == 0u) {
+                        long_finish<L>(k, fin, finp, samples, aocc, t, aux, st);
+                        stat(aux == kAuxAO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                    }
+                    live = false;
+                }
+                if (!__ballot(live)) break;
+                if (live) {
+                    auto dens = [&](f3 q0) {
+                        uint32_t used;
+                        const float d = density_nomadplains_seg<LPR>(cl, g, q0, j, base, &used);
+                        if constexpr (STATS) { // the same noise count as density_nomadplains: octaves + steep noise
+                            if (j == 0u) atomicAdd(&s_st.v[BlockStats::NOISE], (unsigned long long)(used + 1u));
+                            if (lane == (uint32_t)__builtin_ctzll(__ballot(1)))
+                                atomicAdd(&s_st.v[BlockStats::NOISE_WAVES], (unsigned long long)SegOctaves<LPR>::R);
+                        }
+                        return d;
+                    };
+                    march_step_with<L, true, true, decltype(dens), true>(cl, st, dens);
+                }
+            }
+            // the segments' finished shadows return their fin pool slots (one lane per segment holds it)
+            uint32_t fa = j == 0u ? aux : kAuxAO;
+            if (__ballot(fa < kFinSlots)) {
+                q_lock(&q.lock, lane);
+                free_fin_locked(false, fa);
+                q_unlock(&q.lock, lane);
+            }
         }
     };
 
@@ -1179,6 +1275,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         WT(const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); wt[12]++;
            wt[15] = t0; if (drained && wt[18] == 0) { wt[18] = t0; wt[19] = lp; wt[20] = hp; })
         if (lp >= long_batch || (drained && lp > 0u)) {
+            if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
+                if (drained && lp <= kSegQueue) {
+                    do_shadow_seg();
+                    WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
+                    continue;
+                }
+            }
             do_shadow();
             WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
             continue;
