@@ -444,9 +444,9 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
 // (color.hlsl:51).  About 70% of shadow rays end there (the surface faces away from
 // the low sun, or the first sample is already inside the terrain) and those samples
 // are finished on the spot; the rest become long shadow rays (2..~120 steps).
-// A long ray's finishing inputs go to fin[t] (3 float4: albedo+specular rgb and
-// brightness, fcolord, rayleigh rgb and skyAmount) and its march state to a
-// 3-float4 record (long_pack).
+// A long ray's finishing inputs (albedo+specular rgb and brightness, fcolord with fog live,
+// rayleigh rgb and skyAmount) go to a slot of its block's fin pool (fin_store), its march state to
+// a 3-float4 record (long_pack).
 constexpr uint32_t kShadowRec = 3;
 
 // Lanes idle before a long-ray wave refills them: amortises the refill's divergent
