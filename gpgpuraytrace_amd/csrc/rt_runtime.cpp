@@ -1197,7 +1197,8 @@ struct Batch {
 
 // Check the n (camerarays, tracescreen) pairs, upload their constants, build the frame table
 // and order the other frames' device streams before the batch.
-int batch_begin(const rt_compute* cams, const rt_compute* scrs, int n, Batch& b)
+int batch_begin(const rt_compute* cams, const rt_compute* scrs, int n, Batch& b, bool sync_cam = true,
+                bool sync_scr = true)
 {
     if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
     int rc;
@@ -1220,7 +1221,10 @@ int batch_begin(const rt_compute* cams, const rt_compute* scrs, int n, Batch& b)
                    !same_tables(cam->shader, b.s0)) {
             return fail(RT_ERR_INVALID, "frame %d: a batch needs one GPU, resolution, landscape, macro set and noise", f);
         }
-        if ((rc = sync_shader(d, cam->shader)) || (rc = sync_shader(d, scr->shader))) return rc;
+        // a prepass-only call uploads the camerarays constants only: the tracescreen block may still be
+        // read by this device's previous trace, which another stream can be running
+        if ((sync_cam && (rc = sync_shader(d, cam->shader))) || (sync_scr && (rc = sync_shader(d, scr->shader))))
+            return rc;
         rt_array_s* cr = cam->shader->array("CameraResults");
         rt_array_s* cd = scr->shader->array("CellDistance");
         if (!cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
@@ -1274,7 +1278,7 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
     int rc;
     Batch b;
-    if ((rc = batch_begin(cams, scrs, n, b))) return rc;
+    if ((rc = batch_begin(cams, scrs, n, b, (phases & PH_PRE) != 0, (phases & PH_TRACE) != 0))) return rc;
     rt_device dev = b.dev;
     FrameTable& ft = b.ft;
     if (count < 0) count = n;

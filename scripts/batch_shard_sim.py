@@ -40,6 +40,9 @@ def main():
                          "all-gather is not simulated: the other frames' CameraResults come from a full prepass "
                          "run once before timing)")
     ap.add_argument("--barrier-model", action="store_true")
+    ap.add_argument("--lookahead", type=int, default=0,
+                    help="1: issue batch b+1's prepass (split API, rotating CameraResults buffers) before batch b's "
+                         "trace on the groups' streams; 2: the same on a dedicated prepass stream")
     ap.add_argument("--gather-us", type=float, default=40.0,
                     help="modelled all-gather latency per batch (16 KiB per frame over xGMI)")
     a = ap.parse_args()
@@ -60,7 +63,50 @@ def main():
             G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
         torch.cuda.synchronize()
 
+        look = {"next": None, "bufs": [torch.zeros(B * 1024 * 4, dtype=torch.float32, device="cuda:0") for _ in range(a.depth + 2)],
+                "k": 0, "pre_stream": torch.cuda.Stream(device="cuda:0"), "ev": {}}
+
+        def issue_prepass(k, r, n):
+            """prepass of batch index k (its slot group), into rotating buffer k % (depth + 2): a buffer is
+            rewritten only after the trace that read it (batch k - depth - 2, same group) is done"""
+            g = k % a.depth
+            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
+            devs = [d for d, _ in ring.slots[g * B:(g + 1) * B]]
+            buf = look["bufs"][k % len(look["bufs"])]
+            if a.lookahead == 2:
+                ps = look["pre_stream"]
+                for d in devs:
+                    d.set_stream(ps.cuda_stream)
+                G.engine.prepass_batch(ters, 0, B, buf.data_ptr())
+                ev = torch.cuda.Event()
+                ev.record(ps)
+                look["ev"][k] = ev
+                first = devs[0]
+                for d in devs:
+                    d.set_stream(None if d is first else first.stream())
+            else:
+                G.engine.prepass_batch(ters, 0, B, buf.data_ptr())
+
+        def step_look(r, n):
+            k = look["k"]
+            g = k % a.depth
+            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
+            devs = [d for d, _ in ring.slots[g * B:(g + 1) * B]]
+            if look["next"] != k:
+                issue_prepass(k, r, n)
+            issue_prepass(k + 1, r, n)
+            look["next"] = k + 1
+            if a.lookahead == 2:
+                gs = torch.cuda.ExternalStream(devs[0].stream(), device="cuda:0")
+                gs.wait_event(look["ev"].pop(k))
+            G.engine.trace_batch(ters, r, n, look["bufs"][k % len(look["bufs"])].data_ptr())
+            look["k"] = k + 1
+            ring.frame += B
+
         def step(r, n):
+            if a.lookahead:
+                step_look(r, n)
+                return
             if not a.split_prepass or n == 1:
                 ring.render_batch(r, n, present=False)
                 return
