@@ -22,8 +22,11 @@ ref_semantics the same machinery at the reference's own semantics (uncapped, no 
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
 scaling: the frame is fixed); parallel.BatchPlan / run_batch hold the per-batch sequence
-(every rank's prepass of the batch, or with --split-prepass 1 a B/N share + CameraResults
-all-gather; shard rotation, pack, one RCCL gather to rank 0, unpack), which tests/test_dist.py drives with host ops over gloo.
+(every rank's prepass of the batch -- with --lookahead 1 queued one batch ahead on a side stream
+-- or with --split-prepass 1 a B/N share + CameraResults all-gather; shard rotation, pack, one
+RCCL gather to rank 0, unpack), which tests/test_dist.py drives with host ops over gloo.  With
+lookahead the timed region holds exactly the prepasses of its own batches: the last warm-up
+batch and the last timed batch queue no ahead prepass.
 
 Prints ONE JSON line on rank 0 (driver contract), with "roofline" for the dominant
 kernel (tracescreen, timed by HIP events on its own stream in a pass with one batch in
@@ -38,6 +41,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# One hardware queue per busy stream, set before HIP starts: the frame ring's
+# slot-group streams, the ahead-prepass side stream, torch's and RCCL's.  With HIP's default of 4,
+# two busy streams share a queue and the batches the ring overlaps run one after the other
+# (profiles/r03/hw_queues.md: one-rank shard simulation at N=8, one extra stream alive,
+# 0.397 -> 0.430 ms/frame; 8 queues: 0.398).
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
@@ -83,6 +92,11 @@ def parse():
                          "north_star's single gather) = every rank runs every frame's prepass.  The barrier model "
                          "(scripts/batch_shard_sim.py --barrier-model, profiles/r03/batch_shard_barrier.log) puts "
                          "the split's gain at <= 2%% (N=8)")
+    ap.add_argument("--lookahead", type=int, default=0,
+                    help="1 = the timed loop queues the next batch's prepass on the GPU's side stream before this "
+                         "batch's trace (rt_terrain_prepass_ahead, DESIGN.md section 7); 0 (default) = each batch's "
+                         "prepass in line on its slot group's stream (measured 0.6%% faster at B=12: "
+                         "profiles/r03/hw_queues.md).  config.single_frame always runs it (B=1: +1.3%%)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
@@ -106,6 +120,8 @@ def parse():
             setattr(a, key, preset[key])
     if a.graph is None:
         a.graph = 1 if a.config == "c5" else 0
+    if a.lookahead and a.graph:
+        ap.error("--lookahead runs the prepass on a side stream: not with --graph 1")
     if a.cpu_row_step is None:
         a.cpu_row_step = preset["cpu_rows"]
     if a.steps < 1:
@@ -353,7 +369,7 @@ def main():
     camera = G.Camera(W, H, euler=euler)
     ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
-    plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass)
+    plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass, lookahead=a.lookahead)
     coll = P.Collectives(dist, backend, rank, world)
     dev_str = f"cuda:{local}"
     # a batch's devices share its stream (FrameRing): every op of a batch rides on it
@@ -392,6 +408,20 @@ def main():
         def render(self):
             E.render_batch(self.ters, rank if world > 1 else 0, world)
 
+        def prepass_ahead(self):
+            if self.g not in ahead:
+                E.prepass_ahead(self.ters)
+            ahead.discard(self.g)
+
+        def prepass_ahead_next(self):
+            nxt = (self.g + 1) % ring.depth
+            if nxt != self.g:
+                E.prepass_ahead([t for _, t in ring.slots[nxt * B:(nxt + 1) * B]])
+                ahead.add(nxt)
+
+        def trace_ahead(self):
+            E.trace_ahead(self.ters, rank if world > 1 else 0, world)
+
         def pack_batch(self, items):
             base = self.b["packed"].data_ptr()
             E.shard_pack_batch([self.devs[f] for f, _, _ in items], [s for _, s, _ in items], world,
@@ -411,8 +441,9 @@ def main():
                 d.present()
 
     timed_marks, timed_t0 = [], []  # per timed batch: run_batch's phase marks (HIP events) and its stream's t0
+    ahead = set()  # slot groups whose prepass is queued ahead (plan.lookahead)
 
-    def batch_step(n, timed=False):
+    def batch_step(n, timed=False, ahead_next=True):
         ops = DeviceOps(n)
         mark = None
         if timed:
@@ -424,12 +455,13 @@ def main():
                 marks.append((name, ev))
             timed_marks.append(marks)
             timed_t0.append(t0_events[ops.g])
-        P.run_batch(plan, rank, ops, frames=n, mark=mark)
+        P.run_batch(plan, rank, ops, frames=n, mark=mark, ahead_next=ahead_next)
         ring.frame += B
 
     progress(rank, "warmup")
-    for _ in range(-(-a.warmup // B) + ring.depth):
-        batch_step(B)
+    n_warm = -(-a.warmup // B) + ring.depth
+    for i in range(n_warm):
+        batch_step(B, ahead_next=i + 1 < n_warm)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -442,8 +474,8 @@ def main():
         ev.record(bufs[g]["stream"])
         t0_events.append(ev)
     t0 = time.perf_counter()
-    for n in sizes:
-        batch_step(n, timed=True)
+    for i, n in enumerate(sizes):
+        batch_step(n, timed=True, ahead_next=i + 1 < len(sizes))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -515,13 +547,13 @@ def main():
         # frame loop's own queue depth): each frame is its own prepass -> k_order -> k_trace ->
         # k_finish on its slot's stream, and the next frame's prepass overlaps this one's tail
         sring = E.FrameRing(W, H, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
-                            max_steps=a.max_steps, ao_samples=a.ao, batch=1)
-        for _ in range(sring.depth + 1):
-            sring.render_batch()
+                            max_steps=a.max_steps, ao_samples=a.ao, batch=1, lookahead=True)
+        for i in range(sring.depth + 1):
+            sring.render_batch(ahead=i < sring.depth)
         sring.synchronize()
         ts = time.perf_counter()
-        for _ in range(a.steps):
-            sring.render_batch()
+        for i in range(a.steps):
+            sring.render_batch(ahead=i + 1 < a.steps)
         sring.synchronize()
         dt = time.perf_counter() - ts
         sring.destroy()
@@ -530,7 +562,8 @@ def main():
             "value": round(rays_per_frame * a.steps / dt / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt / a.steps * 1e3, 4),
             "primary_plus_shadow_mrays": round(ps * a.steps / dt / 1e6, 3),
-            "how": f"B=1 (one frame per launch sequence), 3 frames in flight on 3 streams, {a.steps} frames"}
+            "how": f"B=1 (one frame per launch sequence), 3 frames in flight on 3 streams, each frame's "
+                   f"prepass queued one frame ahead on the side stream (rt_terrain_prepass_ahead), {a.steps} frames"}
         companions["single_frame_serial"] = {
             "value": round(rays_per_frame * a.steps / dt_serial / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt_serial / a.steps * 1e3, 4),
@@ -540,13 +573,13 @@ def main():
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)
         rring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
-                            time_of_day=0.3, max_steps=0, ao_samples=0, batch=B)
-        for _ in range(rring.depth + 1):
-            rring.render_batch()
+                            time_of_day=0.3, max_steps=0, ao_samples=0, batch=B, lookahead=bool(a.lookahead))
+        for i in range(rring.depth + 1):
+            rring.render_batch(ahead=i < rring.depth)
         rring.synchronize()
         ts = time.perf_counter()
-        for n in sizes:
-            rring.render_batch(frames=n)
+        for i, n in enumerate(sizes):
+            rring.render_batch(frames=n, ahead=i + 1 < len(sizes))
         rring.synchronize()
         dt = time.perf_counter() - ts
         rring.destroy()
@@ -606,7 +639,8 @@ def main():
                        else "")),
                 "batch": B, "batches": sizes, "batches_in_flight": a.frames_in_flight,
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
-                              else "direct launches",
+                              else "direct launches" + (", each batch's prepass queued one batch ahead on the GPU's "
+                                                        "side stream (rt_terrain_prepass_ahead)" if plan.lookahead else ""),
                 "frame_latency_ms": round(latency_ms, 4),  # one batch of B frames at a time
                 # per rank: mean / max ms per timed batch of each run_batch phase on the batch's stream
                 # (prepass, all_gather, trace, pack, gather, unpack; waits for the other batch in flight

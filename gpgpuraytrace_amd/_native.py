@@ -20,7 +20,7 @@ RT_DEVICE_GRAPH = 4
 RT_DEVICE_SEG_TAIL_OFF = 8  # reserved since ABI 4 (no effect)
 RT_DEVICE_SEG_TAIL_ON = 16  # reserved since ABI 4 (no effect)
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
-ABI_VERSION = 4  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
+ABI_VERSION = 5  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -89,6 +89,8 @@ SIGNATURES = {
     "rt_terrain_render_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i]),
     "rt_terrain_prepass_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
     "rt_terrain_trace_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
+    "rt_terrain_prepass_ahead": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i]),
+    "rt_terrain_trace_ahead": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i]),
     "rt_terrain_feed_wait": (_i, [_vp, _vp]),
     "rt_shard_bytes": (_sz, [_vp, _i, _i]),
     "rt_shard_pack": (_i, [_vp, _i, _i, _vp]),

@@ -51,6 +51,7 @@ struct RtLaunch {
     const FrameTable* frames; // device table of the batch's frames
     FrameTable frames_host;   // the same pointers on the host
     uint32_t n_frames;        // frames in the batch (1..RT_MAX_BATCH)
+    hipEvent_t after_order;   // recorded after k_order when set (its read of CameraResults is done)
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);

@@ -1533,6 +1533,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.cells_from_cam = (uint32_t)a.cells_from_cam;
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue);
+    if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill rings
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;

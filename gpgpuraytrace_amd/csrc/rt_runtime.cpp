@@ -145,6 +145,12 @@ struct rt_device_s {
         Staging staging;
     } table, pre_table;
     hipEvent_t sync_ev = nullptr; // orders this device's stream against a batch on another device
+    // rt_terrain_prepass_ahead, for batches led by this device: ev_order follows its last k_order
+    // (the last read of the frames' CameraResults), ev_ahead the ahead prepass on the GPU's side
+    // stream; ahead_cams are that prepass's frames (a trace of another batch prepasses again)
+    hipEvent_t ev_order = nullptr, ev_ahead = nullptr;
+    bool order_recorded = false, ahead_pending = false;
+    std::vector<const void*> ahead_cams;
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -458,6 +464,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.frames = dev->table.d;
     a.frames_host = FrameTable{};
     a.n_frames = 1;
+    a.after_order = nullptr;
     return a;
 }
 
@@ -591,12 +598,28 @@ void stream_unref(hipStream_t s)
         (void)hipStreamDestroy(s);
     }
 }
+
+// rt_terrain_prepass_ahead's side stream: one per GPU, shared by every batch on it (the ahead
+// prepasses run one after another, like the batches), created on first use and kept for the
+// process (devices come and go; the stream carries no state of theirs past its work)
+std::map<int, hipStream_t> g_ahead_streams;
+
+hipStream_t ahead_stream(int ordinal, bool create)
+{
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto it = g_ahead_streams.find(ordinal);
+    if (it != g_ahead_streams.end()) return it->second;
+    hipStream_t s = nullptr;
+    if (!create || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    return g_ahead_streams[ordinal] = s;
+}
 } // namespace
 
 rt_device_s::~rt_device_s()
 {
     (void)hipSetDevice(ordinal);
     if (stream) (void)hipStreamSynchronize(stream); // the stream in use is alive: a reference is held
+    if (hipStream_t side = ahead_stream(ordinal, false)) (void)hipStreamSynchronize(side); // ahead prepasses
     for (auto* c : computes) delete c;              // children die with their device
     for (auto* t : textures) {
         if (t->data) (void)hipFree(t->data);
@@ -609,7 +632,8 @@ rt_device_s::~rt_device_s()
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
     if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
-    if (sync_ev) (void)hipEventDestroy(sync_ev);
+    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead})
+        if (e) (void)hipEventDestroy(e);
     for (auto& pr : ev_pool) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -1035,7 +1059,9 @@ int rt_variable_write(rt_variable v, const void* data)
     if (!v || !data) return fail(RT_ERR_INVALID, "bad arguments");
     Shader* s = v->owner;
     std::lock_guard<std::mutex> lk(g_cb_mu);
-    memcpy(s->cb[v->cbuf].data() + v->offset, data, v->size);
+    uint8_t* dst = s->cb[v->cbuf].data() + v->offset;
+    if (!memcmp(dst, data, v->size)) return RT_OK; // unchanged: no upload (and an ahead prepass stays current)
+    memcpy(dst, data, v->size);
     if (v->cbuf != CB_DISPATCH) s->cb_dirty = true; // ThreadOffset is a launch argument
     return RT_OK;
 }
@@ -1296,25 +1322,33 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             ft.cam[f] = const_cast<float4*>(src);
         }
     }
+    if (dev->ahead_pending) {
+        // an ahead prepass of this device's batches writes CameraResults: it comes first
+        HIP_TRY(hipStreamWaitEvent(dev->stream, dev->ev_ahead, 0));
+        dev->ahead_pending = false;
+    }
+    if (phases == PH_PRE) {
+        // the prepass of frames [first, first + count) only, on its own table
+        if (count == 0) return batch_end(scrs, n, b);
+        RtLaunch la_cam = make_launch(dev, cams[0]->shader);
+        FrameTable sub{};
+        for (int i = 0; i < count; ++i) {
+            sub.k[i] = ft.k[first + i];
+            sub.kcam[i] = ft.kcam[first + i];
+            sub.cam[i] = camera_out ? camera_out + (size_t)(first + i) * 1024 : ft.cam[first + i];
+        }
+        if ((rc = upload_frames(dev, dev->pre_table, sub))) return rc;
+        la_cam.frames = dev->pre_table.d;
+        la_cam.frames_host = sub;
+        la_cam.n_frames = (uint32_t)count;
+        rt_launch_camerarays_batch(la_cam);
+        return batch_end(scrs, n, b);
+    }
     if ((rc = ensure_split_buffers(dev, b.s0->aa, b.s0->ao, n))) return rc;
     RtLaunch la_cam = make_launch(dev, cams[0]->shader), la_scr = make_launch(dev, scrs[0]->shader);
-    if (phases & PH_PRE) {
-        if (phases == PH_PRE) {
-            // the prepass of frames [first, first + count) only, on its own table
-            if (count == 0) return batch_end(scrs, n, b);
-            FrameTable sub{};
-            for (int i = 0; i < count; ++i) {
-                sub.k[i] = ft.k[first + i];
-                sub.kcam[i] = ft.kcam[first + i];
-                sub.cam[i] = camera_out ? camera_out + (size_t)(first + i) * 1024 : ft.cam[first + i];
-            }
-            if ((rc = upload_frames(dev, dev->pre_table, sub))) return rc;
-            la_cam.frames = dev->pre_table.d;
-            la_cam.frames_host = sub;
-            la_cam.n_frames = (uint32_t)count;
-            rt_launch_camerarays_batch(la_cam);
-            return batch_end(scrs, n, b);
-        }
+    if (!graphs && dev->ev_order) {
+        la_scr.after_order = dev->ev_order; // rt_terrain_prepass_ahead: the frames' CameraResults are read
+        dev->order_recorded = true;
     }
     if ((rc = upload_frames(dev, dev->table, ft))) return rc;
     la_cam.frames = la_scr.frames = dev->table.d;
@@ -1385,6 +1419,65 @@ int rt_terrain_trace_batch(const rt_compute* cams, const rt_compute* scrs, int n
     if (!camera_in) return fail(RT_ERR_INVALID, "camera_in: the batch's gathered CameraResults");
     return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, PH_TRACE, 0, -1, nullptr,
                                 (const float4*)camera_in);
+}
+
+// The prepass one batch ahead: the batch's camerarays prepass on the GPU's
+// side stream, after the last k_order of the batches this device leads (the last read of the
+// CameraResults it overwrites).  Issued before the previous batch's trace, it takes CUs before
+// that trace's persistent k_trace holds them all, and the trace of its own batch
+// (rt_terrain_trace_ahead) starts without a prepass in front of it.
+int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int n)
+{
+    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
+    for (int f = 0; f < n; ++f)
+        if (!cams[f] || !scrs[f] || cams[f]->dev != scrs[f]->dev) return fail(RT_ERR_INVALID, "computes must share a device");
+    rt_device lead = scrs[0]->dev;
+    if (lead->flags & RT_DEVICE_GRAPH) return fail(RT_ERR_STATE, "the ahead prepass runs on a side stream: not with RT_DEVICE_GRAPH");
+    if (lead->ahead_pending) return fail(RT_ERR_STATE, "a prepass is already ahead for this device's batch: trace it first");
+    HIP_TRY(hipSetDevice(lead->ordinal));
+    hipStream_t side = ahead_stream(lead->ordinal, true);
+    if (!side) return fail(RT_ERR_HIP, "side stream");
+    if (!lead->ev_order) HIP_TRY(hipEventCreateWithFlags(&lead->ev_order, hipEventDisableTiming));
+    if (!lead->ev_ahead) HIP_TRY(hipEventCreateWithFlags(&lead->ev_ahead, hipEventDisableTiming));
+    // before the first recorded k_order: after everything queued so far
+    if (!lead->order_recorded) {
+        HIP_TRY(hipEventRecord(lead->ev_order, lead->stream));
+        lead->order_recorded = true;
+    }
+    HIP_TRY(hipStreamWaitEvent(side, lead->ev_order, 0));
+    // the batch's devices upload their constants and launch on the side stream for this call
+    std::vector<std::pair<rt_device, hipStream_t>> saved;
+    for (int f = 0; f < n; ++f) {
+        rt_device d = scrs[f]->dev;
+        bool seen = false;
+        for (auto& p : saved) seen |= p.first == d;
+        if (!seen) {
+            saved.emplace_back(d, d->stream);
+            d->stream = side;
+        }
+    }
+    int rc = terrain_render_batch(cams, scrs, n, 0, 1, false, PH_PRE, 0, n, nullptr);
+    for (auto& p : saved) p.first->stream = p.second;
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(lead->ev_ahead, side));
+    lead->ahead_pending = true;
+    lead->ahead_cams.assign(cams, cams + n);
+    return RT_OK;
+}
+
+// setTargetDepths + tracescreen of a batch whose prepass rt_terrain_prepass_ahead queued; without
+// one (or for other frames, or after a camera constant changed since) the full render_batch
+int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count)
+{
+    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH || !scrs[0]) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
+    rt_device lead = scrs[0]->dev;
+    bool ahead = lead->ahead_pending && (size_t)n <= lead->ahead_cams.size();
+    for (int f = 0; ahead && f < n; ++f)
+        ahead = cams[f] == lead->ahead_cams[f] && cams[f]->shader && !cams[f]->shader->cb_dirty;
+    if (!ahead) return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false); // waits for a pending one
+    HIP_TRY(hipStreamWaitEvent(lead->stream, lead->ev_ahead, 0));
+    lead->ahead_pending = false;
+    return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, PH_TRACE);
 }
 
 size_t rt_shard_bytes(rt_device d, int rank, int count)

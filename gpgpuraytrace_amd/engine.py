@@ -540,6 +540,21 @@ def trace_batch(terrains, shard_rank, shard_count, camera_in_ptr):
     check(lib().rt_terrain_trace_batch(cams, scrs, n, shard_rank, shard_count, camera_in_ptr), "terrain_trace_batch")
 
 
+def prepass_ahead(terrains):
+    """rt_terrain_prepass_ahead (ABI 5): queue the batch's prepass on the GPU's side stream, after
+    the last setTargetDepths of the batches the first terrain's device leads.  Issue it before
+    the previous batch's trace_ahead / render_batch; trace_ahead(terrains) consumes it."""
+    n, cams, scrs = _batch_handles(terrains)
+    check(lib().rt_terrain_prepass_ahead(cams, scrs, n), "terrain_prepass_ahead")
+
+
+def trace_ahead(terrains, shard_rank=0, shard_count=1):
+    """rt_terrain_trace_ahead (ABI 5): setTargetDepths + tracescreen after the batch's ahead
+    prepass (the full render_batch when none covers these frames or a camera changed since)."""
+    n, cams, scrs = _batch_handles(terrains)
+    check(lib().rt_terrain_trace_ahead(cams, scrs, n, shard_rank, shard_count), "terrain_trace_ahead")
+
+
 def _cbuffer_matrix(m):
     """Bytes of XMMatrixTranspose(M) -- what the engine writes for a float4x4 cbuffer variable."""
     return np.ascontiguousarray(np.asarray(m, np.float32).T)
@@ -590,11 +605,18 @@ class FrameRing:
     that slot's stream.  depth=1 is the reference's one-frame-at-a-time behaviour.
     graph=True: each slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH).
     batch=B: a slot is B frames rendered by one rt_terrain_render_batch (B devices, the
-    batch on the first one's stream); render_batch() queues the next B frames."""
+    batch on the first one's stream); render_batch() queues the next B frames.
+    lookahead=True (not with graph): render_batch(ahead=True) also queues the NEXT group's prepass
+    on the GPU's side stream before this batch's trace (rt_terrain_prepass_ahead), so it runs
+    beside this trace instead of in front of the next one; set the next frames' cameras before
+    that call (a camera written after it makes the next batch prepass again, in line)."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 graph=False, batch=1, float_output=False, **terrain_kw):
+                 graph=False, batch=1, float_output=False, lookahead=False, **terrain_kw):
         self.depth, self.frame, self.batch = int(depth), 0, int(batch)
+        if lookahead and graph:
+            raise ValueError("lookahead runs the prepass on a side stream: not with graph=True")
+        self.lookahead, self._ahead = bool(lookahead), set()  # groups with an ahead prepass queued
         self.slots = []
         for _ in range(self.depth * self.batch):
             dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph,
@@ -624,12 +646,25 @@ class FrameRing:
             raise ValueError("frames must be 1..batch")
         return self.slots[g * self.batch:g * self.batch + n]
 
-    def render_batch(self, shard_rank=0, shard_count=1, present=True, frames=None):
+    def render_batch(self, shard_rank=0, shard_count=1, present=True, frames=None, ahead=True):
         """Queue the next `batch` frames (or the first `frames` of them: a partial batch) as one
         batch on the next slot group; returns their Devices in frame order (each complete once
-        its stream reaches this point)."""
+        its stream reaches this point).  With lookahead, ahead=False skips queueing the next
+        group's prepass (the last batch of a run)."""
         group = self.group(frames)
-        render_batch([t for _, t in group], shard_rank, shard_count)
+        terrains = [t for _, t in group]
+        if not self.lookahead:
+            render_batch(terrains, shard_rank, shard_count)
+        else:
+            g = (self.frame // self.batch) % self.depth
+            if g not in self._ahead:
+                prepass_ahead(terrains)
+            self._ahead.discard(g)
+            nxt = (g + 1) % self.depth
+            if ahead and nxt != g:
+                prepass_ahead([t for _, t in self.slots[nxt * self.batch:(nxt + 1) * self.batch]])
+                self._ahead.add(nxt)
+            trace_ahead(terrains, shard_rank, shard_count)
         devs = [d for d, _ in group]
         if present:
             for d in devs:

@@ -11,12 +11,15 @@ shard's tile classes.  BatchPlan holds that bookkeeping and run_batch() is the o
 steps every rank runs per batch; bench.py drives it with device ops (HIP kernels, RCCL) and
 tests/test_dist.py with host ops (numpy, gloo), so the CPU tests exercise the same code:
 
-  1. prepass: split (default): rank r runs the camerarays prepass of frames
-     [r*chunk, (r+1)*chunk) of the batch, chunk = ceil(B/N) (ranks past the last frame run an
-     empty range), and an all-gather hands every rank all B frames' CameraResults (16 KiB per
-     frame).  This is a SECOND collective per batch: SURVEY.md section 8e planned per-rank
-     prepass recompute instead; the split removes an N-fold repeat of latency-bound prepass
-     rays.  Unsplit: every rank runs every frame's prepass.
+  1. prepass: unsplit (default): every rank runs every frame's camerarays prepass (SURVEY.md
+     section 8e's per-rank recompute; 1024 rays a frame).  With lookahead (bench.py
+     --lookahead 1) the NEXT batch's prepass is queued on the GPU's side stream before this
+     batch's trace (rt_terrain_prepass_ahead) instead of in line on its own slot group's
+     stream (DESIGN.md section 7 has the measurements).  Split
+     (split_prepass=True): rank r runs the prepass of frames [r*chunk, (r+1)*chunk), chunk =
+     ceil(B/N) (ranks past the last frame run an empty range), and an all-gather hands every
+     rank all B frames' CameraResults (16 KiB per frame) -- a second collective per batch,
+     which the barrier model of DESIGN.md section 7 found slower than recompute.
   2. trace: each rank traces its shard of every frame (setTargetDepths + tracescreen).
   3. pack: frame f's shard (r + f) % N goes to packed[f * max_bytes : ...] (k_shard_copy;
      1024 RGBA8 pixels per tile, tiles in ascending order), the batch's frames in one launch.
@@ -96,11 +99,13 @@ class BatchPlan:
 
     CAMERA_FLOATS = 1024 * 4  # CameraResults of one frame: float4[1024]
 
-    def __init__(self, width, height, batch, world, split_prepass=False):
+    def __init__(self, width, height, batch, world, split_prepass=False, lookahead=False):
         if not 1 <= batch <= 16:
             raise ValueError("batch must be 1..16 frames (RT_MAX_BATCH)")
         self.width, self.height, self.batch, self.world = int(width), int(height), int(batch), int(world)
         self.split_prepass = bool(split_prepass) and self.world > 1
+        # the ahead prepass is the unsplit one's (the split one is gathered before its trace)
+        self.lookahead = bool(lookahead) and not self.split_prepass
         self.chunk = -(-self.batch // self.world)
         self.max_bytes = max(shard_bytes(self.width, self.height, r, self.world) for r in range(self.world))
 
@@ -137,10 +142,13 @@ class BatchPlan:
         return [(src, f, self.shard(src, f), self.pack_offset(f)) for src in range(1, self.world) for f in range(n)]
 
 
-def run_batch(plan, rank, ops, frames=None, mark=None):
+def run_batch(plan, rank, ops, frames=None, mark=None, ahead_next=True):
     """One batch on this rank.  `ops` supplies the actions (bench.py: HIP + RCCL; tests: numpy
     + gloo): prepass(first, count), all_gather_cameras(), trace(), render() (prepass + trace of
-    every frame, the unsplit path), pack_batch([(f, shard, offset)]) (this rank's frames; one
+    every frame, the unsplit path), with plan.lookahead prepass_ahead() (this batch's prepass on
+    the side stream, unless the previous batch queued it), prepass_ahead_next() (the next
+    batch's, before this trace; skipped with ahead_next=False: the last batch of a run) and
+    trace_ahead(), pack_batch([(f, shard, offset)]) (this rank's frames; one
     rt_shard_pack_batch launch on the GPU), gather(), unpack_batch([(src, f, shard, offset)])
     (rank 0: every other rank's frames in one rt_shard_unpack_batch launch), present().
     `frames` < plan.batch renders a partial batch (its first frames).
@@ -158,6 +166,11 @@ def run_batch(plan, rank, ops, frames=None, mark=None):
         ops.all_gather_cameras()
         mark("all_gather")
         ops.trace()
+    elif plan.lookahead:
+        ops.prepass_ahead()
+        if ahead_next:
+            ops.prepass_ahead_next()
+        ops.trace_ahead()
     else:
         ops.render()
     mark("trace")

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 enum {
     RT_OK = 0,
@@ -219,6 +219,20 @@ int rt_terrain_prepass_batch(const rt_compute* camera_cs, const rt_compute* scre
                              void* camera_out);
 int rt_terrain_trace_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
                            int shard_count, const void* camera_in);
+/* (ABI 5) The prepass one batch ahead, for a stream of batches (FrameRing(lookahead=True),
+ * parallel.run_batch): rt_terrain_prepass_ahead queues the batch's camerarays prepass (into each
+ * frame's CameraResults) on the GPU's side stream -- one per GPU, created on first use -- after
+ * the last setTargetDepths of the batches screen_cs[0]'s device leads (their last read of those
+ * arrays).  Issued before the previous batch's trace, it gets CUs before that trace's persistent
+ * kernel holds them all.  rt_terrain_trace_ahead then runs setTargetDepths + tracescreen of the
+ * batch after that prepass; for frames the pending prepass did not cover (other computes, more
+ * frames, or camera constants written since) it renders the full batch (rt_terrain_render_batch)
+ * instead, so the frames always equal rt_terrain_render_batch's bit for bit.  One ahead prepass
+ * per leading device at a time (RT_ERR_STATE otherwise); not on RT_DEVICE_GRAPH devices.
+ * No reference counterpart (Terrain::render runs its prepass in line, Terrain.cpp:105-136). */
+int rt_terrain_prepass_ahead(const rt_compute* camera_cs, const rt_compute* screen_cs, int n);
+int rt_terrain_trace_ahead(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
+                           int shard_count);
 /* Tile-cyclic shard transport: pack this rank's tiles from the framebuffer into a
  * contiguous device buffer (RGBA8, 32x32-pixel tiles in tile order), or unpack a rank's
  * packed tiles into the framebuffer.  Byte counts from rt_shard_bytes. */

@@ -41,21 +41,32 @@ def main():
                          "run once before timing)")
     ap.add_argument("--barrier-model", action="store_true")
     ap.add_argument("--lookahead", type=int, default=0,
-                    help="1: issue batch b+1's prepass (split API, rotating CameraResults buffers) before batch b's "
-                         "trace on the groups' streams; 2: the same on a dedicated prepass stream")
+                    help="1: FrameRing(lookahead=True), each batch's prepass queued on the GPU's side stream before "
+                         "the previous batch's trace (rt_terrain_prepass_ahead); 0 (bench.py's default): in line")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (bench.py sets 8; 0 = leave the environment's)")
+    ap.add_argument("--extra-streams", type=int, default=0,
+                    help="diagnostic: K torch streams kept busy-free but alive (HW queue sharing study)")
     ap.add_argument("--gather-us", type=float, default=40.0,
                     help="modelled all-gather latency per batch (16 KiB per frame over xGMI)")
     a = ap.parse_args()
+    if a.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)  # before HIP starts (torch below)
     if a.barrier_model:
         return barrier_model(a)
     import torch
     import gpgpuraytrace_amd as G
     W, H = a.width, a.height
+    extra = [torch.cuda.Stream(device="cuda:0") for _ in range(a.extra_streams)]
+    for st in extra:  # each stream runs one op, so it holds its hardware queue
+        with torch.cuda.stream(st):
+            torch.zeros(1, device="cuda:0").add_(1)
+    torch.cuda.synchronize()
     cam = G.Camera(W, H)
     base = None
     for B in [int(x) for x in a.batches.split(",")]:
         ring = G.FrameRing(W, H, depth=a.depth, batch=B, camera=cam, time_of_day=0.3, max_steps=a.max_steps,
-                           ao_samples=a.ao)
+                           ao_samples=a.ao, lookahead=bool(a.lookahead) and not a.split_prepass)
         bufs = []
         for g in range(a.depth):
             ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
@@ -63,50 +74,7 @@ def main():
             G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
         torch.cuda.synchronize()
 
-        look = {"next": None, "bufs": [torch.zeros(B * 1024 * 4, dtype=torch.float32, device="cuda:0") for _ in range(a.depth + 2)],
-                "k": 0, "pre_stream": torch.cuda.Stream(device="cuda:0"), "ev": {}}
-
-        def issue_prepass(k, r, n):
-            """prepass of batch index k (its slot group), into rotating buffer k % (depth + 2): a buffer is
-            rewritten only after the trace that read it (batch k - depth - 2, same group) is done"""
-            g = k % a.depth
-            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
-            devs = [d for d, _ in ring.slots[g * B:(g + 1) * B]]
-            buf = look["bufs"][k % len(look["bufs"])]
-            if a.lookahead == 2:
-                ps = look["pre_stream"]
-                for d in devs:
-                    d.set_stream(ps.cuda_stream)
-                G.engine.prepass_batch(ters, 0, B, buf.data_ptr())
-                ev = torch.cuda.Event()
-                ev.record(ps)
-                look["ev"][k] = ev
-                first = devs[0]
-                for d in devs:
-                    d.set_stream(None if d is first else first.stream())
-            else:
-                G.engine.prepass_batch(ters, 0, B, buf.data_ptr())
-
-        def step_look(r, n):
-            k = look["k"]
-            g = k % a.depth
-            ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
-            devs = [d for d, _ in ring.slots[g * B:(g + 1) * B]]
-            if look["next"] != k:
-                issue_prepass(k, r, n)
-            issue_prepass(k + 1, r, n)
-            look["next"] = k + 1
-            if a.lookahead == 2:
-                gs = torch.cuda.ExternalStream(devs[0].stream(), device="cuda:0")
-                gs.wait_event(look["ev"].pop(k))
-            G.engine.trace_batch(ters, r, n, look["bufs"][k % len(look["bufs"])].data_ptr())
-            look["k"] = k + 1
-            ring.frame += B
-
         def step(r, n):
-            if a.lookahead:
-                step_look(r, n)
-                return
             if not a.split_prepass or n == 1:
                 ring.render_batch(r, n, present=False)
                 return
@@ -132,7 +100,8 @@ def main():
                 worst = max(worst, ms)
             if base is None:
                 base = worst
-            print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "n": n, "worst_frame_ms": round(worst, 4),
+            print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass,
+                              "lookahead": int(ring.lookahead), "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()
 

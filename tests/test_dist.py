@@ -129,6 +129,17 @@ class HostOps:
         for f in range(self.n):
             self._render(f, synthetic_cameras(f))
 
+    def prepass_ahead(self):
+        self.log.append(("prepass_ahead",))
+
+    def prepass_ahead_next(self):
+        self.log.append(("prepass_ahead_next",))
+
+    def trace_ahead(self):
+        self.log.append(("trace_ahead",))
+        for f in range(self.n):
+            self._render(f, synthetic_cameras(f))
+
     def pack(self, f, shard, off):
         import torch
 
@@ -167,7 +178,7 @@ def _batch_worker(rank, world, port, w, h, batch, frames, split, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        plan = P.BatchPlan(w, h, batch, world, split_prepass=split)
+        plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead")
         coll = P.Collectives(dist, "gloo", rank, world)
         group = dist.new_group(backend="gloo") if plan.split_prepass else None
         ops = HostOps(plan, rank, coll, w, h, frames, group)
@@ -195,6 +206,8 @@ def _batch_worker(rank, world, port, w, h, batch, frames, split, q):
     (2, 64, 48, 5, 5, True),         # 4 tiles; chunk 3: rank 1 runs 2 prepass frames
     (3, 64, 48, 3, 3, True),         # 4 tiles % 3 != 0: shards of 2, 1, 1 tiles
     (3, 50, 36, 12, 7, False),       # unsplit prepass, partial batch
+    (2, 1920, 1080, 12, 12, "ahead"),  # bench default: unsplit, the next batch's prepass queued ahead
+    (3, 50, 36, 12, 7, "ahead"),     # the same, partial batch
 ])
 def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
     """bench.py's N>1 batch sequence, driven through parallel.run_batch with host ops: split
@@ -214,9 +227,12 @@ def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
     ok, log, per_rank, skew = q.get(timeout=10)
     assert ok
     from gpgpuraytrace_amd import parallel as P
-    plan = P.BatchPlan(w, h, batch, world, split_prepass=split)
+    plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead")
     if plan.split_prepass:
         assert log[0] == ("prepass", 0, min(plan.chunk, frames)) and ("trace",) in log
+    elif plan.lookahead:
+        # this batch's prepass, then the next one's, both queued before this trace
+        assert log[:3] == [("prepass_ahead",), ("prepass_ahead_next",), ("trace_ahead",)]
     else:
         assert log[0] == ("render",)
     # rank 0: one pack of its frames, one unpack of every other rank's (one launch each on the GPU)

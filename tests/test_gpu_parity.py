@@ -590,6 +590,63 @@ def test_frame_ring_in_flight_bitexact():
     ring.destroy()
 
 
+def test_frame_ring_lookahead_bitexact():
+    """FrameRing(lookahead=True) (bench.py's default frame loop): each batch's prepass queued on
+    the side stream before the previous batch's trace (rt_terrain_prepass_ahead), two slot groups
+    so the ahead prepass rewrites CameraResults the batch before it in the same group read; every
+    batch equals the golden frames of its cameras, including a batch whose cameras change after
+    its prepass was queued (rt_terrain_trace_ahead prepasses again) and a partial batch."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    cams = []
+    for spec in (GI.FRAMES[0], GI.FRAMES[1]):  # nomadplains 64x48, reset / lookdown
+        land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+        cams.append((FixedCamera(GI.consts(w, h, pose)), GI.frame_key(*spec)))
+    w, h = cams[0][0].width, cams[0][0].height
+    ring = G.FrameRing(w, h, depth=2, batch=3, camera=cams[0][0], lookahead=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cams[0][0].c["sun"])
+
+    def set_group(g, seq):
+        keys = []
+        for (dev, ter), c in zip(ring.slots[g * 3:(g + 1) * 3], seq):
+            ter.set_camera(cams[c][0])
+            ter.update_terrain()
+            keys.append((dev, cams[c][1]))
+        return keys
+
+    def check(keys, n=3):
+        for dev, key in keys[:n]:
+            assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), key
+
+    seqs = [(0, 1, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (0, 1, 1), (1, 0, 1)]
+    expect = [set_group(0, seqs[0])]
+    for b in range(len(seqs)):
+        if b + 1 < len(seqs):  # the next batch's cameras, before its prepass is queued below
+            expect.append(set_group((b + 1) % 2, seqs[b + 1]))
+        n = 2 if b == 4 else 3  # batch 4: a partial batch (the ahead prepass covered 3 frames)
+        ring.render_batch(frames=n, ahead=b + 1 < len(seqs))
+        if b == 2:  # batch 3's cameras change after its ahead prepass was queued
+            expect[3] = set_group(1, (1, 0, 1))
+        if b >= 1:  # the previous batch (the other group), while this one runs
+            check(expect[b - 1], 2 if b - 1 == 4 else 3)
+    ring.synchronize()
+    check(expect[-1])
+    # one ahead prepass per leading device at a time; none on hipGraph devices
+    ters = [t for _, t in ring.slots[:3]]
+    E.prepass_ahead(ters)
+    with pytest.raises(RuntimeError):
+        E.prepass_ahead(ters)
+    E.trace_ahead(ters)
+    ring.synchronize()
+    ring.destroy()
+    dev, ter = make(GI.consts(w, h, "reset"), graph=True)
+    with pytest.raises(RuntimeError):
+        E.prepass_ahead([ter])
+    dev.destroy()
+
+
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_graph_replay_bitexact(spec):
     """RT_DEVICE_GRAPH (the C5 hipGraph frame loop): frames replayed from the captured graphs
