@@ -4,6 +4,8 @@
 # outputs under gpurun_out/cfg_$ROUND/.
 # usage: ROUND=r02 bash scripts/measure_configs.sh [configs...]   (default: c2 c5 c3 ref)
 cd /tmp && export TMPDIR=/tmp
+# bench.py's hardware-queue count, here too: the profiler starts HIP first
+export GPU_MAX_HW_QUEUES=8
 cd "$GRAFT_REPO_ROOT"
 ROUND=${ROUND:-r03}
 O=gpurun_out/cfg_$ROUND; mkdir -p $O

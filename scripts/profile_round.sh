@@ -4,6 +4,8 @@
 # HBM traffic (FETCH_SIZE, WRITE_SIZE) and SQ issue counters.  Summarised into $OUT (default profiles/$ROUND) by
 # scripts/summarize_profiles.py (run where the repo is, after gpurun merged gpurun_out/).
 cd /tmp && export TMPDIR=/tmp
+# bench.py's hardware-queue count, here too: the profiler starts HIP first
+export GPU_MAX_HW_QUEUES=8
 cd "$GRAFT_REPO_ROOT"
 ROUND=${ROUND:-r03}
 # STEPS/WARMUP: the bench command profiled (STEPS=20 WARMUP=5: the driver's, two 10-frame launches);
