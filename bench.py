@@ -17,8 +17,9 @@ with D batches in flight (engine.FrameRing).  Exactly --steps frames are timed: 
 split into ceil(steps / B) batches of near-equal size.  Every frame is computed in full and
 independently; value / ms_per_step are the steady-state frame rate; config.frame_latency_ms is
 one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
-in flight, config.single_frame_serial one frame at a time with no overlap, and (C3) config.
-ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
+in flight, config.single_frame_serial one frame at a time with no overlap, config.sustained the
+timed loop's batches back to back for ~3 s (rates per 0.5 s window: clocks under a long load), and
+(C3) config.ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
 scaling: the frame is fixed); parallel.BatchPlan / run_batch hold the per-batch sequence
@@ -103,6 +104,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-companions", action="store_true",
                     help="skip config.single_frame / config.ref_semantics (extra timed passes)")
+    ap.add_argument("--sustained-s", type=float, default=3.0,
+                    help="N=1 companion config.sustained: the timed loop's batches back to back for about this "
+                         "many seconds (0 = skip)")
     ap.add_argument("--verify", action="store_true",
                     help="after the timed loop rank 0 checks every assembled frame of the last batch against a "
                          "whole-frame render on one device (RGBA8, bit for bit); adds config.verify (always on "
@@ -587,6 +591,41 @@ def main():
             "value": round(rc["rays"] * a.steps / dt / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt / a.steps * 1e3, 4), "rays_per_frame": rc["rays"],
             "how": "--config ref: the same frames and batching, uncapped march (tracing.hlsl:68), no AO"}
+
+    if world == 1 and not a.no_companions and a.sustained_s > 0:
+        # sustained rate: the timed loop's batches back to back for ~--sustained-s seconds (clocks and
+        # power under a long load), a HIP event after every batch on its stream, read once at the end
+        n_sus = max(2, int(a.sustained_s * 1e3 / (elapsed / a.steps * 1e3 * B) + 0.5))
+        uring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+                            time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
+        for _ in range(uring.depth + 1):
+            uring.render_batch()
+        uring.synchronize()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(torch.cuda.ExternalStream(uring.slots[0][0].stream(), device=f"cuda:{local}"))
+        ends = []
+        for _ in range(n_sus):
+            g = (uring.frame // B) % uring.depth
+            uring.render_batch()
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.ExternalStream(uring.slots[g * B][0].stream(), device=f"cuda:{local}"))
+            ends.append(ev)
+        uring.synchronize()
+        t_end = [ev0.elapsed_time(ev) for ev in ends]  # ms from the start, per batch
+        uring.destroy()
+        total = max(t_end)
+        # rates over windows of ~0.5 s (batch ends in order of completion)
+        t_sorted, wins, last_t, last_n = sorted(t_end), [], 0.0, 0
+        for i, t in enumerate(t_sorted):
+            if t - last_t >= 500.0 or (i + 1 == len(t_sorted) and t - last_t >= 250.0):
+                wins.append(rays_per_frame * B * (i + 1 - last_n) / ((t - last_t) * 1e-3) / 1e6)
+                last_t, last_n = t, i + 1
+        companions["sustained"] = {
+            "value": round(rays_per_frame * B * n_sus / (total * 1e-3) / 1e6, 3), "unit": "Mray/s",
+            "seconds": round(total * 1e-3, 3), "frames": n_sus * B,
+            "window_mrays": [round(w, 1) for w in wins],
+            "how": f"the timed loop's {B}-frame batches back to back for ~{a.sustained_s:g} s "
+                   f"({a.frames_in_flight} in flight), HIP event per batch; windows of ~0.5 s"}
 
     # this rank's phases of the timed batches (HIP events on each batch's stream, from the common
     # start barrier) and its tracescreen launch time; rank 0 reports every rank's (config.per_rank)
