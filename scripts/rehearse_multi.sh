@@ -12,4 +12,4 @@ run() { local n=$1; shift; PORT=$((PORT + 1))
     || { echo "n=$n failed"; tail -20 gpurun_out/reh/$PORT.err; return 1; }
   tail -1 gpurun_out/reh/$PORT.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['n_gpus'], d['config']['parallelism'], '->', d['config'].get('verify'))"
 }
-run 2 --no-companions && run 3 --no-companions --steps 10 --split-prepass 1 && run 3 --batch 5 --steps 5 --no-companions && run 4 --split-prepass 1 --batch 5 --steps 5 --no-companions  # split, 4 ranks x 2 frames: rank 3 has none
+run 2 --no-companions && run 2 --no-companions --lookahead 1 --steps 36 && run 3 --no-companions --steps 10 --split-prepass 1 && run 3 --batch 5 --steps 5 --no-companions && run 4 --split-prepass 1 --batch 5 --steps 5 --no-companions  # split, 4 ranks x 2 frames: rank 3 has none
