@@ -17,7 +17,8 @@ with D batches in flight (engine.FrameRing).  Exactly --steps frames are timed: 
 split into ceil(steps / B) batches of near-equal size.  Every frame is computed in full and
 independently; value / ms_per_step are the steady-state frame rate; config.frame_latency_ms is
 one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
-in flight, config.single_frame_serial one frame at a time with no overlap, config.sustained the
+in flight, config.single_frame_serial one frame at a time with no overlap, config.moving_camera
+the timed loop's batching over --steps distinct frames of a camera path, config.sustained the
 timed loop's batches back to back for ~3 s (rates per 0.5 s window: clocks under a long load), and
 (C3) config.ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
 
@@ -591,6 +592,50 @@ def main():
             "value": round(rc["rays"] * a.steps / dt / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt / a.steps * 1e3, 4), "rays_per_frame": rc["rays"],
             "how": "--config ref: the same frames and batching, uncapped march (tracing.hlsl:68), no AO"}
+
+    if world == 1 and not a.no_companions:
+        # a moving camera: every frame of the run distinct (the eye advances 2 units per frame along
+        # the view direction and the yaw turns 0.01 rad per frame), batched exactly like the timed
+        # loop; rays counted per frame by an instrumented render of each camera, and the run's last
+        # frame compared with that render (RGBA8, bit for bit)
+        base = G.Camera(W, H, euler=euler)
+        path = [G.Camera(W, H, position=base.position + i * 2.0 * np.asarray(base.front, float),
+                         euler=(euler[0], euler[1] + 0.01 * i, euler[2])) for i in range(a.steps)]
+        cdev, cter = make(stats=True)
+        path_rays, want_last = 0, None
+        for i, cam in enumerate(path):
+            cter.set_camera(cam)
+            cter.update_terrain()
+            cter.render_device(0, 1)
+            path_rays += W * H + cdev.stats(reset=True)["hits"] * (1 + a.ao) + 1024
+            if i + 1 == len(path):
+                want_last = cdev.readback()
+        cdev.destroy()
+        mring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+                            time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
+
+        def path_batch(first, n):
+            for (_, ter), cam in zip(mring.group(n), path[first:first + n]):
+                ter.set_camera(cam)
+                ter.update_terrain()
+            return mring.render_batch(frames=n)
+        for i in range(mring.depth + 1):  # warm-up over the path's first batches
+            path_batch((i * B) % max(1, a.steps - B + 1), min(B, a.steps))
+        mring.synchronize()
+        ts, first = time.perf_counter(), 0
+        for n in sizes:
+            devs = path_batch(first, n)
+            first += n
+        mring.synchronize()
+        dt = time.perf_counter() - ts
+        last_ok = bool(np.array_equal(devs[-1].readback(), want_last))
+        mring.destroy()
+        companions["moving_camera"] = {
+            "value": round(path_rays / dt / 1e6, 3), "unit": "Mray/s", "ms_per_frame": round(dt / a.steps * 1e3, 4),
+            "rays_per_frame_mean": round(path_rays / a.steps), "last_frame_rgba8_equal": last_ok,
+            "how": f"{a.steps} distinct frames (eye +2 units and yaw +0.01 rad per frame), the timed loop's "
+                   f"batches {sizes}, cameras written into each slot group before its batch; the last frame "
+                   f"against an instrumented single-frame render of its camera"}
 
     if world == 1 and not a.no_companions and a.sustained_s > 0:
         # sustained rate: the timed loop's batches back to back for ~--sustained-s seconds (clocks and
