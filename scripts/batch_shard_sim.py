@@ -74,9 +74,9 @@ def main():
             G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
         torch.cuda.synchronize()
 
-        def step(r, n):
+        def step(r, n, ahead=True):
             if not a.split_prepass or n == 1:
-                ring.render_batch(r, n, present=False)
+                ring.render_batch(r, n, present=False, ahead=ahead)
                 return
             g = (ring.frame // B) % ring.depth
             ters = [t for _, t in ring.slots[g * B:(g + 1) * B]]
@@ -87,13 +87,13 @@ def main():
         for n in [int(x) for x in a.ns.split(",")]:
             worst, per = 0.0, []
             for r in (range(n) if a.ranks == "all" else [0]):
-                for _ in range(2 * a.depth):
-                    step(r, n)
+                for i in range(2 * a.depth):  # (lookahead: no ahead prepass across the timed region's edges)
+                    step(r, n, ahead=i + 1 < 2 * a.depth)
                 torch.cuda.synchronize()
                 nb = max(1, a.frames // B)
                 t0 = time.perf_counter()
-                for _ in range(nb):
-                    step(r, n)
+                for i in range(nb):
+                    step(r, n, ahead=i + 1 < nb)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / (nb * B) * 1e3
                 per.append(round(ms, 4))
