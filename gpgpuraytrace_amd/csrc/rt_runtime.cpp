@@ -232,6 +232,7 @@ struct Shader {
     bool has_cb[CB_COUNT] = {};
     std::vector<uint8_t> cb[CB_COUNT];
     bool cb_dirty = true;
+    bool grad_dirty = true; // CBNoise (permGradients) changed: its own upload, not one per camera move
     std::vector<std::unique_ptr<rt_variable_s>> vars;
     std::vector<std::unique_ptr<rt_array_s>> arrays;
     rt_texture textures[16] = {};
@@ -430,9 +431,12 @@ int sync_shader(rt_device dev, Shader* s)
         build_consts(*s, *dev, s->host_consts);
         int rc = s->consts_staging.upload(dev->stream, s->d_consts, &s->host_consts, sizeof(RtConsts));
         if (rc) return rc;
-        rc = s->grad_staging.upload(dev->stream, s->d_grad, s->cb[CB_NOISE].data(), 128 * sizeof(float4));
-        if (rc) return rc;
         s->cb_dirty = false;
+    }
+    if (s->grad_dirty) {
+        int rc = s->grad_staging.upload(dev->stream, s->d_grad, s->cb[CB_NOISE].data(), 128 * sizeof(float4));
+        if (rc) return rc;
+        s->grad_dirty = false;
     }
     return RT_OK;
 }
@@ -1063,6 +1067,7 @@ int rt_variable_write(rt_variable v, const void* data)
     if (!memcmp(dst, data, v->size)) return RT_OK; // unchanged: no upload (and an ahead prepass stays current)
     memcpy(dst, data, v->size);
     if (v->cbuf != CB_DISPATCH) s->cb_dirty = true; // ThreadOffset is a launch argument
+    if (v->cbuf == CB_NOISE) s->grad_dirty = true;
     return RT_OK;
 }
 size_t rt_variable_size(rt_variable v) { return v ? (size_t)v->size : 0; }
@@ -1926,6 +1931,7 @@ void net_loop() // VariableManager.cpp:124-188
                 if (v.name == name && v.size == size) {
                     memcpy(v.owner->cb[v.cbuf].data() + v.offset, data.data(), (size_t)size);
                     v.owner->cb_dirty = true;
+                    if (v.cbuf == CB_NOISE) v.owner->grad_dirty = true;
                     break;
                 }
         }
