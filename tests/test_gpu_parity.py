@@ -647,6 +647,34 @@ def test_frame_ring_lookahead_bitexact():
     dev.destroy()
 
 
+def test_trace_ahead_uses_the_ahead_prepass_unless_a_camera_changed():
+    """rt_terrain_trace_ahead consumes the pending ahead prepass (one prepass in the stats) when the
+    camera constants were only rewritten with the same bytes (rt_variable_write skips unchanged
+    bytes), and prepasses again in line after a real camera change; the frames are golden both ways."""
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    s0, s1 = GI.FRAMES[0], GI.FRAMES[1]  # nomadplains 64x48, reset / lookdown
+    land, pose0, w, h, aa, ms, ao = GI.unpack(s0)
+    pose1 = GI.unpack(s1)[1]
+    dev, ter = make(GI.consts(w, h, pose0), stats=True)
+    one = gold[GI.frame_key(*s0) + "_stats"][1]  # prepass steps of one frame
+    dev.stats(reset=True)
+    E.prepass_ahead([ter])
+    ter.update_terrain()  # the same camera written again
+    E.trace_ahead([ter])
+    dev.synchronize()
+    assert dev.stats(reset=True)["prepass_steps"] == one
+    assert np.array_equal(dev.readback(), gold[GI.frame_key(*s0) + "_rgba8"])
+    E.prepass_ahead([ter])
+    ter.set_camera(FixedCamera(GI.consts(w, h, pose1)))
+    ter.update_terrain()  # a real change after the ahead prepass was queued
+    E.trace_ahead([ter])
+    dev.synchronize()
+    assert dev.stats(reset=True)["prepass_steps"] == one + gold[GI.frame_key(*s1) + "_stats"][1]
+    assert np.array_equal(dev.readback(), gold[GI.frame_key(*s1) + "_rgba8"])
+    dev.destroy()
+
+
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_graph_replay_bitexact(spec):
     """RT_DEVICE_GRAPH (the C5 hipGraph frame loop): frames replayed from the captured graphs
