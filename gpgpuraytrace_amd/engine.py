@@ -9,6 +9,8 @@ ShaderArray (Graphics/IShaderVariable.h), Texture (Factories/ITexture.h), Noise
 reference: bool returns / None for missing names; HIP failures raise.
 """
 import ctypes as C
+import os
+import warnings
 
 import numpy as np
 
@@ -617,6 +619,16 @@ class FrameRing:
         if lookahead and graph:
             raise ValueError("lookahead runs the prepass on a side stream: not with graph=True")
         self.lookahead, self._ahead = bool(lookahead), set()  # groups with an ahead prepass queued
+        # one HIP hardware queue per busy stream: the groups', the side stream, torch's default
+        # (DESIGN.md section 7); fewer make two groups share one and their batches serialise
+        want = self.depth + 1 + int(self.lookahead)
+        try:
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        except ValueError:
+            have = 4
+        if self.depth > 1 and have < want:
+            warnings.warn(f"FrameRing: {want} busy streams but GPU_MAX_HW_QUEUES={have}; set it to >= {want} "
+                          "before HIP starts, or the batches in flight may run one after the other", stacklevel=2)
         self.slots = []
         for _ in range(self.depth * self.batch):
             dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph,

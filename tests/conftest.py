@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+# the frame rings under test keep several streams busy: one HIP hardware queue each, as bench.py
+# sets; before anything starts HIP
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 
 def pytest_configure(config):
