@@ -723,6 +723,7 @@ def main():
                     + (" + prepass split over ranks (RCCL all-gather of CameraResults)" if plan.split_prepass
                        else "")),
                 "batch": B, "batches": sizes, "batches_in_flight": a.frames_in_flight,
+                "hip_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "frame_loop": "hipGraph replay per slot (prepass graph + tracescreen graph)" if a.graph
                               else "direct launches" + (", each batch's prepass queued one batch ahead on the GPU's "
                                                         "side stream (rt_terrain_prepass_ahead)" if plan.lookahead else ""),
