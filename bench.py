@@ -19,7 +19,7 @@ independently; value / ms_per_step are the steady-state frame rate; config.frame
 one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
 in flight, config.single_frame_serial one frame at a time with no overlap, config.moving_camera
 the timed loop's batching over --steps distinct frames of a camera path, config.sustained the
-timed loop's batches back to back for ~3 s (rates per ~1 s window: clocks under a long load), and
+timed loop's batches back to back for ~5 s (rates per ~1 s window: clocks under a long load), and
 (C3) config.ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
 
 N>1: the frame's 32x32-pixel tiles are dealt tile-cyclically over the ranks (strong
@@ -105,7 +105,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-companions", action="store_true",
                     help="skip config.single_frame / config.ref_semantics (extra timed passes)")
-    ap.add_argument("--sustained-s", type=float, default=3.0,
+    ap.add_argument("--sustained-s", type=float, default=5.0,
                     help="N=1 companion config.sustained: the timed loop's batches back to back for about this "
                          "many seconds (0 = skip)")
     ap.add_argument("--verify", action="store_true",
