@@ -389,6 +389,8 @@ def main():
                              for _ in range(world)] if rank == 0 else None,
                 "cams": torch.zeros(plan.camera_floats(), dtype=torch.float32, device=dev_str),
             })
+        # the fills ran on torch's stream; the batches' streams are non-blocking (no implicit order)
+        torch.cuda.synchronize()
 
     class DeviceOps:
         """run_batch's actions on this GPU: HIP kernels through the C-ABI, RCCL collectives."""

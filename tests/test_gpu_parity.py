@@ -460,6 +460,7 @@ def test_shards_assemble_to_full_frame(world):
     devs = [make(consts) for _ in range(world)]
     maxb = max(E.shard_bytes(d, r, world) for r, (d, _) in enumerate(devs))
     bufs = [torch.zeros(maxb, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    torch.cuda.synchronize()  # the fill (torch's stream) before the devices' non-blocking streams
     for r, (d, t) in enumerate(devs):
         t.render_device(r, world)
         E.shard_pack(d, r, world, bufs[r].data_ptr())
@@ -499,6 +500,7 @@ def test_shard_batch_pack_unpack_roundtrip(w, h, world, frames):
         assert np.array_equal(d.readback().view(np.uint32).reshape(h, w), img)
     plan = P.BatchPlan(w, h, frames, world)
     packed = torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()  # the fill (torch's stream) before the devices' non-blocking streams
     items = [(f, f % world, plan.pack_offset(f)) for f in range(frames)]
     E.shard_pack_batch([devs[f] for f, _, _ in items], [s for _, s, _ in items], world,
                        [packed.data_ptr() + off for _, _, off in items])
@@ -716,6 +718,7 @@ def test_graph_constants_shards_and_swap():
     assert dev.graph_info() == (2, 6)
     # two shards replayed on one device, packed, then assembled
     bufs = [torch.zeros(E.shard_bytes(dev, r, 2), dtype=torch.uint8, device="cuda:0") for r in range(2)]
+    torch.cuda.synchronize()  # the fill (torch's stream) before the device's non-blocking stream
     for r in (1, 0):
         ter.render_device(r, 2)
         E.shard_pack(dev, r, 2, bufs[r].data_ptr())
@@ -815,6 +818,7 @@ def test_batch_shards_graphs_and_ring():
             for f, (d, _) in enumerate(frames):
                 # frame f of a batch traces shard (r + f) % 2 (the per-frame rotation)
                 bufs[r, f] = torch.zeros(E.shard_bytes(d, (r + f) % 2, 2), dtype=torch.uint8, device="cuda:0")
+                torch.cuda.synchronize()  # the fill (torch's stream) before the device's stream
                 E.shard_pack(d, (r + f) % 2, 2, bufs[r, f].data_ptr())
                 d.synchronize()
         for f, (d, _) in enumerate(ranks[0]):
@@ -862,12 +866,19 @@ def test_batch_ragged_rotated_shards_bitexact(w, h, world, split):
     plan = P.BatchPlan(w, h, len(specs), world, split_prepass=split)
     ranks = [[make(consts[s[1]]) for s in specs] for _ in range(world)]
     cams = torch.full((plan.camera_floats(),), float("nan"), dtype=torch.float32, device="cuda:0")
+    packed = [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    # the fills run on torch's stream; the devices' streams are non-blocking (no implicit order)
+    torch.cuda.synchronize()
     if split:
         for r, frames in enumerate(ranks):
             first, count = plan.prepass_range(r)
             # frame f's CameraResults land at f * 16 KiB: rank r's frames fill its plan.camera_slice(r)
             E.prepass_batch([t for _, t in frames], first, count, cams.data_ptr())
-    packed = [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+        # every rank's prepass is complete before any rank traces (bench.py: the all-gather); a
+        # rank's trace reads the other ranks' frames' CameraResults
+        for frames in ranks:
+            for d, _ in frames:
+                d.synchronize()
     for r, frames in enumerate(ranks):
         ters = [t for _, t in frames]
         if split:
@@ -900,6 +911,7 @@ def test_batch_split_prepass_bitexact():
     frames = _batch(specs, stats=True)
     ters = [t for _, t in frames]
     buf = torch.full((len(specs), 1024, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()  # the fill (torch's stream) before the devices' non-blocking streams
     # (5, 0) and (6, 0): ranks past the last frame (bench.py at N = 8 with 12-frame batches)
     for first, count in ((0, 2), (2, 2), (4, 1), (5, 0), (6, 0)):
         E.prepass_batch(ters, first, count, buf.data_ptr())
