@@ -900,6 +900,48 @@ def test_batch_ragged_rotated_shards_bitexact(w, h, world, split):
             d.destroy()
 
 
+@pytest.mark.parametrize("world", [2, 8])
+def test_c4_sharded_batch_1080p_assembles_whole_frames(world):
+    """BASELINE configs[3] (C4: 1920x1080 tiled over 2/4/8 GPUs, RCCL gather) emulated on one GPU
+    at full size with the C3 settings (512-step cap, shadow, 1 AO): N ranks each trace their
+    rotated shard (r + f) % N of every frame of a 4-frame batch mixing both poses
+    (rt_terrain_render_batch), pack it at the plan's offsets (rt_shard_pack_batch); rank 0 unpacks
+    every other rank's frames (rt_shard_unpack_batch), exactly bench.py's run_batch at N > 1 with
+    the gather's copy done by hand.  Every assembled RGBA8 frame equals the whole-frame render of
+    its pose (itself checked against the oracle by test_baseline_config_rows_bitexact)."""
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    poses = ["reset", "lookdown", "reset", "lookdown"]
+    want = {}
+    for pose in ("reset", "lookdown"):
+        dev, ter = make(GI.consts(1920, 1080, pose), max_steps=512, ao=1)
+        ter.render_device()
+        want[pose] = dev.readback()
+        dev.destroy()
+    plan = P.BatchPlan(1920, 1080, len(poses), world)
+    ranks = [[make(GI.consts(1920, 1080, pose), max_steps=512, ao=1) for pose in poses] for _ in range(world)]
+    packed = [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    torch.cuda.synchronize()  # the fills (torch's stream) before the devices' non-blocking streams
+    for r, frames in enumerate(ranks):
+        E.render_batch([t for _, t in frames], r, world)
+        items = plan.packs(r)
+        E.shard_pack_batch([frames[f][0] for f, _, _ in items], [s for _, s, _ in items], world,
+                           [packed[r].data_ptr() + off for _, _, off in items])
+        for d, _ in frames:
+            d.synchronize()
+    items = plan.unpacks()
+    E.shard_unpack_batch([ranks[0][f][0] for _, f, _, _ in items], [s for _, _, s, _ in items], world,
+                         [packed[src].data_ptr() + off for src, _, _, off in items])
+    for f, ((d, _), pose) in enumerate(zip(ranks[0], poses)):
+        got = d.readback()
+        assert np.array_equal(got, want[pose]), (world, f, pose, int((got != want[pose]).any(-1).sum()))
+    for frames in ranks:
+        for d, _ in frames:
+            d.destroy()
+
+
 def test_batch_split_prepass_bitexact():
     """rt_terrain_prepass_batch in three ranks' shares into one buffer (what the all-gather
     produces), then rt_terrain_trace_batch from it: the golden frames, and every frame's
