@@ -275,10 +275,31 @@ def progress(rank, msg):
     print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
 
 
+def launch_ranks(a):
+    """`python bench.py --gpus N` (N > 1) outside a torch.distributed launcher: run the same command
+    under `torch.distributed.run` (one rank per GPU, rendezvous on 127.0.0.1) as a CHILD process,
+    before this process touches the GPU, and exit with its code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    progress(0, f"--gpus {a.gpus} without a launcher: starting {a.gpus} ranks under torch.distributed.run")
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse()
     if a.traffic_child:
         return traffic_child(a)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(a)
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != a.gpus:
+        progress(int(os.environ.get("RANK", "0")), f"note: --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}; "
+                 "the run uses WORLD_SIZE ranks")
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -768,4 +789,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
