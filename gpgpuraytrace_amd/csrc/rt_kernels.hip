@@ -794,6 +794,14 @@ constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a d
 #define RT_SEG_QUEUE 64
 #endif
 constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSegQueue = RT_SEG_QUEUE;
+// A primary unit's last few rays (nomadplains): once at most kPrimarySeg rays of an 8x8 unit are
+// still marching, they continue as segments of 64 / kPrimarySeg lanes per ray (primary_seg in
+// k_trace) instead of keeping 64 lanes on a few rays' octave loops.  0: off.
+#ifndef RT_PRIMARY_SEG // A/B: make variant FLAGS=-DRT_PRIMARY_SEG=n (0, 4, 8 or 16)
+#define RT_PRIMARY_SEG 8
+#endif
+constexpr uint32_t kPrimarySeg = RT_PRIMARY_SEG;
+static_assert(kPrimarySeg == 0u || kPrimarySeg == 4u || kPrimarySeg == 8u || kPrimarySeg == 16u, "lanes per ray");
 
 // STATS kernels: a k_trace block's march-step and hit counters (LDS atomics; the block's last wave
 // adds them to the frame statistics)
@@ -1120,6 +1128,72 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
     };
 
+    // ---- a primary unit's last <= kPrimarySeg live rays, a segment of kSegLanes lanes per ray ----
+    // lb: the unit's live rays; st: every lane's march (the finished rays' final states stay in
+    // their lanes).  The live rays' states move to their segments (ray r of lb to lanes r*LPR ..),
+    // march there with the density's octaves spread over the segment (density_nomadplains_seg,
+    // bit-identical to density_nomadplains; pow_nonneg_flat for the step factor, bit-identical to
+    // pow_nonneg) and come back when every segment's ray has left the march.
+    auto primary_seg = [&](const Ctx& cf, March<L, true>& st, bool lv, uint64_t lb, float spx, float spy) {
+        if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && !STATS) {
+            constexpr uint32_t LPR = 64u / (kPrimarySeg ? kPrimarySeg : 8u);
+            const uint32_t lid = late(lane);
+            const uint32_t j = lid & (LPR - 1u), grp = lid / LPR, base = lid & ~(LPR - 1u);
+            const uint32_t n = (uint32_t)__popcll(lb);
+            // the lane of live ray grp (scalar loop over lb's <= kPrimarySeg set bits)
+            uint32_t src = lid;
+            uint64_t rem = lb;
+            for (uint32_t r = 0; r < n; ++r) {
+                const uint32_t sl = (uint32_t)__builtin_ctzll(rem);
+                rem &= rem - 1ull;
+                src = grp == r ? sl : src;
+            }
+            March<L, true> sg;
+            sg.p = rtm::mk(__shfl(st.p.x, (int)src), __shfl(st.p.y, (int)src), __shfl(st.p.z, (int)src));
+            sg.dir = rtm::mk(__shfl(st.dir.x, (int)src), __shfl(st.dir.y, (int)src), __shfl(st.dir.z, (int)src));
+            sg.sd = __shfl(st.sd, (int)src);
+            sg.dist = __shfl(st.dist, (int)src);
+            sg.step = __shfl(st.step, (int)src);
+            sg.lastStep = __shfl(st.lastStep, (int)src);
+            sg.d = __shfl(st.d, (int)src);
+            sg.iters = __shfl(st.iters, (int)src);
+            sg.f = {0.0f, 0.0f, 0.0f, 0.0f}; // no fog in nomadplains (March::FOG is false)
+            sg.fog = false;
+            bool live = grp < n;
+            const SegOctaves<LPR> g = seg_octaves<LPR>(cf, j);
+            for (;;) {
+                if (live && !march_live<L, true, false>(cf, sg, RT_CAMERA_FAR, max_steps)) live = false;
+                if (!__ballot(live)) break;
+                if (live) {
+                    auto dens = [&](f3 q0) {
+                        uint32_t used;
+                        return density_nomadplains_seg<LPR, true>(cf, g, q0, j, base, &used);
+                    };
+                    march_step_with<L, true, false, decltype(dens), true>(cf, sg, dens);
+                }
+            }
+            // back to the rays' lanes (the march changes only these fields)
+            const int back = (int)(lane_rank(lb) * LPR);
+            const float sd = __shfl(sg.sd, back), dist = __shfl(sg.dist, back), step = __shfl(sg.step, back);
+            const float last = __shfl(sg.lastStep, back), d = __shfl(sg.d, back);
+            const int iters = __shfl(sg.iters, back);
+            if (lv) {
+                st.sd = sd;
+                st.dist = dist;
+                st.step = step;
+                st.lastStep = last;
+                st.d = d;
+                st.iters = iters;
+            }
+            // every ray's origin and direction again, as march_begin formed them (the pixel ray,
+            // normalised): they are not held across the segments' march
+            f3 p, dir;
+            get_pixel_ray(cf, spx, spy, &p, &dir);
+            st.p = p;
+            st.dir = rtm::scale(dir, rtm::rcp(rtm::length(dir)));
+        }
+    };
+
     // ---- a batch of up to 64 queued hits: shading + first shadow step ----
     auto do_shade = [&]() {
         q_lock(&q.lock, lane);
@@ -1218,6 +1292,12 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     cf.nz.phase = RT_PHASE_PRIMARY;
                 }
 #endif
+                if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && !STATS) {
+                    if ((uint32_t)__popcll(lb) <= kPrimarySeg) {
+                        primary_seg(cf, st, lv, lb, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1]);
+                        break;
+                    }
+                }
                 if (lv) march_step<L, true, false>(cf, st);
                 if (it == 96u) __builtin_amdgcn_s_setprio(1);
                 else if (it == 224u) __builtin_amdgcn_s_setprio(2);

@@ -409,7 +409,12 @@ __device__ __forceinline__ SegOctaves<LPR> seg_octaves(const Ctx& c, uint32_t j)
     return g;
 }
 
-template <int LPR>
+// LOWREG: the octave values are gathered one at a time inside the weighted sum (each gather
+// waits for the previous fma), so one gathered value is live instead of all 18, and each round's
+// octave scales come from the LDS octave table (nz.oct: the same np_scale / np_scale_y values)
+// instead of registers: for callers that hold other rays' state across the march (k_trace's
+// primary_seg), at the cost of a serial chain.
+template <int LPR, bool LOWREG = false>
 __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const SegOctaves<LPR>& g, f3 p, uint32_t j,
                                                          uint32_t base, uint32_t* octaves)
 {
@@ -429,7 +434,15 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
         const bool need = v < (uint32_t)NV && (v == 0u || (int)v <= n_oct);
         float n = 0.0f;
         if (__ballot(need)) {
-            float nx = q0.x * g.sx[r], ny = q0.y * g.sy[r], nzz = q0.z * g.sx[r];
+            float sx = g.sx[r], sy = g.sy[r];
+            if constexpr (LOWREG) { // the same scales from the LDS octave table, per round (no VGPRs held)
+                typedef __attribute__((address_space(3))) const float lds_f;
+                const uint32_t o = v >= 1u && v <= (uint32_t)RT_NP_OCTAVES ? v : 1u;
+                const lds_f* sc = (const lds_f*)(c.nz.oct + o);
+                sx = sc[0];
+                sy = sc[1];
+            }
+            float nx = q0.x * sx, ny = q0.y * sy, nzz = q0.z * sx;
             if (r == 0 && v == 0u) {
                 nx = p1.x * 0.007138f;
                 ny = p1.z * 0.007138f;
@@ -439,15 +452,26 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
         }
         nv[r] = need ? n : 0.0f;
     }
-    float on[NV];
+    float s = 0.0f, on0;
+    if constexpr (LOWREG) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) on[v] = __shfl(nv[v / LPR], (int)(base + (uint32_t)(v % LPR)), 64);
-    float s = 0.0f;
+        for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
+            int idx = (int)(base + (uint32_t)(N % LPR));
+            asm volatile("" : "+v"(idx) : "v"(s)); // this gather after the previous fma
+            s = fma(__shfl(nv[N / LPR], idx, 64), g.rcp[N], s);
+        }
+        on0 = __shfl(nv[0], (int)base, 64);
+    } else {
+        float on[NV];
 #pragma unroll
-    for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N], g.rcp[N], s);
+        for (int v = 0; v < NV; ++v) on[v] = __shfl(nv[v / LPR], (int)(base + (uint32_t)(v % LPR)), 64);
+#pragma unroll
+        for (int N = 1; N <= RT_NP_OCTAVES; ++N) s = fma(on[N], g.rcp[N], s);
+        on0 = on[0];
+    }
     *octaves = (uint32_t)n_oct;
     s = rtm::pow_nonneg_flat(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
-    float steep = rtm::sat((on[0] - 0.2f) * 6.0f) * 7.5f;
+    float steep = rtm::sat((on0 - 0.2f) * 6.0f) * 7.5f;
     s = terraces(s, p1.y, steep);
     // floor lift: pow(0, 1.5) == 0 exactly, so a wave whose bases are all 0 (every
     // sample above y = 25, the common case) skips the polynomial
