@@ -315,9 +315,10 @@ def main():
     if os.environ.get("RT_BENCH_WATCHDOG"):  # diagnostics: every rank's Python stack every N s on stderr
         import faulthandler
         faulthandler.dump_traceback_later(int(os.environ["RT_BENCH_WATCHDOG"]), repeat=True)
+    # the rank's GPU first: RCCL's communicator and the barrier's device follow the current device
+    torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group(backend)
-    torch.cuda.set_device(local)
 
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
