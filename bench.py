@@ -48,7 +48,8 @@ sys.path.insert(0, ROOT)
 # two busy streams share a queue and the batches the ring overlaps run one after the other
 # (profiles/r03/hw_queues.md: one-rank shard simulation at N=8, one extra stream alive,
 # 0.397 -> 0.430 ms/frame; 8 queues: 0.398).
-os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# (RT_BENCH_HW_QUEUES overrides the count for A/B runs)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
 
 METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
@@ -699,7 +700,16 @@ def main():
 
     # this rank's phases of the timed batches (HIP events on each batch's stream, from the common
     # start barrier) and its tracescreen launch time; rank 0 reports every rank's (config.per_rank)
-    phases = P.phase_summary(timed_marks, lambda x, y: x.elapsed_time(y), t0=timed_t0)
+    def event_ms(x, y):
+        """HIP event pair -> ms; None if HIP refuses the pair (the phase summary is diagnostic: it
+        must not end the run; the C1 config's events were refused once, hipErrorCapturedEvent)"""
+        try:
+            return x.elapsed_time(y)
+        except Exception as e:  # noqa: BLE001
+            progress(rank, f"phase marks: elapsed_time refused ({type(e).__name__}); phase left out")
+            return None
+
+    phases = P.phase_summary(timed_marks, event_ms, t0=timed_t0)
     phases.update({"rank": rank, "tracescreen_kernel_ms": round(k_avg_ms, 4)})
     per_rank = [phases]
     if world > 1:

@@ -1052,7 +1052,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // ---- after the drain: up to 64 / kSegLanes queued long rays, a segment of lanes per ray ----
     auto do_shadow_seg = [&]() {
         if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
-            constexpr uint32_t LPR = kSegLanes, RPW = 64u / kSegLanes;
+            constexpr uint32_t LPR = kSegLanes ? kSegLanes : 8u, RPW = 64u / LPR; // (8 only to compile the discarded branch when off)
             // late(): the segment's lane values (and the octave scales derived from them) are formed
             // here, not hoisted into the kernel's prologue where they would stay live throughout
             const uint32_t lid = late(lane);
@@ -1128,7 +1128,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
     };
 
-    // ---- a primary unit's last <= kPrimarySeg live rays, a segment of kSegLanes lanes per ray ----
+    // ---- a primary unit's last <= kPrimarySeg live rays, a segment of 64 / kPrimarySeg lanes per ray ----
     // lb: the unit's live rays; st: every lane's march (the finished rays' final states stay in
     // their lanes).  The live rays' states move to their segments (ray r of lb to lanes r*LPR ..),
     // march there with the density's octaves spread over the segment (density_nomadplains_seg,

@@ -190,7 +190,7 @@ PHASES = ("prepass", "all_gather", "trace", "pack", "gather", "unpack")
 
 def phase_summary(batches, elapsed_ms, t0=None):
     """Per-phase times of one rank's batches.  batches: per batch the [(name, clock)] marks of
-    run_batch (a HIP event or a host time); elapsed_ms(a, b): ms from clock a to clock b; t0: the
+    run_batch (a HIP event or a host time); elapsed_ms(a, b): ms from clock a to clock b, or None when unreadable (left out); t0: the
     clock the timed region started at (per batch, or one for all), for each batch's trace start.
     Returns {"batches", "phase_ms" (mean per batch), "phase_ms_max", "trace_start_ms" (per batch,
     from t0: the prepass + all-gather end; the batch start when the prepass is not split)}.  A
@@ -200,12 +200,16 @@ def phase_summary(batches, elapsed_ms, t0=None):
     starts = []
     for i, marks in enumerate(batches):
         for (_, a), (name, b) in zip(marks, marks[1:]):
-            per[name].append(elapsed_ms(a, b))
+            ms = elapsed_ms(a, b)
+            if ms is not None:  # None: the clock pair could not be read (the phase is left out)
+                per[name].append(ms)
         if t0 is not None:
             z = t0[i] if isinstance(t0, (list, tuple)) else t0
             names = [m[0] for m in marks]
             at = marks[names.index("all_gather")][1] if "all_gather" in names else marks[0][1]
-            starts.append(elapsed_ms(z, at))
+            ms = elapsed_ms(z, at)
+            if ms is not None:
+                starts.append(ms)
     out = {"batches": len(batches),
            "phase_ms": {p: round(float(sum(v) / len(v)), 4) for p, v in per.items() if v},
            "phase_ms_max": {p: round(float(max(v)), 4) for p, v in per.items() if v}}
