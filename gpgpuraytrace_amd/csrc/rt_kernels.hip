@@ -802,6 +802,13 @@ constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSe
 #endif
 constexpr uint32_t kPrimarySeg = RT_PRIMARY_SEG;
 static_assert(kPrimarySeg == 0u || kPrimarySeg == 4u || kPrimarySeg == 8u || kPrimarySeg == 16u, "lanes per ray");
+// The instrumented (STATS) kernels march a unit's last rays on 64 lanes: the counters would cost the
+// segment's registers (spills).  A diagnostic build (-DRT_STATS_PRIMARY_SEG=1, it spills) counts the
+// product's segment tail to measure its noise lane utilisation.
+#ifndef RT_STATS_PRIMARY_SEG
+#define RT_STATS_PRIMARY_SEG 0
+#endif
+constexpr bool kStatsPrimarySeg = RT_STATS_PRIMARY_SEG != 0;
 
 // STATS kernels: a k_trace block's march-step and hit counters (LDS atomics; the block's last wave
 // adds them to the frame statistics)
@@ -1135,7 +1142,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // bit-identical to density_nomadplains; pow_nonneg_flat for the step factor, bit-identical to
     // pow_nonneg) and come back when every segment's ray has left the march.
     auto primary_seg = [&](const Ctx& cf, March<L, true>& st, bool lv, uint64_t lb, float spx, float spy) {
-        if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && !STATS) {
+        if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && (!STATS || kStatsPrimarySeg)) {
             constexpr uint32_t LPR = 64u / (kPrimarySeg ? kPrimarySeg : 8u);
             const uint32_t lid = late(lane);
             const uint32_t j = lid & (LPR - 1u), grp = lid / LPR, base = lid & ~(LPR - 1u);
@@ -1167,7 +1174,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (live) {
                     auto dens = [&](f3 q0) {
                         uint32_t used;
-                        return density_nomadplains_seg<LPR, true>(cf, g, q0, j, base, &used);
+                        const float d = density_nomadplains_seg<LPR, true>(cf, g, q0, j, base, &used);
+                        if constexpr (STATS) { // diagnostic build only (kStatsPrimarySeg): density_nomadplains' count
+                            if (j == 0u) atomicAdd(&s_st.v[BlockStats::NOISE], (unsigned long long)(used + 1u));
+                            if (lane == (uint32_t)__builtin_ctzll(__ballot(1)))
+                                atomicAdd(&s_st.v[BlockStats::NOISE_WAVES], (unsigned long long)SegOctaves<LPR>::R);
+                        }
+                        return d;
                     };
                     march_step_with<L, true, false, decltype(dens), true>(cf, sg, dens);
                 }
@@ -1292,7 +1305,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     cf.nz.phase = RT_PHASE_PRIMARY;
                 }
 #endif
-                if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && !STATS) {
+                if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && (!STATS || kStatsPrimarySeg)) {
                     if ((uint32_t)__popcll(lb) <= kPrimarySeg) {
                         primary_seg(cf, st, lv, lb, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1]);
                         break;
