@@ -263,3 +263,20 @@ def test_batch_plan_bookkeeping():
     assert P.frame_shard(5, 0, 1) == 0
     with pytest.raises(ValueError):
         P.BatchPlan(64, 48, 17, 2)
+
+
+def test_phase_summary_leaves_out_unreadable_pairs():
+    """bench.py's event_ms returns None when HIP refuses an event pair: that phase (or the trace
+    start) is left out of config.per_rank instead of ending the run."""
+    from gpgpuraytrace_amd import parallel as P
+    marks = [("start", 0.0), ("trace", 2.0), ("pack", 2.5), ("gather", 3.0)]
+
+    def ms(a, b):
+        return None if (a, b) == (2.0, 2.5) else b - a
+
+    out = P.phase_summary([marks, marks], ms, t0=0.0)
+    assert out["phase_ms"] == {"trace": 2.0, "gather": 0.5}
+    assert "pack" not in out["phase_ms_max"]
+    assert out["trace_start_ms"] == [0.0, 0.0]
+    out = P.phase_summary([marks], lambda a, b: None, t0=0.0)
+    assert out["phase_ms"] == {} and out["trace_start_ms"] == []
