@@ -995,6 +995,39 @@ def test_batch_1080p_equals_single_frames(ao, ms):
         d.destroy()
 
 
+@pytest.mark.parametrize("ao", [0, 1])
+def test_edge_scenes_all_sky_and_eye_in_terrain(ao):
+    """Degenerate frames, single and batched (64x48, C3 step cap): a camera pitched up (every
+    prepass ray and every pixel misses: no hit records, no long rays, an all-zero hit ballot for
+    k_finish) and eyes inside the terrain at y = 30 and y = 12 (every ray hits within a few steps:
+    every pixel goes through the hit stack, shading and shadow / AO rays).  Each frame equals the
+    oracle's bit for bit and the march counts equal the oracle's."""
+    from gpgpuraytrace_amd import camera
+    from gpgpuraytrace_amd import engine as E
+    scenes = [camera.frame_constants(64, 48, euler=(-2.0, -4.6, 0.0)),
+              camera.frame_constants(64, 48, position=(0.0, 30.0, 0.0)),
+              camera.frame_constants(64, 48, position=(0.0, 12.0, 0.0))]
+    nz = O.noise_tables()
+    refs = [O.render(nz, O.make_frame(c, max_steps=512, ao=ao)) for c in scenes]
+    assert refs[0]["stats"]["primary_hits"] == 0 and refs[1]["stats"]["primary_hits"] == 64 * 48
+    for c, ref in zip(scenes, refs):
+        dev, ter = make(c, max_steps=512, ao=ao, stats=True)
+        ter.render_device()
+        assert bits_equal(dev.readback_float(), ref["rgba32f"])
+        assert np.array_equal(dev.readback(), ref["rgba8"])
+        st = dev.stats()
+        for key, okey in (("hits", "primary_hits"), ("primary_steps", "primary_steps"),
+                          ("shadow_steps", "shadow_steps"), ("prepass_steps", "prepass_steps")):
+            assert st[key] == ref["stats"][okey], key
+        dev.destroy()
+    frames = [make(c, max_steps=512, ao=ao) for c in scenes + scenes[::-1]]
+    E.render_batch([t for _, t in frames])
+    for (d, _), ref in zip(frames, refs + refs[::-1]):
+        assert np.array_equal(d.readback(), ref["rgba8"])
+    for d, _ in frames:
+        d.destroy()
+
+
 def test_batch_rejects_mixed_macro_sets():
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
