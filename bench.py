@@ -271,6 +271,24 @@ def measure_traffic(a, B):
         f"{kib['WRITE_SIZE'] / 1024:.1f} MiB")
 
 
+def stream_capturing(stream):
+    """hipStreamIsCapturing on a torch stream (bench.py's timed-region check): True while a hipGraph
+    capture is active on it."""
+    import ctypes
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipStreamIsCapturing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+    st = ctypes.c_int(0)
+    rc = _HIP.hipStreamIsCapturing(ctypes.c_void_p(stream.cuda_stream), ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"hipStreamIsCapturing failed: {rc}")
+    return st.value == 1  # hipStreamCaptureStatusActive
+
+
+_HIP = None
+
+
 def progress(rank, msg):
     """One progress line on stderr (the JSON line stays alone on stdout)."""
     print(f"[bench rank {rank}] {msg}", file=sys.stderr, flush=True)
@@ -412,8 +430,13 @@ def main():
                              for _ in range(world)] if rank == 0 else None,
                 "cams": torch.zeros(plan.camera_floats(), dtype=torch.float32, device=dev_str),
             })
-        # the fills ran on torch's stream; the batches' streams are non-blocking (no implicit order)
-        torch.cuda.synchronize()
+        # the fills ran on torch's stream; the batches' streams are non-blocking (no implicit order):
+        # every slot group's stream waits for them through the C-ABI's event handoff (ABI 6), no host
+        # synchronisation
+        filled = torch.cuda.Event()
+        filled.record(torch.cuda.current_stream())
+        for g in range(ring.depth):
+            ring.slots[g * B][0].wait_event(filled.cuda_event)
 
     class DeviceOps:
         """run_batch's actions on this GPU: HIP kernels through the C-ABI, RCCL collectives."""
@@ -471,6 +494,7 @@ def main():
                 d.present()
 
     timed_marks, timed_t0 = [], []  # per timed batch: run_batch's phase marks (HIP events) and its stream's t0
+    capturing_marks = []  # marks recorded while their stream was capturing a hipGraph (expected: none)
     ahead = set()  # slot groups whose prepass is queued ahead (plan.lookahead)
 
     def batch_step(n, timed=False, ahead_next=True):
@@ -480,6 +504,8 @@ def main():
             marks, stream = [], ops.b["stream"]
 
             def mark(name):
+                if stream_capturing(stream):
+                    capturing_marks.append((len(timed_marks) - 1, name))
                 ev = torch.cuda.Event(enable_timing=True)
                 ev.record(stream)
                 marks.append((name, ev))
@@ -503,6 +529,7 @@ def main():
         ev = torch.cuda.Event(enable_timing=True)
         ev.record(bufs[g]["stream"])
         t0_events.append(ev)
+    captures_before = sum(d.graph_info()[0] for d, _ in ring.slots)
     t0 = time.perf_counter()
     for i, n in enumerate(sizes):
         batch_step(n, timed=True, ahead_next=i + 1 < len(sizes))
@@ -511,6 +538,30 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    graph_captures_timed = sum(d.graph_info()[0] for d, _ in ring.slots) - captures_before
+    for d, _ in ring.slots:  # a dropped k_trace queue push (never expected) fails the run
+        d.check()
+
+    # this rank's phases of the timed batches (HIP events on each batch's stream, from the common
+    # start barrier), read NOW: the events were recorded on the ring's streams, and HIP's event
+    # queries look at the stream an event was recorded on -- read after ring.destroy() (as in round 3)
+    # they touched destroyed streams, the likely source of the hipErrorCapturedEvent seen at C1 / C5
+    # (no capture runs in the timed region: graph_captures_in_timed_region, marks_on_capturing_stream)
+    names = {id(ev): f"batch {b} mark '{nm}'" for b, mk in enumerate(timed_marks) for nm, ev in mk}
+    names.update({id(ev): f"t0 of slot group {g}" for g, ev in enumerate(t0_events)})
+
+    def event_ms(x, y):
+        """HIP event pair -> ms; a refused pair fails the run, naming the pair"""
+        try:
+            return x.elapsed_time(y)
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError(f"phase marks: HIP refused elapsed_time({names.get(id(x))} -> {names.get(id(y))}): "
+                               f"{e}; graph captures in the timed region: {graph_captures_timed}, marks recorded "
+                               f"on a capturing stream: {capturing_marks}") from e
+
+    phases = P.phase_summary(timed_marks, event_ms, t0=timed_t0)
+    capture_check = {"graph_captures_in_timed_region": graph_captures_timed,
+                     "marks_on_capturing_stream": len(capturing_marks)}
 
     progress(rank, f"timed done ({elapsed * 1e3:.1f} ms)")
     # the timed loop's own output: the first and last frame of its last batch (rank 0 holds every
@@ -698,18 +749,7 @@ def main():
             "how": f"the timed loop's {B}-frame batches back to back for ~{a.sustained_s:g} s "
                    f"({a.frames_in_flight} in flight), HIP event per batch; windows of ~1 s"}
 
-    # this rank's phases of the timed batches (HIP events on each batch's stream, from the common
-    # start barrier) and its tracescreen launch time; rank 0 reports every rank's (config.per_rank)
-    def event_ms(x, y):
-        """HIP event pair -> ms; None if HIP refuses the pair (the phase summary is diagnostic: it
-        must not end the run; the C1 config's events were refused once, hipErrorCapturedEvent)"""
-        try:
-            return x.elapsed_time(y)
-        except Exception as e:  # noqa: BLE001
-            progress(rank, f"phase marks: elapsed_time refused ({type(e).__name__}); phase left out")
-            return None
-
-    phases = P.phase_summary(timed_marks, event_ms, t0=timed_t0)
+    # this rank's tracescreen launch time with its phases; rank 0 reports every rank's (config.per_rank)
     phases.update({"rank": rank, "tracescreen_kernel_ms": round(k_avg_ms, 4)})
     per_rank = [phases]
     if world > 1:
@@ -769,6 +809,7 @@ def main():
                 # included), each batch's trace start from the common start barrier, and the rank's
                 # tracescreen launch (roofline pass); trace_start_skew_ms = per batch max - min over ranks
                 "per_rank": per_rank,
+                "timed_capture_check": capture_check,
                 **({"trace_start_skew_ms": P.start_skew(per_rank)} if world > 1 else {}),
                 **companions,
                 **({"verify": f"all {sizes[-1]} frames of the last timed batch equal a whole-frame render on one "

@@ -17,10 +17,8 @@ RT_OK = 0
 RT_DEVICE_FLOAT_OUTPUT = 1
 RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
-RT_DEVICE_SEG_TAIL_OFF = 8  # reserved since ABI 4 (no effect)
-RT_DEVICE_SEG_TAIL_ON = 16  # reserved since ABI 4 (no effect)
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
-ABI_VERSION = 5  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
+ABI_VERSION = 6  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -62,6 +60,9 @@ SIGNATURES = {
     "rt_device_set_profiling": (_i, [_vp, _i]),
     "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
+    "rt_device_wait_event": (_i, [_vp, _vp]),
+    "rt_device_record_event": (_i, [_vp, _vp]),
+    "rt_device_check": (_i, [_vp]),
     "rt_texture_create": (_i, [_vp, C.POINTER(_vp)]),
     "rt_texture_init": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i]),
     "rt_texture_destroy": (None, [_vp]),
@@ -125,13 +126,20 @@ def lib():
                 f"gpgpuraytrace_amd: native library missing at {LIB_PATH}; build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (make -C gpgpuraytrace_amd/csrc)")
         L = C.CDLL(LIB_PATH)
-        for name, (res, args) in SIGNATURES.items():
-            f = getattr(L, name)
-            f.restype = res
-            f.argtypes = args
+        # the version first: an older library lacks later exports, and binding those would fail
+        # with a bare AttributeError before this message could say what to do
+        L.rt_abi_version.restype, L.rt_abi_version.argtypes = _i, []
         if L.rt_abi_version() < ABI_VERSION:  # an older library: its structs are shorter than ours
             raise ImportError(f"gpgpuraytrace_amd: {LIB_PATH} has ABI {L.rt_abi_version()}, this binding "
                               f"needs >= {ABI_VERSION}; rebuild it (make -C gpgpuraytrace_amd/csrc)")
+        for name, (res, args) in SIGNATURES.items():
+            try:
+                f = getattr(L, name)
+            except AttributeError:
+                raise ImportError(f"gpgpuraytrace_amd: {LIB_PATH} does not export {name}; rebuild it "
+                                  "(make -C gpgpuraytrace_amd/csrc)") from None
+            f.restype = res
+            f.argtypes = args
         _lib = L
     return _lib
 

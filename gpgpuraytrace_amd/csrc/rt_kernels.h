@@ -5,9 +5,13 @@
 
 #include "rt_types.h"
 
-// work counters (one 64-byte block, zeroed by k_order before every k_trace)
+// work counters (one 64-byte block, zeroed by k_order before every k_trace), then the device's
+// sticky flags (zeroed at device creation and by rt_device_check only): a k_trace queue push that
+// would exceed its bound raises a flag instead of storing (rt_spill_caps)
 enum { RT_CTR_PRIMARY = 0 };
 #define RT_CTR_BYTES 64
+#define RT_QUEUE_BYTES 128
+enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u };
 
 // A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by
 // one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
@@ -41,6 +45,7 @@ struct RtLaunch {
     uint32_t hit_cap, long_spill_cap;
     int cells_from_cam;       // k_order derives CellDistance from CameraResults (setTargetDepths) first
     int small_rings;          // diagnostic (RT_DEVICE_DEBUG_SMALL_RINGS): k_trace's LDS long ring holds 64 entries, its fin pool 8
+    int fit;                  // hit pixels finish in k_trace (aa 1, <= 1 AO ray, no float output; UnitMap::fit)
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     float4* finpool;          // the same per block in a pool of RT_FIN_SLOTS slots of 3 float4 (fin is the fallback)
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word

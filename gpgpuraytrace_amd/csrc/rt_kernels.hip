@@ -20,6 +20,7 @@
 
 #include "rt_kernels.h"
 #include "rt_shader.h"
+#include "rt_variants.h"
 
 using namespace rts;
 using rtm::f3;
@@ -83,7 +84,7 @@ __device__ __forceinline__ Ctx make_ctx(const RtConsts* k, const uint32_t* lds)
     Ctx c;
     c.nz.img = reinterpret_cast<const char*>(lds);
     c.nz.oct = reinterpret_cast<const float4*>(lds + kOctBase);
-    c.nz.so16 = kLdsGxy | ((threadIdx.x & 15u) * 16u);
+    c.nz.so16 = kLdsGxy | ((threadIdx.x & (RT_LDS_SLOTS - 1u)) * 16u);
     c.nz.calls = 0;
     c.nz.lds_calls = nullptr;
     c.nz.phase = RT_PHASE_OTHER;
@@ -269,6 +270,10 @@ struct UnitMap {
     uint32_t frame_rot; // 1: frame f of a batch traces shard (tile_first + f) % tile_stride
     uint32_t order_batch; // k_order: 1 one longest-first order over the batch, 0 one per frame (frame-major)
     uint32_t cells_from_cam; // k_order first derives each frame's CellDistance from its CameraResults
+    // 1: one sample per pixel, no float output, <= 1 AO ray per hit: hit pixels are finished in k_trace
+    // where their last ray ends (fit_pixel), and k_finish only finishes the hits whose long shadow and
+    // AO ray race (their bit in hitmask); with no AO, no k_finish at all
+    uint32_t fit;
 };
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
@@ -450,10 +455,7 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
 constexpr uint32_t kShadowRec = 3;
 
 // Lanes idle before a long-ray wave refills them: amortises the refill's divergent
-// prologue against the idle lanes it leaves.
-#ifndef RT_REFILL_IDLE // A/B: make variant FLAGS=-DRT_REFILL_IDLE=n
-#define RT_REFILL_IDLE 4
-#endif
+// prologue against the idle lanes it leaves (knobs: rt_variants.h).
 constexpr uint32_t kRefillIdle = RT_REFILL_IDLE;
 
 // color.hlsl:53-71 after the shadow ray, then tracescreen.hlsl:33-35 fog and sky blends
@@ -584,6 +586,7 @@ __device__ __forceinline__ void per_frame(bool valid, uint32_t f_lane, Body body
 // every density sample) and its normalised SunDirection (a shadow ray's direction).
 struct FrameRays {
     float v[RT_MAX_BATCH][6];
+    uint32_t* out8[RT_MAX_BATCH]; // the frames' RGBA8 framebuffers (UnitMap::fit: pixels stored by long rays)
 };
 __device__ __forceinline__ void frame_rays_load(FrameRays& s, const FrameTable* __restrict__ ft, uint32_t n_frames)
 {
@@ -597,6 +600,7 @@ __device__ __forceinline__ void frame_rays_load(FrameRays& s, const FrameTable* 
         s.v[threadIdx.x][3] = sd.x;
         s.v[threadIdx.x][4] = sd.y;
         s.v[threadIdx.x][5] = sd.z;
+        s.out8[threadIdx.x] = ft->out8[threadIdx.x];
     }
 }
 
@@ -658,9 +662,12 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, fl
     return h;
 }
 
-// A long ray's `aux` word: an AO ray (kAuxAO), or a shadow ray whose finishing inputs (fin_store)
-// sit in its block's fin pool slot aux (< kFinSlots), or at fin[t] when the pool was empty (kAuxFinT).
-constexpr uint32_t kAuxAO = 0xffffffffu, kAuxFinT = 0xfffffffeu;
+// A long ray's `aux` word: an AO ray (sign bit set: kAuxAO, its occlusion counted in aocc for k_finish;
+// or, with UnitMap::fit, kAuxAOCand | rgb24 = its hit's pixel if the ray is occluded, stored where the
+// ray ends), or a shadow ray whose finishing inputs (fin_store) sit in its block's fin pool slot aux
+// (< kFinSlots), or at fin[t] when the pool was empty (kAuxFinT).
+constexpr uint32_t kAuxAO = 0xffffffffu, kAuxAOCand = 0x80000000u, kAuxFinT = 0x7ffffffeu;
+__device__ __forceinline__ bool aux_ao(uint32_t aux) { return (int32_t)aux < 0; }
 
 // Long-ray record (48 B): (p, dist), (step, aux, iters, t), (shadow fog | AO dir; a fog-free
 // landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
@@ -673,7 +680,7 @@ __device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, 
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
     r[1] = make_float4(st.step, __uint_as_float(aux), __uint_as_float((uint32_t)st.iters), __uint_as_float(t));
-    if (aux == kAuxAO) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
+    if (aux_ao(aux)) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
     else if constexpr (March<L, true>::FOG) r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
     // no fog: a shadow ray's f is +0 throughout (march_step), so r2 is neither written nor read
 }
@@ -689,7 +696,7 @@ __device__ __forceinline__ uint32_t long_unpack(const float4 r0, const float4 r1
     st.lastStep = 0.0f; // not read (SKIPREFINE)
     st.d = 0.0f;
     st.iters = (int)__float_as_uint(r1.z);
-    if (*aux == kAuxAO) {
+    if (aux_ao(*aux)) {
         st.dir = rtm::mk(r2.x, r2.y, r2.z);
         st.f = {0.0f, 0.0f, 0.0f, 0.0f};
         st.fog = false;
@@ -731,21 +738,45 @@ __device__ __forceinline__ void fin_store(float4* __restrict__ f, const ShadeHit
     }
 }
 
-// A long ray left its loop: a shadow ray finishes its sample from its fin record; an AO ray
-// counts its occlusion for k_finish.
-template <int L>
-__device__ __forceinline__ void long_finish(const RtConsts* k, const float4* __restrict__ fin,
-                                            const float4* __restrict__ finp, float4* __restrict__ samples,
-                                            uint32_t* __restrict__ aocc, uint32_t t, uint32_t aux,
-                                            const March<L, true>& st)
+// UnitMap::fit: k_finish's arithmetic for a pixel of one sample, (0 + v * ao) * rcp(1) per channel, as
+// UNORM8 (tracescreen.hlsl:67-75 with AA_SAMPLES 1), where the hit's last ray ends
+__device__ __forceinline__ uint32_t fit_pixel(float4 v, float ao)
 {
-    if (aux == kAuxAO) {
-        if (st.d > 0.0f) ao_count(aocc, t);
+    const float ia = rtm::rcp(1.0f);
+    return unorm8((0.0f + v.x * ao) * ia) | (unorm8((0.0f + v.y * ao) * ia) << 8) |
+           (unorm8((0.0f + v.z * ao) * ia) << 16) | 0xff000000u;
+}
+
+// UnitMap::fit: store the final pixel of sample t (one sample per pixel) from a lane of any frame
+__device__ __forceinline__ void fit_store(const RtConsts* k, const UnitMap& m, const FrameRays& fr, uint32_t t,
+                                          uint32_t px8)
+{
+    const uint32_t f = frame_of(m, t), W = (uint32_t)k->width;
+    uint32_t px, py;
+    unit_pixel(m, f, (t - f * m.frame_samples) >> 6, t & 63u, W, (uint32_t)k->height, &px, &py);
+    gptr(fr.out8[f])[(size_t)late(py) * W + px] = px8;
+}
+
+// A long ray left its loop: a shadow ray finishes its sample from its fin record (with fit and no AO,
+// its pixel); an AO ray counts its occlusion for k_finish, or (fit) stores its hit's occluded pixel.
+template <int L>
+__device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m, const FrameRays& fr,
+                                            const float4* __restrict__ fin, const float4* __restrict__ finp,
+                                            float4* __restrict__ samples, uint32_t* __restrict__ aocc, uint32_t t,
+                                            uint32_t aux, const March<L, true>& st)
+{
+    if (aux_ao(aux)) {
+        if (st.d > 0.0f) {
+            if (aux == kAuxAO) ao_count(aocc, t);
+            else fit_store(k, m, fr, t, aux | 0xff000000u);
+        }
     } else {
         constexpr uint32_t FR = FinRec<L>::N;
         const float4* f = aux == kAuxFinT ? fin + (size_t)FR * t : finp + (size_t)FR * aux;
         const float4 fog = FogLive<L>::value ? ld_fresh(f + 1) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        sample_store(k, samples, t, shade_finish(k, ld_fresh(f), fog, ld_fresh(f + FR - 1u), st.d, st.f.w));
+        const float4 v = shade_finish(k, ld_fresh(f), fog, ld_fresh(f + FR - 1u), st.d, st.f.w);
+        if (m.fit && k->ao_samples == 0) fit_store(k, m, fr, t, fit_pixel(v, 1.0f));
+        else sample_store(k, samples, t, v);
     }
 }
 
@@ -772,42 +803,20 @@ constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 Ki
 // are the same lines over and over and stay in the XCD's L2 (fin[t] instead: a sparse write and a
 // re-fetch per long shadow).  An empty pool falls back to fin[t].
 constexpr uint32_t kFinSlots = RT_FIN_SLOTS;
-#ifndef RT_LONG_BATCH // A/B: make variant FLAGS=-DRT_LONG_BATCH=n
-#define RT_LONG_BATCH 128
-#endif
 constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a wave switch to them
-#ifndef RT_COMPACT_LIVE // A/B: make variant FLAGS=-DRT_COMPACT_LIVE=n
-#define RT_COMPACT_LIVE 56
-#endif
 constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
 // After the unit queue drains (nomadplains): a long-ray wave left with at most kSegHandBack live rays
 // and an empty ring hands them back, and a wave that finds at most kSegQueue rays queued marches them
 // as segments of kSegLanes lanes per ray (density_nomadplains_seg: the octaves spread over the
 // segment), cutting the per-step latency that sets a launch's last few hundred microseconds.
-#ifndef RT_SEG_LANES // A/B: make variant FLAGS=-DRT_SEG_LANES=n (0: off)
-#define RT_SEG_LANES 8
-#endif
-#ifndef RT_SEG_HANDBACK
-#define RT_SEG_HANDBACK 16
-#endif
-#ifndef RT_SEG_QUEUE
-#define RT_SEG_QUEUE 64
-#endif
 constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSegQueue = RT_SEG_QUEUE;
 // A primary unit's last few rays (nomadplains): once at most kPrimarySeg rays of an 8x8 unit are
 // still marching, they continue as segments of 64 / kPrimarySeg lanes per ray (primary_seg in
 // k_trace) instead of keeping 64 lanes on a few rays' octave loops.  0: off.
-#ifndef RT_PRIMARY_SEG // A/B: make variant FLAGS=-DRT_PRIMARY_SEG=n (0, 4, 8 or 16)
-#define RT_PRIMARY_SEG 8
-#endif
 constexpr uint32_t kPrimarySeg = RT_PRIMARY_SEG;
 static_assert(kPrimarySeg == 0u || kPrimarySeg == 4u || kPrimarySeg == 8u || kPrimarySeg == 16u, "lanes per ray");
-// The instrumented (STATS) kernels march a unit's last rays on 64 lanes: the counters would cost the
-// segment's registers (spills).  A diagnostic build (-DRT_STATS_PRIMARY_SEG=1, it spills) counts the
-// product's segment tail to measure its noise lane utilisation.
-#ifndef RT_STATS_PRIMARY_SEG
-#define RT_STATS_PRIMARY_SEG 0
-#endif
+// The instrumented (STATS) kernels take the same segment tail (their counters cost registers there:
+// they spill, the product does not), so their march and noise counts pass through the product's code.
 constexpr bool kStatsPrimarySeg = RT_STATS_PRIMARY_SEG != 0;
 
 // STATS kernels: a k_trace block's march-step and hit counters (LDS atomics; the block's last wave
@@ -825,8 +834,14 @@ struct TraceQueues {
     uint32_t active;  // waves inside a primary unit or a shading batch (they may still push)
     uint32_t drained; // the global unit queue is exhausted
     uint32_t pad;
-    uint32_t ls_head, ls_tail; // the block's long-ray spill ring (HBM)
-    uint32_t f_top, pad2;      // free slots of the block's fin pool: fin_free[0, f_top)
+    union { // the block's long-ray spill ring (HBM)
+        struct {
+            uint32_t ls_head, ls_tail;
+        };
+        uint64_t ls_ht;
+    };
+    uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
+    uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
 };
@@ -857,30 +872,14 @@ __device__ __forceinline__ void q_unlock(uint32_t* lock, uint32_t lane)
     if (lane == 0) atomicExch(lock, 0u);
 }
 
-// Debug build only (make trace, -DRT_WAVE_TRACE): per-wave timeline of k_trace for
-// scheduler studies (scripts/wave_trace.py).  RT_WT_FIELDS u64 per wave slot.
-#ifdef RT_LIVE_HIST
-__device__ unsigned long long g_live_hist[65];
-#endif
-
-#ifdef RT_WAVE_TRACE
-#define RT_WT_FIELDS 21
-#define RT_WT_MAX_WAVES 8192
-__device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];
-#define WT(...) __VA_ARGS__
-#else
-#define WT(...)
-#endif
+// Diagnostic builds only (rt_variants.h): the live-lane histogram and k_trace's per-wave timeline
+// (RT_WT_FIELDS u64 per wave slot, scripts/wave_trace.py).
+RT_DIAG_LIVE_HIST(__device__ unsigned long long g_live_hist[65];)
+WT(__device__ unsigned long long g_wave_trace[RT_WT_MAX_WAVES * RT_WT_FIELDS];)
 
 // k_trace's block: 16 waves (4 per SIMD, 128 VGPRs each) for the fog-free landscapes; the fog-live
 // one (greenrocks: fog state in every march and record) and simple (its two-plane density) need
 // more than 128 VGPRs and run 12 waves (3 per SIMD, up to 168 VGPRs) instead of spilling.
-#ifndef RT_TRACE_WAVES_FAST // A/B: make variant FLAGS=-DRT_TRACE_WAVES_FAST=12
-#define RT_TRACE_WAVES_FAST 16
-#endif
-#ifndef RT_TRACE_WAVES_WIDE // A/B: make variant FLAGS=-DRT_TRACE_WAVES_WIDE=16
-#define RT_TRACE_WAVES_WIDE 12
-#endif
 template <int L>
 struct TraceThreads {
     static constexpr uint32_t value = 64u * ((L == RT_GREENROCKS || L == RT_SIMPLE) ? RT_TRACE_WAVES_WIDE : RT_TRACE_WAVES_FAST);
@@ -917,6 +916,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.drained = 0;
         q.ls_head = q.ls_tail = 0;
         q.f_top = fin_slots;
+        q.overflow = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
@@ -955,10 +955,17 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
         } else {
-            const uint32_t stl = vload(q.ls_tail);
-            if (want) long_pack(st, t, aux, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
+            // the spill ring's bound (rt_spill_caps) holds by the work priorities; a push past it is
+            // dropped and flagged (rt_device_check), never written over queued rays
+            const uint64_t ht = vload(q.ls_ht); // (tail << 32) | head, one LDS read
+            const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ht >> 32));
+            const bool fits = stl - (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ht) + n <= long_spill_cap;
+            if (want && fits) long_pack(st, t, aux, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
             __builtin_amdgcn_s_waitcnt(0);
-            if (lane == 0) q.ls_tail = stl + n;
+            if (lane == 0) {
+                q.ls_tail = fits ? stl + n : stl;
+                q.overflow |= fits ? 0u : RT_FLAG_SPILL_OVERFLOW;
+            }
         }
         q_unlock(&q.lock, lane);
     };
@@ -987,11 +994,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
-            if (live && !march_live<L, true, true>(cl, st, aux == kAuxAO ? RT_AO_END : 100.0f, 0)) {
-                long_finish<L>(k, fin, finp, samples, aocc, t, aux, st);
+            if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
+                long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 live = false;
-                stat(aux == kAuxAO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -1009,7 +1016,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
                     const float* fr = s_fr.v[frame_of(m, t)];
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
-                    if (aux != kAuxAO) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                    if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     live = true;
                 };
                 if (mine && rank < take) {
@@ -1044,14 +1051,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 c.nz.calls = cl.nz.calls;
                 return;
             }
-#ifdef RT_COUNT_LONG_STEPS // diagnostic build: live lanes per long-ray march step (scripts/phase_util.py);
-                             // 2: only while the unit queue is drained, 3: only before
-            if (live && (RT_COUNT_LONG_STEPS == 1 || (RT_COUNT_LONG_STEPS == 2) == (vload(q.drained) != 0u))) {
+            RT_DIAG_LONG_STEPS(if (live && (RT_COUNT_LONG_STEPS == 1 || (RT_COUNT_LONG_STEPS == 2) == (vload(q.drained) != 0u))) {
                 cl.nz.phase = RT_COUNT_PHASE;
                 count_noise(cl.nz);
                 cl.nz.phase = RT_PHASE_LONG;
-            }
-#endif
+            })
             if (live) march_step<L, true, true>(cl, st);
         }
     };
@@ -1092,7 +1096,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
                 const float* fr = s_fr.v[frame_of(m, t)];
                 cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
-                if (aux != kAuxAO) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                 live = true;
             }
             __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
@@ -1103,10 +1107,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             q_unlock(&q.lock, lane);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
             for (;;) {
-                if (live && !march_live<L, true, true>(cl, st, aux == kAuxAO ? RT_AO_END : 100.0f, 0)) {
+                if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
                     if (j == 0u) {
-                        long_finish<L>(k, fin, finp, samples, aocc, t, aux, st);
-                        stat(aux == kAuxAO ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                        long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
+                        stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
                     }
                     live = false;
                 }
@@ -1175,7 +1179,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     auto dens = [&](f3 q0) {
                         uint32_t used;
                         const float d = density_nomadplains_seg<LPR, true>(cf, g, q0, j, base, &used);
-                        if constexpr (STATS) { // diagnostic build only (kStatsPrimarySeg): density_nomadplains' count
+                        if constexpr (STATS) { // the same noise count as density_nomadplains: octaves + steep noise
                             if (j == 0u) atomicAdd(&s_st.v[BlockStats::NOISE], (unsigned long long)(used + 1u));
                             if (lane == (uint32_t)__builtin_ctzll(__ballot(1)))
                                 atomicAdd(&s_st.v[BlockStats::NOISE_WAVES], (unsigned long long)SegOctaves<LPR>::R);
@@ -1228,6 +1232,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         March<L, true> st;
         bool more = false;
         uint32_t aux = kAuxAO;
+        uint32_t ao_aux = kAuxAO; // the hit's AO ray: counted (kAuxAO) or carrying its occluded pixel (fit)
         const bool valid = lane < take;
         ShadeHit h;
         per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
@@ -1237,7 +1242,15 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             c.nz.calls = cf.nz.calls;
             more = h.more;
             if (!more) {
-                sample_store(k, samples, t, shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w));
+                const float4 v = shade_finish(k, h.cb, h.fog, h.ray, st.d, st.f.w);
+                if (m.fit) {
+                    // the pixel is final now (no AO), or its unoccluded value is (ao_factor(0, 1) = 1) and
+                    // the AO ray carries the occluded one (ao_factor(1, 1)); no sample, no k_finish
+                    gptr(ft->out8[f])[(size_t)late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
+                    if (k->ao_samples) ao_aux = kAuxAOCand | (fit_pixel(v, ao_factor(1u, 1)) & 0xffffffu);
+                } else {
+                    sample_store(k, samples, t, v);
+                }
                 stat(BlockStats::SHADOW, (uint32_t)st.iters);
             }
             // the long shadows' finishing inputs: a fin pool slot each (this frame's lanes are the
@@ -1254,15 +1267,20 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (more) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
             }
         });
+        // fit with AO: the hits whose long shadow races their AO ray are k_finish's (their bit in the
+        // unit's hitmask word t >> 6, zero from the unit)
+        if (m.fit && k->ao_samples && valid && more) atomicOr((unsigned long long*)&hitmask[t >> 6], 1ull << (t & 63u));
         if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // the fin record is in L2 before the ray is visible
             push_long(more, st, t, aux);
         }
-        // AO extension: the hit's AO rays start as long rays
+        // AO extension: the hit's AO rays start as long rays (fit: after its unoccluded pixel is stored,
+        // which an occluded AO ray overwrites)
+        if (m.fit) __builtin_amdgcn_s_waitcnt(0);
         for (int kk = 0; kk < k->ao_samples; ++kk) {
             March<L, true> ao;
             if (valid) ao_begin(c, h, (uint32_t)kk, ao);
-            push_long(valid, ao, t, kAuxAO);
+            push_long(valid, ao, t, ao_aux);
         }
     };
 
@@ -1294,17 +1312,12 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 lv = lv && march_live<L, true, false>(cf, st, RT_CAMERA_FAR, max_steps);
                 const uint64_t lb = __ballot(lv);
                 if (lb == 0ull) break;
-#ifdef RT_LIVE_HIST // diagnostic build: histogram of live lanes per primary march step (rt_debug_live_hist)
-                if (lane == (uint32_t)__builtin_ctzll(__ballot(1)))
-                    atomicAdd(&g_live_hist[__popcll(lb)], 1ull);
-#endif
-#ifdef RT_COUNT_PRIMARY_STEPS // diagnostic build: live lanes per primary march step (scripts/phase_util.py)
-                if (lv) {
+                RT_DIAG_LIVE_HIST(if (lane == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(&g_live_hist[__popcll(lb)], 1ull);)
+                RT_DIAG_PRIMARY_STEPS(if (lv) {
                     cf.nz.phase = RT_COUNT_PHASE;
                     count_noise(cf.nz);
                     cf.nz.phase = RT_PHASE_PRIMARY;
-                }
-#endif
+                })
                 if constexpr (L == RT_NOMADPLAINS && kPrimarySeg > 0u && (!STATS || kStatsPrimarySeg)) {
                     if ((uint32_t)__popcll(lb) <= kPrimarySeg) {
                         primary_seg(cf, st, lv, lb, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1]);
@@ -1335,19 +1348,24 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 }
             }
             const uint64_t hb = __ballot(hit);
-            if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = hb; // k_finish skips the misses
+            // k_finish skips the misses; with fit it finishes only the hits the shading marks
+            if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = m.fit ? 0ull : hb;
             if (hb) {
                 // the hits' records go on the block's hit stack in rank order (dense lines), stored
-                // before the top publishes them.  The stack never overflows: a wave starts a unit
+                // before the top publishes them.  The stack does not overflow: a wave starts a unit
                 // only while fewer than 64 hits are queued, so at most 63 + 16 waves x 64 x aa are
-                // (rt_spill_caps' hit_cap).
+                // (rt_spill_caps' hit_cap); a push past it is dropped and flagged (rt_device_check).
                 const uint32_t n = (uint32_t)__popcll(hb), rank = lane_rank(hb);
                 if (hit) stat(BlockStats::HITS, 1u);
                 q_lock(&q.lock, lane);
                 const uint32_t top = vload(q.h_top);
-                if (hit) hit_store<L>(hq + (size_t)(top + rank) * HR, t, rr);
+                const bool fits = (uint32_t)__builtin_amdgcn_readfirstlane(top) + n <= hit_cap;
+                if (hit && fits) hit_store<L>(hq + (size_t)(top + rank) * HR, t, rr);
                 __builtin_amdgcn_s_waitcnt(0);
-                if (lane == 0) q.h_top = top + n;
+                if (lane == 0) {
+                    if (fits) q.h_top = top + n;
+                    else q.overflow |= RT_FLAG_HIT_OVERFLOW;
+                }
                 q_unlock(&q.lock, lane);
             }
         }
@@ -1359,6 +1377,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // SIMD instead of filling the first few CUs' SIMDs four deep, which sets the frame time
     // when there are barely more units than waves (an 8-way shard has ~4k units for 4k waves).
     const uint32_t n_static = gridDim.x * (blockDim.x >> 6);
+    const uint32_t first_qi = first_unit_index(); // scalar, formed before the loop
     bool first_unit = true;
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
@@ -1388,7 +1407,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
         if (!drained || first_unit) { // a wave's static first unit is taken even after the queue drained
             if (lane == 0) atomicAdd(&q.active, 1u);
-            const uint32_t qi = first_unit ? first_unit_index() : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+            const uint32_t qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
             first_unit = false;
             if (qi < m.n_units * m.n_frames) {
                 // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
@@ -1403,6 +1422,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) break;
         __builtin_amdgcn_s_sleep(2);
         WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
+    }
+    // a dropped push (never, by rt_spill_caps' bound) becomes the device's sticky flag (rt_device_check)
+    if (lane == 0) {
+        const uint32_t ov = vload(q.overflow);
+        if (ov) atomicOr(counters + RT_CTR_BYTES / 4, ov);
     }
     WT(wt[1] = __builtin_amdgcn_s_memrealtime();
        for (int o = 32; o >= 1; o >>= 1) {
@@ -1615,15 +1639,13 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
-#ifdef RT_ORDER_BATCH // A/B: force the batch-wide (1) or the frame-major (0) unit order
-    m.order_batch = RT_ORDER_BATCH;
-#else
-    m.order_batch = m.n_frames > 1u && m.n_units < kOrderBatchUnitsPerWave * pblocks * 16u;
-#endif
+    m.order_batch = RT_ORDER_BATCH >= 0 ? (uint32_t)RT_ORDER_BATCH
+                                        : (uint32_t)(m.n_frames > 1u && m.n_units < kOrderBatchUnitsPerWave * pblocks * 16u);
     // k_finish holds no LDS: up to 2 blocks per CU
     uint32_t fblocks = need < 2u * blocks ? need : 2u * blocks;
     dim3 blk(1024);
     m.cells_from_cam = (uint32_t)a.cells_from_cam;
+    m.fit = (uint32_t)a.fit;
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
@@ -1636,7 +1658,9 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
                            a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots);
-        hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
+        // fit without AO: every hit pixel is final in k_trace
+        if (!(m.fit && a.ao_samples == 0))
+            hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});
     else primary(std::false_type{});

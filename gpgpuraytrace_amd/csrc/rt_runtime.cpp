@@ -151,6 +151,10 @@ struct rt_device_s {
     hipEvent_t ev_order = nullptr, ev_ahead = nullptr;
     bool order_recorded = false, ahead_pending = false;
     std::vector<const void*> ahead_cams;
+    // every device whose frames a pending ahead prepass writes (the lead included): its CameraResults
+    // are not read -- by a render this device leads, or a map -- before ev_ahead_in
+    hipEvent_t ev_ahead_in = nullptr;
+    bool ahead_in_pending = false;
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -164,6 +168,17 @@ static int recorder_capture(rt_recorder r);
 static void recorder_detach(rt_recorder r);
 
 namespace {
+// Work on stream s that touches device d's frames (their CameraResults) comes after a pending ahead
+// prepass that writes them (rt_terrain_prepass_ahead, on the GPU's side stream).
+int ahead_wait(rt_device_s* d, hipStream_t s)
+{
+    if (!d->ahead_in_pending) return 0;
+    const hipError_t e = hipStreamWaitEvent(s, d->ev_ahead_in, 0);
+    if (e != hipSuccess) return (int)e;
+    d->ahead_in_pending = false;
+    return 0;
+}
+
 // bracket one tracescreen launch with a pair of events when profiling is on
 struct KernelTimer {
     rt_device_s* d;
@@ -460,6 +475,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     rt_spill_caps(s->aa, s->ao, &a.hit_cap, &a.long_spill_cap);
     a.cells_from_cam = 0;
     a.small_rings = (dev->flags & RT_DEVICE_DEBUG_SMALL_RINGS) ? 1 : 0;
+    a.fit = 0;
     a.fin = dev->fin;
     a.finpool = dev->finpool;
     a.aocc = dev->aocc;
@@ -636,7 +652,7 @@ rt_device_s::~rt_device_s()
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
     if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
-    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead})
+    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in})
         if (e) (void)hipEventDestroy(e);
     for (auto& pr : ev_pool) {
         (void)hipEventDestroy(pr.first);
@@ -650,8 +666,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
 {
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
-    if ((flags & RT_DEVICE_SEG_TAIL_OFF) && (flags & RT_DEVICE_SEG_TAIL_ON))
-        return fail(RT_ERR_INVALID, "RT_DEVICE_SEG_TAIL_OFF and RT_DEVICE_SEG_TAIL_ON are exclusive");
+    const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS;
+    if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (ordinal < 0 || ordinal >= n) return fail(RT_ERR_INVALID, "GPU ordinal %d out of range (%d devices)", ordinal, n);
@@ -677,7 +693,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMalloc(&d->stats, sizeof(RtStats)));
     HIP_TRY(hipMemset(d->stats, 0, sizeof(RtStats)));
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
-    HIP_TRY(hipMalloc(&d->queue, RT_CTR_BYTES));
+    HIP_TRY(hipMalloc(&d->queue, RT_QUEUE_BYTES));
+    HIP_TRY(hipMemset(d->queue, 0, RT_QUEUE_BYTES)); // the counters are reset per launch, the flags here
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
     return RT_OK;
@@ -832,6 +849,35 @@ int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned lon
 }
 
 // ---- textures -------------------------------------------------------------
+int rt_device_wait_event(rt_device d, void* ev)
+{
+    if (!d || !ev) return fail(RT_ERR_INVALID, "null device or event");
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipStreamWaitEvent(d->stream, (hipEvent_t)ev, 0));
+    return RT_OK;
+}
+
+int rt_device_record_event(rt_device d, void* ev)
+{
+    if (!d || !ev) return fail(RT_ERR_INVALID, "null device or event");
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipEventRecord((hipEvent_t)ev, d->stream));
+    return RT_OK;
+}
+
+int rt_device_check(rt_device d)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    HIP_TRY(hipSetDevice(d->ordinal));
+    HIP_TRY(hipStreamSynchronize(d->stream));
+    uint32_t flags = 0;
+    HIP_TRY(hipMemcpy(&flags, reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 4, hipMemcpyDeviceToHost));
+    if (!flags) return RT_OK;
+    HIP_TRY(hipMemset(reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 0, 4));
+    return fail(RT_ERR_STATE, "k_trace queue overflow:%s%s (a push past rt_spill_caps' bound was dropped)",
+                (flags & RT_FLAG_HIT_OVERFLOW) ? " hit stack" : "", (flags & RT_FLAG_SPILL_OVERFLOW) ? " long-ray spill ring" : "");
+}
+
 int rt_texture_create(rt_device d, rt_texture* out)
 {
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
@@ -1100,7 +1146,8 @@ void* rt_array_map(rt_array a)
         return nullptr;
     }
     hipStream_t s = a->dev->stream;
-    if (hipMemcpyAsync(a->host.data(), a->dev_ptr, a->host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
+    if (ahead_wait(a->dev, s) != 0 ||
+        hipMemcpyAsync(a->host.data(), a->dev_ptr, a->host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
         hipStreamSynchronize(s) != hipSuccess) {
         fail(RT_ERR_HIP, "map readback failed");
         return nullptr;
@@ -1163,7 +1210,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.hitq,
                           (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_cap, (uint64_t)a.long_spill_cap,
-                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool,
+                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)a.fit, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));
@@ -1307,6 +1354,17 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
 {
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
     if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
+    if (cams && scrs && n >= 1 && n <= RT_MAX_BATCH && scrs[0] && scrs[0]->dev) {
+        // a pending ahead prepass writes these frames' CameraResults: it comes before anything this
+        // call queues, the constant uploads of batch_begin included (they rewrite the block the
+        // side-stream prepass reads)
+        rt_device lead = scrs[0]->dev;
+        for (int f = 0; f < n; ++f)
+            if (scrs[f] && scrs[f]->dev && ahead_wait(scrs[f]->dev, lead->stream) != 0)
+                return fail(RT_ERR_HIP, "waiting for the ahead prepass failed");
+        // a full render prepasses in line: the lead's pending ahead prepass is superseded
+        if (lead->ahead_pending && phases != PH_PRE) lead->ahead_pending = false;
+    }
     int rc;
     Batch b;
     if ((rc = batch_begin(cams, scrs, n, b, (phases & PH_PRE) != 0, (phases & PH_TRACE) != 0))) return rc;
@@ -1326,11 +1384,6 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             if (ft.cam[f] != scrs[f]->dev->scratch_cam) cam_copy[f] = ft.cam[f];
             ft.cam[f] = const_cast<float4*>(src);
         }
-    }
-    if (dev->ahead_pending) {
-        // an ahead prepass of this device's batches writes CameraResults: it comes first
-        HIP_TRY(hipStreamWaitEvent(dev->stream, dev->ev_ahead, 0));
-        dev->ahead_pending = false;
     }
     if (phases == PH_PRE) {
         // the prepass of frames [first, first + count) only, on its own table
@@ -1361,6 +1414,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
     // setTargetDepths runs at the start of the tracescreen launch (k_order), from the CameraResults
     la_scr.cells_from_cam = 1;
+    // one sample per pixel, at most one AO ray and no float output: hit pixels finish where their last
+    // ray ends (k_trace), not through a per-sample colour and k_finish
+    la_scr.fit = b.s0->aa == 1 && b.s0->ao <= 1;
+    for (int f = 0; f < n; ++f) la_scr.fit = la_scr.fit && ft.out32[f] == nullptr;
     auto pre = [&] {
         if (phases & PH_PRE) rt_launch_camerarays_batch(la_cam);
     };
@@ -1466,6 +1523,12 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
     if (rc) return rc;
     HIP_TRY(hipEventRecord(lead->ev_ahead, side));
     lead->ahead_pending = true;
+    for (auto& p : saved) { // every device whose frames it wrote (not the lead alone)
+        rt_device d = p.first;
+        if (!d->ev_ahead_in) HIP_TRY(hipEventCreateWithFlags(&d->ev_ahead_in, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(d->ev_ahead_in, side));
+        d->ahead_in_pending = true;
+    }
     lead->ahead_cams.assign(cams, cams + n);
     return RT_OK;
 }

@@ -1,0 +1,91 @@
+// rt_variants.h -- compile-time knobs and diagnostic hooks of the trace kernels.
+//
+// The product build takes every default below.  A/B builds override a knob on the compiler line
+// (`make -C gpgpuraytrace_amd/csrc variant NAME=x FLAGS="-DRT_LONG_BATCH=96"`, loaded by
+// scripts/with_variant.py); diagnostic builds define one of the RT_DIAG_* switches at the end.  The
+// kernel source (rt_kernels.hip) only names the constants and the one-line hooks, so the hot file
+// reads as the product.  DESIGN.md sections 4-5 record what each knob measured.
+#pragma once
+
+// ---- k_trace's scheduler ----------------------------------------------------------------------
+// lanes idle before a long-ray wave refills them from the ring (amortises the refill's prologue)
+#ifndef RT_REFILL_IDLE
+#define RT_REFILL_IDLE 4
+#endif
+// queued long rays that make a wave switch to them
+#ifndef RT_LONG_BATCH
+#define RT_LONG_BATCH 128
+#endif
+// live lanes below which a long-ray wave whose ring ran dry hands its rays back
+#ifndef RT_COMPACT_LIVE
+#define RT_COMPACT_LIVE 56
+#endif
+// after the unit queue drains (nomadplains): a long-ray wave with <= RT_SEG_HANDBACK live rays and an
+// empty ring hands them back; a wave that finds <= RT_SEG_QUEUE queued marches them as segments of
+// RT_SEG_LANES lanes per ray (0: off)
+#ifndef RT_SEG_LANES
+#define RT_SEG_LANES 8
+#endif
+#ifndef RT_SEG_HANDBACK
+#define RT_SEG_HANDBACK 16
+#endif
+#ifndef RT_SEG_QUEUE
+#define RT_SEG_QUEUE 64
+#endif
+// a primary unit's last <= RT_PRIMARY_SEG rays march on 64 / RT_PRIMARY_SEG lanes each (0, 4, 8, 16)
+#ifndef RT_PRIMARY_SEG
+#define RT_PRIMARY_SEG 8
+#endif
+// the instrumented (STATS) kernels take the product's primary segment tail too (1), so their march and
+// noise counts are asserted through the timed kernel's code path; 0 keeps a 64-lane tail there
+#ifndef RT_STATS_PRIMARY_SEG
+#define RT_STATS_PRIMARY_SEG 1
+#endif
+// waves per k_trace block: 16 for the landscapes that fit 128 VGPRs, 12 for simple / greenrocks
+#ifndef RT_TRACE_WAVES_FAST
+#define RT_TRACE_WAVES_FAST 16
+#endif
+#ifndef RT_TRACE_WAVES_WIDE
+#define RT_TRACE_WAVES_WIDE 12
+#endif
+// lane slots of the LDS gradient planes (rt_shader.h NoiseView): 16 makes the gxy ds_read_b128 reads
+// conflict-free and the gz ds_read_b64 reads 2-way; 8 / 4 (every slot holds the same data, so the
+// results are the same bits) double / quadruple both -- the A/B that prices the LDS bank conflicts
+#ifndef RT_LDS_SLOTS
+#define RT_LDS_SLOTS 16
+#endif
+// k_order: RT_ORDER_BATCH forces the batch-wide (1) or frame-major (0) unit order; -1 = automatic
+// (batch-wide below kOrderBatchUnitsPerWave units per wave slot)
+#ifndef RT_ORDER_BATCH
+#define RT_ORDER_BATCH -1
+#endif
+
+// ---- diagnostic builds (never in the product) ------------------------------------------------
+// RT_WAVE_TRACE          per-wave timeline of k_trace (make trace; scripts/wave_trace.py)
+// RT_LIVE_HIST           histogram of live lanes per primary march step (rt_debug_live_hist)
+// RT_COUNT_PRIMARY_STEPS count live lanes per primary march step as noise (scripts/phase_util.py)
+// RT_COUNT_LONG_STEPS=k  the same for long-ray steps (1 always, 2 after the drain, 3 before)
+// RT_COUNT_PHASE=k       count only the noise of k_trace work kind k (rt_shader.h count_noise)
+// RT_EXTRA_OCTAVE=n      n dead octaves per nomadplains density sample (issue-cost experiment)
+#ifdef RT_WAVE_TRACE
+#define RT_WT_FIELDS 21
+#define RT_WT_MAX_WAVES 8192
+#define WT(...) __VA_ARGS__
+#else
+#define WT(...)
+#endif
+#ifdef RT_LIVE_HIST
+#define RT_DIAG_LIVE_HIST(...) __VA_ARGS__
+#else
+#define RT_DIAG_LIVE_HIST(...)
+#endif
+#ifdef RT_COUNT_PRIMARY_STEPS
+#define RT_DIAG_PRIMARY_STEPS(...) __VA_ARGS__
+#else
+#define RT_DIAG_PRIMARY_STEPS(...)
+#endif
+#ifdef RT_COUNT_LONG_STEPS
+#define RT_DIAG_LONG_STEPS(...) __VA_ARGS__
+#else
+#define RT_DIAG_LONG_STEPS(...)
+#endif

@@ -220,6 +220,21 @@ class Device:
         check(lib().rt_device_graph_info(self._h, C.byref(cap), C.byref(lau)), "graph_info")
         return int(cap.value), int(lau.value)
 
+    def wait_event(self, hip_event):
+        """rt_device_wait_event (ABI 6): the device's later work waits for `hip_event` (a hipEvent_t
+        handle, e.g. torch.cuda.Event.cuda_event recorded after the caller's fills on its stream)."""
+        check(lib().rt_device_wait_event(self._h, int(hip_event)), "wait_event")
+
+    def record_event(self, hip_event):
+        """rt_device_record_event (ABI 6): record `hip_event` after the device's queued work (the
+        caller's stream then waits for it before reading the device's outputs)."""
+        check(lib().rt_device_record_event(self._h, int(hip_event)), "record_event")
+
+    def check(self):
+        """rt_device_check (ABI 6): synchronise and raise NativeError if a k_trace queue push was
+        dropped at its bound since the last check (never expected: rt_spill_caps)."""
+        check(lib().rt_device_check(self._h), "device check")
+
     def framebuffer_pointer(self):
         return lib().rt_device_framebuffer(self._h)
 

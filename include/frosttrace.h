@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 enum {
     RT_OK = 0,
@@ -45,16 +45,14 @@ enum {
     RT_DEVICE_FLOAT_OUTPUT = 1u,
     RT_DEVICE_STATS = 2u,
     RT_DEVICE_GRAPH = 4u,
-    RT_DEVICE_SEG_TAIL_OFF = 8u,
-    RT_DEVICE_SEG_TAIL_ON = 16u,
+    /* 8u, 16u: retired in ABI 6 (ABI <= 5 RT_DEVICE_SEG_TAIL_OFF / _ON, no effect since ABI 4);
+     * rt_device_create rejects them, as every unknown flag */
     RT_DEVICE_DEBUG_SMALL_RINGS = 32u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
  * every frame; a changed launch argument (shader swap, buffers, shard, stats) re-captures.
  * No reference counterpart (the D3D frame loop re-records its dispatches every frame).
- * RT_DEVICE_SEG_TAIL_OFF / _ON: reserved (ABI <= 3 selected a trace-kernel tail variant that
- * ABI 4 removed; both are accepted and have no effect).  Setting both fails with RT_ERR_INVALID.
  * RT_DEVICE_DEBUG_SMALL_RINGS (ABI 4, diagnostic): the trace kernel's per-CU LDS long-ray ring holds
  * 64 entries instead of 570 and its fin pool 8 slots instead of 1536, so queued long rays take the
  * per-block spill rings in HBM and most long shadows the fin[t] fallback (the parity tests run
@@ -132,6 +130,23 @@ int rt_device_set_profiling(rt_device dev, int enable);
 int rt_device_kernel_time(rt_device dev, double* total_ms, int* launches);
 /* RT_DEVICE_GRAPH bookkeeping: graphs captured and graph launches since device creation. */
 int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned long long* launches);
+/* (ABI 6) Stream handoff without a host synchronisation.  `hip_event` is a hipEvent_t the caller
+ * owns (a C++ host's, or torch.cuda.Event.cuda_event).  rt_device_wait_event: the work the device
+ * queues from now on waits for the event -- e.g. buffers the caller filled on its own stream, then
+ * recorded the event there (rt_shard_unpack's source, the split prepass's gathered CameraResults).
+ * rt_device_record_event: records the event after everything queued on the device so far; the
+ * caller's stream waits for it (hipStreamWaitEvent) before it reads the device's outputs.  The
+ * device streams are non-blocking, so without one of these (or a host synchronisation) a caller's
+ * stream and a device's run in no order.  No reference counterpart (D3D11 orders one immediate
+ * context implicitly). */
+int rt_device_wait_event(rt_device dev, void* hip_event);
+int rt_device_record_event(rt_device dev, void* hip_event);
+/* (ABI 6) Queue-overflow check: k_trace's per-block queues (hit stack, long-ray spill ring) are
+ * bounded by its work priorities (rt_spill_caps); a push that would exceed a bound is not stored and
+ * raises a sticky flag on the device instead of overwriting queued work.  rt_device_check
+ * synchronises the device stream and returns RT_ERR_STATE (the message names the queue) if any
+ * flag was raised since the last check, clearing it; RT_OK otherwise. */
+int rt_device_check(rt_device dev);
 
 /* ---- ITexture (IDevice::createTexture + ITexture::create(dims, fmt, w, h, data, binding, cpu)) ---- */
 int rt_texture_create(rt_device dev, rt_texture* out);

@@ -40,6 +40,10 @@ def main():
                          "all-gather is not simulated: the other frames' CameraResults come from a full prepass "
                          "run once before timing)")
     ap.add_argument("--barrier-model", action="store_true")
+    ap.add_argument("--no-prepass", action="store_true",
+                    help="diagnostic bound for a prepass fused into the previous batch's trace: every batch traces "
+                         "from CameraResults computed once before timing (rt_terrain_trace_batch), no prepass "
+                         "in the timed loop")
     ap.add_argument("--lookahead", type=int, default=0,
                     help="1: FrameRing(lookahead=True), each batch's prepass queued on the GPU's side stream before "
                          "the previous batch's trace (rt_terrain_prepass_ahead); 0 (bench.py's default): in line")
@@ -75,6 +79,11 @@ def main():
         torch.cuda.synchronize()
 
         def step(r, n, ahead=True):
+            if a.no_prepass:
+                g = (ring.frame // B) % ring.depth
+                G.engine.trace_batch([t for _, t in ring.slots[g * B:(g + 1) * B]], r, n, bufs[g].data_ptr())
+                ring.frame += B
+                return
             if not a.split_prepass or n == 1:
                 ring.render_batch(r, n, present=False, ahead=ahead)
                 return
@@ -100,7 +109,7 @@ def main():
                 worst = max(worst, ms)
             if base is None:
                 base = worst
-            print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass,
+            print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "no_prepass": a.no_prepass,
                               "lookahead": int(ring.lookahead), "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()

@@ -31,9 +31,11 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         ao=0, graph=False, small_rings=False):
+         ao=0, graph=False, small_rings=False, float_output=True):
+    """float_output=False: the product's device (RGBA8 only), where one sample per pixel with at most one
+    AO ray finishes hit pixels in k_trace (UnitMap::fit) instead of through per-sample colours."""
     import gpgpuraytrace_amd as G
-    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=True,
+    dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=float_output,
                                     stats=stats, graph=graph, small_rings=small_rings)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
@@ -169,23 +171,32 @@ def test_density_bitexact(land):
 
 
 # --- whole frames vs the golden oracle frames ----------------------------------------------
-@pytest.mark.parametrize("kernels", ["stats", "product", "spill"])
+@pytest.mark.parametrize("kernels", ["stats", "product", "spill", "fit", "fit_spill"])
 @pytest.mark.parametrize("spec", GI.FRAMES, ids=[GI.frame_key(*s) for s in GI.FRAMES])
 def test_frame_bitexact_device_path(spec, kernels):
     """stats: the instrumented kernels (their counts equal the oracle's too); product: the
     uninstrumented kernels the bench times; spill: the product kernels with a 64-entry LDS long ring
     and an 8-slot fin pool (RT_DEVICE_DEBUG_SMALL_RINGS), so queued long rays go through the
-    per-block spill rings and long shadows through the fin[t] fallback."""
+    per-block spill rings and long shadows through the fin[t] fallback; fit / fit_spill: the same
+    without float output, the bench's device (one sample per pixel and <= 1 AO ray: hit pixels
+    finished in k_trace, UnitMap::fit), UNORM8 against the golden frame."""
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
+    fit = kernels.startswith("fit")
     dev, ter = make(GI.consts(w, h, pose), land=land, aa=aa, max_steps=ms, stats=kernels == "stats", ao=ao,
-                    small_rings=kernels == "spill")
+                    small_rings=kernels.endswith("spill"), float_output=not fit)
     ter.render_device()
     dev.present()
-    img, img8 = dev.readback_float(), dev.readback()
-    assert bits_equal(img, gold[key + "_rgba32f"])
+    img8 = dev.readback()
     assert np.array_equal(img8, gold[key + "_rgba8"])
+    dev.check()
+    if fit:
+        assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
+        dev.destroy()
+        return
+    img = dev.readback_float()
+    assert bits_equal(img, gold[key + "_rgba32f"])
     if kernels != "stats":
         assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"])
         dev.destroy()
@@ -212,7 +223,10 @@ def test_noise_wave_iterations_bound_lane_utilisation():
     calls = st["noise_calls"] - pre["noise_calls"]
     waves = st["noise_wave_iters"] - pre["noise_wave_iters"]
     assert pre["noise_wave_iters"] == 0 and waves > 0
-    assert 0.0 < calls / (64.0 * waves) <= 1.0
+    util = calls / (64.0 * waves)
+    # a 64x48 frame's units are mostly partial rays near the horizon: measured PLACEHOLDER
+    print("noise lane utilisation 64x48:", util)
+    assert 0.2 < util <= 1.0, util
     dev.destroy()
 
 
@@ -429,21 +443,25 @@ def test_other_landscapes_720p_rows_bitexact(land, ao):
     dev.destroy()
 
 
-@pytest.mark.parametrize("name,small_rings", [("c2", False), ("c3", False), ("c3", True)])
-def test_baseline_config_batch_rows_bitexact(name, small_rings):
+@pytest.mark.parametrize("name,small_rings,fit", [("c2", False, False), ("c3", False, False), ("c3", True, False),
+                                                  ("c2", False, True), ("c3", False, True), ("c3", True, True)])
+def test_baseline_config_batch_rows_bitexact(name, small_rings, fit):
     """The bench's entry point: one rt_terrain_render_batch of 4 frames (reset, look-down,
     reset, look-down) at the config's size; every frame equals the oracle on its row sample.
-    small_rings: the C3 batch with 64-entry LDS rings, so most queued work spills to HBM."""
+    small_rings: the C3 batch with 64-entry LDS rings, so most queued work spills to HBM.  fit: the
+    bench's RGBA8-only devices (hit pixels finished in k_trace; C2 has no k_finish at all)."""
     from gpgpuraytrace_amd import engine as E
     w, h, ms, ao, step = BASELINE_CONFIGS[name]
     poses = ["reset", "lookdown", "reset", "lookdown"]
     refs = {p: _config_rows(name, p, 3) for p in ("reset", "lookdown")}
-    frames = [make(refs[p][0], max_steps=ms, ao=ao, small_rings=small_rings) for p in poses]
+    frames = [make(refs[p][0], max_steps=ms, ao=ao, small_rings=small_rings, float_output=not fit) for p in poses]
     E.render_batch([t for _, t in frames])
     for (dev, _), p in zip(frames, poses):
         _, (ref, ref8, _, _, _), rows = refs[p]
-        assert bits_equal(dev.readback_float()[rows], ref[rows])
+        if not fit:
+            assert bits_equal(dev.readback_float()[rows], ref[rows])
         assert np.array_equal(dev.readback()[rows], ref8[rows])
+        dev.check()
     for d, _ in frames:
         d.destroy()
 
@@ -1233,3 +1251,124 @@ def test_sky_known_answers_device(eye_i):
         assert G.lib().rt_debug_sky(ter.compute._h, d.ctypes.data, out.ctypes.data, len(d)) == 0
         assert bits_equal(out, O.sky(O.noise_tables(), K.frame(K.EYES[eye_i], t), d))
         dev.destroy()
+
+
+# --- stream handoff (ABI 6 rt_device_wait_event / rt_device_record_event) -----------------------------
+def _hip():
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+    return lib
+
+
+def test_event_handoff_without_host_sync():
+    """A buffer filled on torch's stream (behind a ~20 ms spin kernel, so an unordered reader would
+    see the old contents) is handed to a device by event, no host synchronisation: rt_shard_unpack on
+    the device stream reads the filled bytes.  The other way, a rendered frame is handed to torch's
+    stream by rt_device_record_event and copied there: the golden frame."""
+    import torch
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    key = GI.frame_key("nomadplains", "reset", 64, 48, 1, 0)
+    dev, ter = make(GI.consts(64, 48, "reset"))
+    n = E.shard_bytes(dev, 0, 1)
+    buf = torch.zeros(n, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    pattern = (torch.arange(n, device="cuda:0") % 251).to(torch.uint8)
+    torch.cuda._sleep(50_000_000)  # ~20 ms on the torch stream before the fill
+    buf.copy_(pattern)
+    filled = torch.cuda.Event()
+    filled.record(torch.cuda.current_stream())
+    dev.wait_event(filled.cuda_event)
+    E.shard_unpack(dev, 0, 1, buf.data_ptr())  # tiles -> framebuffer (64x48: 2x2 tiles, partly outside)
+    got = dev.readback().view(np.uint32).reshape(48, 64)
+    want = np.zeros((48, 64), np.uint32)
+    from gpgpuraytrace_amd import parallel as P
+    P.unpack_host(want, pattern.cpu().numpy().view(np.uint32), 0, 1)
+    assert np.array_equal(got, want)
+    # device -> torch: the frame, recorded on the device stream, copied on torch's stream
+    torch.cuda.synchronize()
+    ter.render_device()
+    done = torch.cuda.Event()
+    dev.record_event(done.cuda_event)
+    torch.cuda.current_stream().wait_event(done)
+    out = torch.empty(64 * 48 * 4, dtype=torch.uint8, device="cuda:0")
+    assert _hip().hipMemcpyAsync(out.data_ptr(), dev.framebuffer_pointer(), out.numel(), 3,
+                                 torch.cuda.current_stream().cuda_stream) == 0  # device to device
+    assert np.array_equal(out.cpu().numpy().reshape(48, 64, 4), gold[key + "_rgba8"])
+    dev.check()
+    dev.destroy()
+
+
+def test_device_flags_retired_and_check():
+    """ABI 6: the retired flags 8 and 16 (ABI <= 5 RT_DEVICE_SEG_TAIL_*) and any unknown flag are
+    rejected; rt_device_check is RT_OK after frames through the spill rings (no dropped push)."""
+    import gpgpuraytrace_amd as G
+    h = C.c_void_p()
+    for bad in (8, 16, 64, 1 << 20):
+        assert G.lib().rt_device_create(0, 64, 48, bad, C.byref(h)) == -1  # RT_ERR_INVALID
+    dev, ter = make(GI.consts(64, 48, "lookdown"), small_rings=True, ao=4)
+    for _ in range(3):
+        ter.render_device()
+    dev.check()
+    dev.destroy()
+
+
+def test_graph_ring_phase_marks_readable():
+    """bench.py's timed loop on a hipGraph FrameRing (C5's frame loop, 2 slot groups of 2 frames):
+    run_batch's phase marks (torch events on each batch's stream) read right after the loop, with no
+    graph capture inside it after warm-up and no mark recorded on a capturing stream -- every pair
+    readable (round 3 read them after the ring's streams were destroyed and lost C5 marks)."""
+    import torch
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    import bench
+    gold = GI.load()
+    spec = GI.FRAMES[1]
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    cam = FixedCamera(GI.consts(w, h, pose))
+    ring = G.FrameRing(w, h, depth=2, batch=2, camera=cam, graph=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cam.c["sun"])
+    plan = P.BatchPlan(w, h, 2, 1)
+
+    class Ops:
+        def __init__(self):
+            self.group = ring.group()
+
+        def render(self):
+            E.render_batch([t for _, t in self.group], 0, 1)
+
+        def present(self):
+            for d, _ in self.group:
+                d.present()
+
+    streams = [torch.cuda.ExternalStream(ring.slots[g * 2][0].stream(), device="cuda:0") for g in range(2)]
+    for _ in range(3):  # warm-up: both groups capture their graphs
+        P.run_batch(plan, 0, Ops())
+        ring.frame += 2
+    torch.cuda.synchronize()
+    caps = sum(d.graph_info()[0] for d, _ in ring.slots)
+    marks, capturing = [], 0
+    for _ in range(4):
+        g = (ring.frame // 2) % 2
+        mk = []
+
+        def mark(name, mk=mk, s=streams[g]):
+            nonlocal capturing
+            capturing += bench.stream_capturing(s)
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(s)
+            mk.append((name, ev))
+        P.run_batch(plan, 0, Ops(), mark=mark)
+        marks.append(mk)
+        ring.frame += 2
+    torch.cuda.synchronize()
+    assert sum(d.graph_info()[0] for d, _ in ring.slots) == caps  # no capture in the timed loop
+    assert capturing == 0
+    summary = P.phase_summary(marks, lambda a, b: a.elapsed_time(b))
+    assert summary["batches"] == 4 and len(summary["phase_ms"]) == 1 and summary["phase_ms"]["trace"] > 0
+    for d, _ in ring.slots:
+        assert np.array_equal(d.readback(), gold[GI.frame_key(*spec) + "_rgba8"])
+    ring.destroy()
