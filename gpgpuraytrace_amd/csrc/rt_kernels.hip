@@ -767,16 +767,22 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
 {
     if (aux_ao(aux)) {
         if (st.d > 0.0f) {
-            if (aux == kAuxAO) ao_count(aocc, t);
-            else fit_store(k, m, fr, t, aux | 0xff000000u);
+            if (aux == kAuxAO) {
+                if (!(RT_DIAG_SKIP & 8)) ao_count(aocc, t);
+            } else if (!(RT_DIAG_SKIP & 2)) {
+                fit_store(k, m, fr, t, aux | 0xff000000u);
+            }
         }
     } else {
         constexpr uint32_t FR = FinRec<L>::N;
         const float4* f = aux == kAuxFinT ? fin + (size_t)FR * t : finp + (size_t)FR * aux;
         const float4 fog = FogLive<L>::value ? ld_fresh(f + 1) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float4 v = shade_finish(k, ld_fresh(f), fog, ld_fresh(f + FR - 1u), st.d, st.f.w);
-        if (m.fit && k->ao_samples == 0) fit_store(k, m, fr, t, fit_pixel(v, 1.0f));
-        else sample_store(k, samples, t, v);
+        if (m.fit && k->ao_samples == 0) {
+            if (!(RT_DIAG_SKIP & 2)) fit_store(k, m, fr, t, fit_pixel(v, 1.0f));
+        } else if (!(RT_DIAG_SKIP & 4)) {
+            sample_store(k, samples, t, v);
+        }
     }
 }
 
@@ -1246,9 +1252,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (m.fit) {
                     // the pixel is final now (no AO), or its unoccluded value is (ao_factor(0, 1) = 1) and
                     // the AO ray carries the occluded one (ao_factor(1, 1)); no sample, no k_finish
-                    gptr(ft->out8[f])[(size_t)late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
+                    if (!(RT_DIAG_SKIP & 2)) gptr(ft->out8[f])[(size_t)late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
                     if (k->ao_samples) ao_aux = kAuxAOCand | (fit_pixel(v, ao_factor(1u, 1)) & 0xffffffu);
-                } else {
+                } else if (!(RT_DIAG_SKIP & 4)) {
                     sample_store(k, samples, t, v);
                 }
                 stat(BlockStats::SHADOW, (uint32_t)st.iters);
@@ -1264,7 +1270,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (more) aux = rank < got ? (uint32_t)q.fin_free[top - 1u - rank] : kAuxFinT;
                 if (lane == lead) q.f_top = top - got;
                 q_unlock(&q.lock, lane - lead);
-                if (more) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
+                if (more && !(RT_DIAG_SKIP & 16)) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
             }
         });
         // fit with AO: the hits whose long shadow races their AO ray are k_finish's (their bit in the
@@ -1340,7 +1346,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     const float4 v = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
                     if (aa == 1u) { // the pixel is final (k_finish's sum of one sample times rcp(1) is v itself)
                         const size_t o = (size_t)py * W + px;
-                        gptr(ft->out8[f])[o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
+                        if (!(RT_DIAG_SKIP & 1))
+                            gptr(ft->out8[f])[o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
                         if (float4* o32 = ft->out32[f]) gstore(o32 + o, make_float4(v.x, v.y, v.z, 1.0f));
                     } else {
                         samples[t] = v;
@@ -1509,7 +1516,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         c1 = c1 * ia;
         c2 = c2 * ia;
         size_t o = (size_t)py * (size_t)k->width + px;
-        out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
+        if (!(RT_DIAG_SKIP & 64)) out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
         if (out32) gstore(out32 + o, make_float4(c0, c1, c2, 1.0f));
     }
 }

@@ -67,6 +67,12 @@
 // RT_COUNT_LONG_STEPS=k  the same for long-ray steps (1 always, 2 after the drain, 3 before)
 // RT_COUNT_PHASE=k       count only the noise of k_trace work kind k (rt_shader.h count_noise)
 // RT_EXTRA_OCTAVE=n      n dead octaves per nomadplains density sample (issue-cost experiment)
+// RT_DIAG_SKIP=mask      HBM attribution: drop a class of stores (wrong pixels, same control flow):
+//                        1 miss pixels, 2 k_trace hit pixels (fit), 4 hit samples, 8 AO-count atomics,
+//                        16 long-shadow fin records, 64 k_finish pixels
+#ifndef RT_DIAG_SKIP
+#define RT_DIAG_SKIP 0
+#endif
 #ifdef RT_WAVE_TRACE
 #define RT_WT_FIELDS 21
 #define RT_WT_MAX_WAVES 8192

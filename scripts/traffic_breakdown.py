@@ -39,12 +39,16 @@ def main():
     ap.add_argument("--batch", type=int, default=10)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "traffic_breakdown.json"))
     ap.add_argument("--timeout", type=int, default=120)
+    ap.add_argument("--variant", default="", help="experiment build librt_hip_<variant>.so (scripts/with_variant.py)")
+    ap.add_argument("--groups", default="all", help="'all' or 'bytes' (FETCH_SIZE and WRITE_SIZE only)")
     a, rest = ap.parse_known_args()
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
-    child = [sys.executable, os.path.join(ROOT, "bench.py"), "--traffic-child", "--batch", str(a.batch)] + rest
-    env = dict(os.environ, TMPDIR="/tmp")
-    result = {"batch": a.batch, "child": " ".join(child[1:]), "kernels": {}}
-    for g in GROUPS:
+    child = [sys.executable, os.path.join(ROOT, "scripts", "with_variant.py"), os.path.join(ROOT, "bench.py"),
+             "--traffic-child", "--batch", str(a.batch)] + rest
+    env = dict(os.environ, TMPDIR="/tmp", RT_LIB_VARIANT=a.variant)
+    groups = GROUPS if a.groups == "all" else GROUPS[:2]
+    result = {"batch": a.batch, "variant": a.variant, "child": " ".join(child[1:]), "kernels": {}}
+    for g in groups:
         work = tempfile.mkdtemp(prefix="tb_", dir="/tmp")
         cmd = ["timeout", "-s", "KILL", str(a.timeout), prof, "--pmc"] + g + ["--output-format", "csv", "-d", work,
                                                                                "-o", "run", "--"] + child
@@ -80,6 +84,9 @@ def main():
     json.dump(result, open(a.out, "w"), indent=1)
     for k, cs in result["kernels"].items():
         print(k, {c: round(v) for c, v in sorted(cs.items())})
+    tot = {c: sum(cs.get(c, 0.0) for cs in result["kernels"].values() if c in cs) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+    print(f"variant={a.variant or 'product'} total FETCH_SIZE {tot['FETCH_SIZE'] / 1024:.1f} MiB, WRITE_SIZE "
+          f"{tot['WRITE_SIZE'] / 1024:.1f} MiB, 2F+W {(2 * tot['FETCH_SIZE'] + tot['WRITE_SIZE']) / 1024:.1f} MiB", flush=True)
 
 
 if __name__ == "__main__":

@@ -224,9 +224,9 @@ def test_noise_wave_iterations_bound_lane_utilisation():
     waves = st["noise_wave_iters"] - pre["noise_wave_iters"]
     assert pre["noise_wave_iters"] == 0 and waves > 0
     util = calls / (64.0 * waves)
-    # a 64x48 frame's units are mostly partial rays near the horizon: measured PLACEHOLDER
-    print("noise lane utilisation 64x48:", util)
-    assert 0.2 < util <= 1.0, util
+    # a 64x48 frame is mostly partial units (its 8x8 units straddle the horizon): measured 0.449 with
+    # the product's primary segment tail (ABI 6); far too many counted wave iterations fall below this
+    assert 0.35 < util <= 1.0, util
     dev.destroy()
 
 
@@ -1290,6 +1290,7 @@ def test_event_handoff_without_host_sync():
     torch.cuda.synchronize()
     ter.render_device()
     done = torch.cuda.Event()
+    done.record()  # torch creates its events on first record; the device then re-records it on its stream
     dev.record_event(done.cuda_event)
     torch.cuda.current_stream().wait_event(done)
     out = torch.empty(64 * 48 * 4, dtype=torch.uint8, device="cuda:0")
