@@ -11,7 +11,7 @@
 enum { RT_CTR_PRIMARY = 0 };
 #define RT_CTR_BYTES 64
 #define RT_QUEUE_BYTES 128
-enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u };
+enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_TIMEOUT = 4u };
 
 // A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by
 // one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
@@ -25,6 +25,19 @@ struct FrameTable {
     float2* cells[RT_MAX_BATCH]; // CellDistance, float2[1024]
     uint32_t* out8[RT_MAX_BATCH];
     float4* out32[RT_MAX_BATCH]; // may be null
+};
+
+// The NEXT batch's camerarays prepass fused into this batch's k_trace (nomadplains):
+// `tasks` tasks of 8 rays (8 lanes per ray) of the frames of `ft` (their camerarays constant blocks
+// kcam, their CameraResults cam), taken from ctl[0]; a finished task stores its rays' CameraResults
+// (one whole 128-B line, sc1) and adds 8 to ctl[1]; that batch's k_order waits for ctl[1] to reach
+// its rays (frames x 1024) before it reads them.  tasks == 0: none.
+#define RT_FUSE_RAYS_PER_TASK 8
+#define RT_FUSE_TASKS_PER_FRAME (RT_CAMERA_RES * RT_CAMERA_RES / RT_FUSE_RAYS_PER_TASK)
+struct FusedPrepass {
+    const FrameTable* ft;
+    uint32_t* ctl;
+    uint32_t tasks;
 };
 
 struct RtLaunch {
@@ -57,6 +70,9 @@ struct RtLaunch {
     FrameTable frames_host;   // the same pointers on the host
     uint32_t n_frames;        // frames in the batch (1..RT_MAX_BATCH)
     hipEvent_t after_order;   // recorded after k_order when set (its read of CameraResults is done)
+    FusedPrepass fuse_next;   // the next batch's prepass, run inside this k_trace (tasks 0: none); k_order zeroes its ctl
+    const uint32_t* wait_ctl; // this batch's prepass ran inside the previous k_trace: k_order waits for wait_ctl[1]
+    uint32_t wait_total;      //   to reach this many rays
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);

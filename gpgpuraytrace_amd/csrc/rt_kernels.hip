@@ -235,7 +235,9 @@ __device__ __forceinline__ void cell_depths_frame(const float4* __restrict__ cam
 {
     const int i = threadIdx.x;
     __syncthreads(); // s_d's previous frame is no longer read
-    s_d[i] = cam[i].w;
+    // sc1 (L1-bypassing) load: a fused prepass wrote these in another kernel (FusedPrepass; the
+    // hand-off's loads are all global_load_dword sc1 after k_order's poll and barrier)
+    s_d[i] = __hip_atomic_load(reinterpret_cast<const float*>(cam + i) + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     int xpos = i % RT_CAMERA_RES, ypos = i / RT_CAMERA_RES;
     float dmin = cd_interp(s_d, xpos, ypos);
@@ -363,13 +365,34 @@ __device__ __forceinline__ void hit_store(float4* __restrict__ r, uint32_t t, co
 constexpr uint32_t kOrderLdsBuckets = 144u * 1024u;
 constexpr uint32_t kOrderBatchUnitsPerWave = 4u;
 __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
-                                                uint32_t* __restrict__ order, uint32_t* __restrict__ counters)
+                                                uint32_t* __restrict__ order, uint32_t* __restrict__ counters,
+                                                const uint32_t* wait_ctl, uint32_t wait_total, uint32_t* zero_ctl)
 {
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
     __shared__ uint8_t s_b[kOrderLdsBuckets];
-    // k_trace's work counters start at zero (k_trace follows on the stream)
+    // k_trace's work counters start at zero (k_trace follows on the stream), and so do the counters
+    // of the next batch's prepass that k_trace runs (FusedPrepass)
     if (blockIdx.x == 0 && threadIdx.x < RT_CTR_BYTES / 4) counters[threadIdx.x] = 0u;
+    if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 2) zero_ctl[threadIdx.x] = 0u;
+    if (wait_ctl) {
+        // this batch's prepass runs inside the previous batch's k_trace (FusedPrepass): wait until its
+        // rays are in (each task stored its line with sc1, waited, then added to ctl[1]).  The tasks are
+        // taken before that kernel's waves may leave, and they are finished by resident waves, so the
+        // wait ends; the bound (0.5 s of the 100 MHz clock) turns a broken protocol into a flagged error
+        // (rt_device_check) instead of a hang.
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(wait_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_total) {
+                __builtin_amdgcn_s_sleep(8);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+                    atomicOr(counters + RT_CTR_BYTES / 4, RT_FLAG_PREPASS_TIMEOUT);
+                    break;
+                }
+            }
+        }
+        __syncthreads(); // every load of the CameraResults after the poll
+    }
     // setTargetDepths (Terrain.cpp:398-439) of this workgroup's frames first: the device path's
     // CellDistance comes from the prepass's CameraResults (one launch fewer than a separate kernel)
     if (m.cells_from_cam) {
@@ -493,13 +516,24 @@ __device__ __forceinline__ float4 miss_sample(const Ctx& c, float px, float py, 
     return make_float4(rtm::sat(col.x), rtm::sat(col.y), rtm::sat(col.z), 0.0f);
 }
 
-// Loads of data another wave of this kernel wrote: bypass the CU's L1 (a line cached
-// there earlier would be stale), served by the XCD's L2 the producer wrote through.
-__device__ __forceinline__ float ld_fresh1(const float* p) { return __builtin_nontemporal_load(p); }
+// Loads of data another wave of this kernel (on this CU) wrote: bypass the CU's L1 (a line cached
+// there earlier would be stale), served by the XCD's L2 the producer wrote through: `sc1` loads.
+// Not nontemporal ones: an nt load marks the line evict-first, so the per-block LIFO hit stack and
+// fin pool, whose few lines are rewritten over and over, were written back to HBM after every pop
+// (profiles/r04/traffic_attribution.md).  ld_rec: record i (16-B units) of a block-local array (a
+// uniform base, so a buffer load); ld_fresh: any address (the fin[t] fallback), waited at once.
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_rec(const float4* base, uint32_t i)
+{
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(base), (short)0, 0x7fffffff, 0x00020000);
+    const v4f_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 16 /* sc1 */);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
 __device__ __forceinline__ float4 ld_fresh(const float4* p)
 {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+    v4f_t v;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
@@ -775,9 +809,18 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
         }
     } else {
         constexpr uint32_t FR = FinRec<L>::N;
-        const float4* f = aux == kAuxFinT ? fin + (size_t)FR * t : finp + (size_t)FR * aux;
-        const float4 fog = FogLive<L>::value ? ld_fresh(f + 1) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float4 v = shade_finish(k, ld_fresh(f), fog, ld_fresh(f + FR - 1u), st.d, st.f.w);
+        float4 f0, f1, fog = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (aux == kAuxFinT) { // the pool was empty: fin[t] (rare)
+            const float4* f = fin + (size_t)FR * t;
+            f0 = ld_fresh(f);
+            if constexpr (FogLive<L>::value) fog = ld_fresh(f + 1);
+            f1 = ld_fresh(f + FR - 1u);
+        } else {
+            f0 = ld_rec(finp, FR * aux);
+            if constexpr (FogLive<L>::value) fog = ld_rec(finp, FR * aux + 1u);
+            f1 = ld_rec(finp, FR * aux + FR - 1u);
+        }
+        const float4 v = shade_finish(k, f0, fog, f1, st.d, st.f.w);
         if (m.fit && k->ao_samples == 0) {
             if (!(RT_DIAG_SKIP & 2)) fit_store(k, m, fr, t, fit_pixel(v, 1.0f));
         } else if (!(RT_DIAG_SKIP & 4)) {
@@ -903,7 +946,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                                                 uint32_t long_spill_cap,
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
-                                                uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots)
+                                                uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots,
+                                                FusedPrepass np)
 {
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
@@ -1029,8 +1073,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
                     take_ray(r[0], r[1], r[2]);
                 } else if (mine) {
-                    const float4* r = lspill + (size_t)((sh + rank - take) % long_spill_cap) * kShadowRec;
-                    take_ray(ld_fresh(r), ld_fresh(r + 1), ld_fresh(r + 2));
+                    const uint32_t ri = ((sh + rank - take) % long_spill_cap) * kShadowRec;
+                    take_ray(ld_rec(lspill, ri), ld_rec(lspill, ri + 1u), ld_rec(lspill, ri + 2u));
                 }
                 if (lane == 0) {
                     q.l_head = head + take;
@@ -1094,10 +1138,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     r1 = r[1];
                     r2 = r[2];
                 } else {
-                    const float4* r = lspill + (size_t)((sh + grp - take) % long_spill_cap) * kShadowRec;
-                    r0 = ld_fresh(r);
-                    r1 = ld_fresh(r + 1);
-                    r2 = ld_fresh(r + 2);
+                    const uint32_t ri = ((sh + grp - take) % long_spill_cap) * kShadowRec;
+                    r0 = ld_rec(lspill, ri);
+                    r1 = ld_rec(lspill, ri + 1u);
+                    r2 = ld_rec(lspill, ri + 2u);
                 }
                 t = long_unpack(r0, r1, r2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
                 const float* fr = s_fr.v[frame_of(m, t)];
@@ -1224,11 +1268,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         const uint32_t take = top < 64u ? top : 64u;
         float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0;
         if (lane < take) {
-            const float4* r = hq + (size_t)(top - take + lane) * HR;
-            r0 = ld_fresh(r);
+            const uint32_t ri = (top - take + lane) * HR;
+            r0 = ld_rec(hq, ri);
             if constexpr (HR == 3u) {
-                r1 = ld_fresh(r + 1);
-                r2 = ld_fresh(r + 2);
+                r1 = ld_rec(hq, ri + 1u);
+                r2 = ld_rec(hq, ri + 2u);
             }
         }
         __builtin_amdgcn_s_waitcnt(0); // read before the slots can be reused
@@ -1287,6 +1331,56 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             March<L, true> ao;
             if (valid) ao_begin(c, h, (uint32_t)kk, ao);
             push_long(valid, ao, t, ao_aux);
+        }
+    };
+
+    // ---- a task of the NEXT batch's camerarays prepass (FusedPrepass; camerarays.hlsl:12-21) ----
+    // 8 rays, one 8-lane segment each (ray r on lanes 8r..8r+7), marched as k_camerarays_group marches
+    // them: the octaves of each density sample spread over the segment (density_nomadplains_seg,
+    // bit-identical to density_nomadplains), that frame's camerarays constants, frame 0's launch
+    // constants.  The 8 results form one 128-B line of CameraResults, stored whole by one sc1
+    // instruction; after the store is acknowledged the task adds 8 to ctl[1] (the next k_order polls it).
+    auto do_prepass = [&](uint32_t qt) {
+        if constexpr (L == RT_NOMADPLAINS) {
+            constexpr uint32_t LPR = RT_FUSE_RAYS_PER_TASK;
+            const uint32_t f = qt / RT_FUSE_TASKS_PER_FRAME;
+            const uint32_t ray = (qt - f * RT_FUSE_TASKS_PER_FRAME) * RT_FUSE_RAYS_PER_TASK + late(lane) / LPR;
+            const uint32_t lid = late(lane);
+            const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
+            Ctx cp = c;
+            cp.k = np.ft->kcam[0];
+            cp.kf = (KPtr)np.ft->kcam[f];
+            cp.eye = rtm::mk(uniform_f(cp.kf->eye[0]), uniform_f(cp.kf->eye[1]), uniform_f(cp.kf->eye[2]));
+            cp.sun = rtm::mk(uniform_f(cp.kf->sun[0]), uniform_f(cp.kf->sun[1]), uniform_f(cp.kf->sun[2]));
+            const uint32_t tx = ray % RT_CAMERA_RES, ty = ray / RT_CAMERA_RES;
+            const float r31 = rtm::rcp(31.0f);
+            const uint32_t pxs = (uint32_t)(((float)tx * r31) * cp.k->screen[0]);
+            const uint32_t pys = (uint32_t)(((float)ty * r31) * cp.k->screen[1]);
+            f3 p, dir;
+            get_pixel_ray(cp, (float)pxs, (float)pys, &p, &dir);
+            March<L, false> st;
+            march_begin(cp, st, p, RT_CAMERA_NEAR, 2.0f, dir);
+            const SegOctaves<LPR> g = seg_octaves<LPR>(cp, j);
+            __builtin_amdgcn_s_setprio(3); // latency-bound: the next batch's k_order waits for these rays
+            while (march_live<L, false, true>(cp, st, RT_CAMERA_FAR, 0)) {
+                auto dens = [&](f3 q0) {
+                    uint32_t used;
+                    return density_nomadplains_seg<LPR, true>(cp, g, q0, j, base, &used);
+                };
+                march_step_with<L, false, true, decltype(dens), true>(cp, st, dens);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            RayResult rr = march_result(st);
+            if (rr.density < 0.0f) rr.pd.w = RT_CAMERA_FAR;
+            if (j == 0u) {
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                const v4f v = {rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w};
+                float4* dst = np.ft->cam[f] + ray;
+                asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
+            }
+            asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+            if (lane == 0) __hip_atomic_fetch_add(np.ctl + 1, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
         }
     };
 
@@ -1386,8 +1480,21 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     const uint32_t n_static = gridDim.x * (blockDim.x >> 6);
     const uint32_t first_qi = first_unit_index(); // scalar, formed before the loop
     bool first_unit = true;
+    bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
+        // the next batch's prepass first (after a wave's static first unit): its k_order waits for it.
+        // A wave leaves only after it found no task left, so every task is taken by a resident wave.
+        if constexpr (L == RT_NOMADPLAINS) {
+            if (np_open && !first_unit) {
+                const uint32_t qt = wave_fetch(np.ctl, lane);
+                if (qt < np.tasks) {
+                    do_prepass(qt);
+                    continue;
+                }
+                np_open = false;
+            }
+        }
         const uint32_t lp = queued_long();
         const uint32_t hp = queued_hits();
         const bool drained = vload(q.drained) != 0u;
@@ -1654,7 +1761,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.cells_from_cam = (uint32_t)a.cells_from_cam;
     m.fit = (uint32_t)a.fit;
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
-    hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue);
+    hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue,
+                       a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill rings
     auto primary = [&](auto stats_tag) {
@@ -1664,7 +1772,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                            a.perm2d, a.grad, m,
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
-                           a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots);
+                           a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots, a.fuse_next);
         // fit without AO: every hit pixel is final in k_trace
         if (!(m.fit && a.ao_samples == 0))
             hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);

@@ -143,7 +143,7 @@ struct rt_device_s {
         FrameTable last{};
         bool valid = false;
         Staging staging;
-    } table, pre_table;
+    } table, pre_table, fuse_table;
     hipEvent_t sync_ev = nullptr; // orders this device's stream against a batch on another device
     // rt_terrain_prepass_ahead, for batches led by this device: ev_order follows its last k_order
     // (the last read of the frames' CameraResults), ev_ahead the ahead prepass on the GPU's side
@@ -155,6 +155,15 @@ struct rt_device_s {
     // are not read -- by a render this device leads, or a map -- before ev_ahead_in
     hipEvent_t ev_ahead_in = nullptr;
     bool ahead_in_pending = false;
+    // the prepass of the batch this device leads fused into another batch's k_trace (FusedPrepass):
+    // STAGED = constants and frame table uploaded by rt_terrain_prepass_ahead, waiting for a trace to
+    // take it; FUSED = a k_trace runs it (ev_fuser_done follows that launch).  fctl: its task / ray
+    // counters (zeroed by the fusing batch's k_order, polled by this batch's k_order)
+    enum { FUSE_NONE = 0, FUSE_STAGED = 1, FUSE_FUSED = 2 };
+    int fuse_state = FUSE_NONE, fuse_n = 0;
+    uint32_t* fctl = nullptr;
+    std::vector<rt_device_s*> fuse_devs; // the devices of its frames
+    hipEvent_t ev_fuser_done = nullptr;
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -485,6 +494,9 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.frames_host = FrameTable{};
     a.n_frames = 1;
     a.after_order = nullptr;
+    a.fuse_next = FusedPrepass{nullptr, nullptr, 0u};
+    a.wait_ctl = nullptr;
+    a.wait_total = 0;
     return a;
 }
 
@@ -624,6 +636,16 @@ void stream_unref(hipStream_t s)
 // process (devices come and go; the stream carries no state of theirs past its work)
 std::map<int, hipStream_t> g_ahead_streams;
 
+// lead devices whose batch is STAGED for fusing, per GPU, oldest first
+std::map<int, std::vector<rt_device_s*>> g_fuse_staged;
+
+void fuse_forget(rt_device_s* d)
+{
+    std::lock_guard<std::mutex> lk(g_stream_mu);
+    auto& v = g_fuse_staged[d->ordinal];
+    v.erase(std::remove(v.begin(), v.end(), d), v.end());
+}
+
 hipStream_t ahead_stream(int ordinal, bool create)
 {
     std::lock_guard<std::mutex> lk(g_stream_mu);
@@ -638,6 +660,8 @@ hipStream_t ahead_stream(int ordinal, bool create)
 rt_device_s::~rt_device_s()
 {
     (void)hipSetDevice(ordinal);
+    fuse_forget(this);
+    if (fuse_state == FUSE_FUSED && ev_fuser_done) (void)hipEventSynchronize(ev_fuser_done); // it writes our frames
     if (stream) (void)hipStreamSynchronize(stream); // the stream in use is alive: a reference is held
     if (hipStream_t side = ahead_stream(ordinal, false)) (void)hipStreamSynchronize(side); // ahead prepasses
     for (auto* c : computes) delete c;              // children die with their device
@@ -647,12 +671,12 @@ rt_device_s::~rt_device_s()
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
                     (void*)hitq, (void*)finpool, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
-                    (void*)bgrx, (void*)table.d, (void*)pre_table.d})
+                    (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
     if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
-    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in})
+    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in, ev_fuser_done})
         if (e) (void)hipEventDestroy(e);
     for (auto& pr : ev_pool) {
         (void)hipEventDestroy(pr.first);
@@ -695,6 +719,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     HIP_TRY(hipMalloc(&d->scratch_cam, 1024 * sizeof(float4)));
     HIP_TRY(hipMalloc(&d->queue, RT_QUEUE_BYTES));
     HIP_TRY(hipMemset(d->queue, 0, RT_QUEUE_BYTES)); // the counters are reset per launch, the flags here
+    HIP_TRY(hipMalloc(&d->fctl, 16));
+    HIP_TRY(hipMemset(d->fctl, 0, 16));
     HIP_TRY(hipDeviceGetAttribute(&d->num_cus, hipDeviceAttributeMultiprocessorCount, ordinal));
     *out = d.release();
     return RT_OK;
@@ -874,8 +900,10 @@ int rt_device_check(rt_device d)
     HIP_TRY(hipMemcpy(&flags, reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 4, hipMemcpyDeviceToHost));
     if (!flags) return RT_OK;
     HIP_TRY(hipMemset(reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 0, 4));
-    return fail(RT_ERR_STATE, "k_trace queue overflow:%s%s (a push past rt_spill_caps' bound was dropped)",
-                (flags & RT_FLAG_HIT_OVERFLOW) ? " hit stack" : "", (flags & RT_FLAG_SPILL_OVERFLOW) ? " long-ray spill ring" : "");
+    return fail(RT_ERR_STATE, "device flags 0x%x:%s%s%s", flags,
+                (flags & RT_FLAG_HIT_OVERFLOW) ? " k_trace hit stack overflow (a push past rt_spill_caps' bound was dropped)" : "",
+                (flags & RT_FLAG_SPILL_OVERFLOW) ? " k_trace long-ray spill ring overflow" : "",
+                (flags & RT_FLAG_PREPASS_TIMEOUT) ? " k_order timed out waiting for a fused prepass" : "");
 }
 
 int rt_texture_create(rt_device d, rt_texture* out)
@@ -1175,10 +1203,20 @@ size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
 void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
 
 // ---- Terrain::render on the device -------------------------------------------
-enum { PH_PRE = 1, PH_TRACE = 2 };
+// PH_STAGE (rt_terrain_prepass_ahead, fused): upload the camerarays constants and the frame table a
+// fusing k_trace reads, launch nothing
+enum { PH_PRE = 1, PH_TRACE = 2, PH_STAGE = 4 };
+// the tracescreen launch's fused-prepass roles (FusedPrepass): the next batch's prepass it runs, and
+// the wait of its k_order for this batch's prepass that the previous k_trace ran
+struct TraceFuse {
+    FusedPrepass next{nullptr, nullptr, 0u};
+    const uint32_t* wait_ctl = nullptr;
+    uint32_t wait_total = 0;
+};
 static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
                                 int shard_count, bool feed, int phases = PH_PRE | PH_TRACE, int first = 0,
-                                int count = -1, float4* camera_out = nullptr, const float4* camera_in = nullptr);
+                                int count = -1, float4* camera_out = nullptr, const float4* camera_in = nullptr,
+                                const TraceFuse* fuse = nullptr);
 
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
@@ -1350,7 +1388,7 @@ int batch_end(const rt_compute* scrs, int n, Batch& b)
 // (n x 1024 float4) for the split prepass of rt_terrain_prepass_batch / rt_terrain_trace_batch.
 static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
                                 int shard_count, bool feed, int phases, int first, int count, float4* camera_out,
-                                const float4* camera_in)
+                                const float4* camera_in, const TraceFuse* fuse)
 {
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
     if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
@@ -1363,11 +1401,15 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             if (scrs[f] && scrs[f]->dev && ahead_wait(scrs[f]->dev, lead->stream) != 0)
                 return fail(RT_ERR_HIP, "waiting for the ahead prepass failed");
         // a full render prepasses in line: the lead's pending ahead prepass is superseded
-        if (lead->ahead_pending && phases != PH_PRE) lead->ahead_pending = false;
+        if (lead->ahead_pending && phases != PH_PRE && phases != PH_STAGE) lead->ahead_pending = false;
+        if ((phases & PH_PRE) && lead->fuse_state != rt_device_s::FUSE_NONE) { // so is a staged / fused one
+            fuse_forget(lead);
+            lead->fuse_state = rt_device_s::FUSE_NONE;
+        }
     }
     int rc;
     Batch b;
-    if ((rc = batch_begin(cams, scrs, n, b, (phases & PH_PRE) != 0, (phases & PH_TRACE) != 0))) return rc;
+    if ((rc = batch_begin(cams, scrs, n, b, (phases & (PH_PRE | PH_STAGE)) != 0, (phases & PH_TRACE) != 0))) return rc;
     rt_device dev = b.dev;
     FrameTable& ft = b.ft;
     if (count < 0) count = n;
@@ -1384,6 +1426,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             if (ft.cam[f] != scrs[f]->dev->scratch_cam) cam_copy[f] = ft.cam[f];
             ft.cam[f] = const_cast<float4*>(src);
         }
+    }
+    if (phases == PH_STAGE) { // the frames' camerarays constants (above) and the table a fusing k_trace reads
+        if ((rc = upload_frames(dev, dev->fuse_table, ft))) return rc;
+        return batch_end(scrs, n, b);
     }
     if (phases == PH_PRE) {
         // the prepass of frames [first, first + count) only, on its own table
@@ -1414,6 +1460,11 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
     // setTargetDepths runs at the start of the tracescreen launch (k_order), from the CameraResults
     la_scr.cells_from_cam = 1;
+    if (fuse) {
+        la_scr.fuse_next = fuse->next;
+        la_scr.wait_ctl = fuse->wait_ctl;
+        la_scr.wait_total = fuse->wait_total;
+    }
     // one sample per pixel, at most one AO ray and no float output: hit pixels finish where their last
     // ray ends (k_trace), not through a per-sample colour and k_finish
     la_scr.fit = b.s0->aa == 1 && b.s0->ao <= 1;
@@ -1483,11 +1534,14 @@ int rt_terrain_trace_batch(const rt_compute* cams, const rt_compute* scrs, int n
                                 (const float4*)camera_in);
 }
 
-// The prepass one batch ahead: the batch's camerarays prepass on the GPU's
-// side stream, after the last k_order of the batches this device leads (the last read of the
-// CameraResults it overwrites).  Issued before the previous batch's trace, it takes CUs before
-// that trace's persistent k_trace holds them all, and the trace of its own batch
-// (rt_terrain_trace_ahead) starts without a prepass in front of it.
+// The prepass one batch ahead.  For nomadplains on uninstrumented devices the
+// batch is STAGED: its camerarays constants and a frame table go up on the GPU's side stream (after the
+// last k_order of the batches this device leads: the last read of the CameraResults and of the
+// constants), and the next trace on this GPU (rt_terrain_trace_ahead of another batch) runs its
+// prepass inside that trace's persistent k_trace (FusedPrepass): the rays ride on that kernel's
+// throughput instead of a latency-bound launch that waits for its CUs.  Otherwise the prepass itself
+// is queued on the side stream, issued before the previous batch's trace so that it takes CUs before
+// that trace's k_trace holds them all.
 int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int n)
 {
     if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
@@ -1496,6 +1550,12 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
     rt_device lead = scrs[0]->dev;
     if (lead->flags & RT_DEVICE_GRAPH) return fail(RT_ERR_STATE, "the ahead prepass runs on a side stream: not with RT_DEVICE_GRAPH");
     if (lead->ahead_pending) return fail(RT_ERR_STATE, "a prepass is already ahead for this device's batch: trace it first");
+    if (lead->fuse_state == rt_device_s::FUSE_FUSED && lead->ev_fuser_done) {
+        // an earlier fused prepass of this device's frames that no trace consumed: it still writes them
+        HIP_TRY(hipStreamWaitEvent(lead->stream, lead->ev_fuser_done, 0));
+    }
+    fuse_forget(lead);
+    lead->fuse_state = rt_device_s::FUSE_NONE;
     HIP_TRY(hipSetDevice(lead->ordinal));
     hipStream_t side = ahead_stream(lead->ordinal, true);
     if (!side) return fail(RT_ERR_HIP, "side stream");
@@ -1507,6 +1567,8 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
         lead->order_recorded = true;
     }
     HIP_TRY(hipStreamWaitEvent(side, lead->ev_order, 0));
+    const Shader* s0 = scrs[0]->shader;
+    const bool fuse = s0 && s0->landscape == RT_NOMADPLAINS && !(lead->flags & RT_DEVICE_STATS);
     // the batch's devices upload their constants and launch on the side stream for this call
     std::vector<std::pair<rt_device, hipStream_t>> saved;
     for (int f = 0; f < n; ++f) {
@@ -1518,34 +1580,101 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
             d->stream = side;
         }
     }
-    int rc = terrain_render_batch(cams, scrs, n, 0, 1, false, PH_PRE, 0, n, nullptr);
+    int rc = terrain_render_batch(cams, scrs, n, 0, 1, false, fuse ? PH_STAGE : PH_PRE, 0, n, nullptr);
     for (auto& p : saved) p.first->stream = p.second;
     if (rc) return rc;
     HIP_TRY(hipEventRecord(lead->ev_ahead, side));
     lead->ahead_pending = true;
-    for (auto& p : saved) { // every device whose frames it wrote (not the lead alone)
+    lead->ahead_cams.assign(cams, cams + n);
+    lead->fuse_devs.clear();
+    for (auto& p : saved) { // every device whose frames it writes or stages (not the lead alone)
         rt_device d = p.first;
         if (!d->ev_ahead_in) HIP_TRY(hipEventCreateWithFlags(&d->ev_ahead_in, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(d->ev_ahead_in, side));
         d->ahead_in_pending = true;
+        lead->fuse_devs.push_back(d);
     }
-    lead->ahead_cams.assign(cams, cams + n);
+    if (fuse) {
+        lead->fuse_state = rt_device_s::FUSE_STAGED;
+        lead->fuse_n = n;
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        g_fuse_staged[lead->ordinal].push_back(lead);
+    }
     return RT_OK;
 }
 
-// setTargetDepths + tracescreen of a batch whose prepass rt_terrain_prepass_ahead queued; without
-// one (or for other frames, or after a camera constant changed since) the full render_batch
+// setTargetDepths + tracescreen of a batch whose prepass rt_terrain_prepass_ahead queued or staged:
+// after the side-stream prepass, or (fused) with k_order waiting for the rays the previous k_trace
+// computed; a batch that was staged but never fused prepasses in line; without one (or for other
+// frames, or after a camera constant changed since) the full render_batch.  In every case the
+// oldest batch staged on this GPU by another device is fused into this launch's k_trace.
 int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count)
 {
-    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH || !scrs[0]) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
+    if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH || !scrs[0] || !scrs[0]->shader) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
     rt_device lead = scrs[0]->dev;
+    HIP_TRY(hipSetDevice(lead->ordinal));
     bool ahead = lead->ahead_pending && (size_t)n <= lead->ahead_cams.size();
     for (int f = 0; ahead && f < n; ++f)
         ahead = cams[f] == lead->ahead_cams[f] && cams[f]->shader && !cams[f]->shader->cb_dirty;
-    if (!ahead) return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false); // waits for a pending one
-    HIP_TRY(hipStreamWaitEvent(lead->stream, lead->ev_ahead, 0));
+    TraceFuse tf;
+    int phases = PH_PRE | PH_TRACE;
+    const int state = lead->fuse_state;
+    if (ahead && state == rt_device_s::FUSE_FUSED) {
+        // the previous k_trace ran this batch's prepass: k_order polls its ray counter, so the frames'
+        // devices need not wait for that whole kernel (their ahead_in event follows it)
+        tf.wait_ctl = lead->fctl;
+        tf.wait_total = (uint32_t)lead->fuse_n * (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES);
+        for (rt_device d : lead->fuse_devs) d->ahead_in_pending = false;
+        phases = PH_TRACE;
+    } else if (ahead && state == rt_device_s::FUSE_NONE) {
+        HIP_TRY(hipStreamWaitEvent(lead->stream, lead->ev_ahead, 0)); // the side-stream prepass
+        phases = PH_TRACE;
+    }
+    // (STAGED and never fused, or not covered: the full render, in line; a fused prepass this call does
+    // not use is waited for through the frames' ahead_in events, before anything is uploaded)
+    fuse_forget(lead);
+    lead->fuse_state = rt_device_s::FUSE_NONE;
     lead->ahead_pending = false;
-    return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, PH_TRACE);
+    // the next batch: the oldest staged by another device of this GPU that can share this k_trace (its
+    // landscape, noise tables and frame size)
+    rt_device z = nullptr;
+    const Shader* s0 = scrs[0]->shader;
+    if (s0->landscape == RT_NOMADPLAINS && !(lead->flags & (RT_DEVICE_STATS | RT_DEVICE_GRAPH))) {
+        std::lock_guard<std::mutex> lk(g_stream_mu);
+        auto& v = g_fuse_staged[lead->ordinal];
+        for (auto it = v.begin(); it != v.end(); ++it) {
+            rt_device c = *it;
+            const rt_compute cz = c->ahead_cams.empty() ? nullptr : (rt_compute)c->ahead_cams[0];
+            if (c == lead || c->width != lead->width || c->height != lead->height || !cz || !cz->shader ||
+                cz->shader->landscape != RT_NOMADPLAINS || !same_tables(cz->shader, s0))
+                continue;
+            z = c;
+            v.erase(it);
+            break;
+        }
+    }
+    if (z) {
+        // its staged constants and table are up, and its previous k_order (the last poll of its counters,
+        // which this launch's k_order zeroes) is done
+        HIP_TRY(hipStreamWaitEvent(lead->stream, z->ev_ahead, 0));
+        tf.next = FusedPrepass{z->fuse_table.d, z->fctl, (uint32_t)z->fuse_n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+    }
+    int rc = terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, phases, 0, -1, nullptr, nullptr, &tf);
+    if (z) {
+        if (rc) { // not launched: z stays staged (prepasses in line when traced)
+            std::lock_guard<std::mutex> lk(g_stream_mu);
+            g_fuse_staged[z->ordinal].insert(g_fuse_staged[z->ordinal].begin(), z);
+            return rc;
+        }
+        if (!z->ev_fuser_done) HIP_TRY(hipEventCreateWithFlags(&z->ev_fuser_done, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(z->ev_fuser_done, lead->stream));
+        z->fuse_state = rt_device_s::FUSE_FUSED;
+        for (rt_device d : z->fuse_devs) { // a render of z's frames that does not use the fused prepass waits for it
+            HIP_TRY(hipEventRecord(d->ev_ahead_in, lead->stream));
+            d->ahead_in_pending = true;
+        }
+    }
+    return rc;
 }
 
 size_t rt_shard_bytes(rt_device d, int rank, int count)

@@ -1373,3 +1373,87 @@ def test_graph_ring_phase_marks_readable():
     for d, _ in ring.slots:
         assert np.array_equal(d.readback(), gold[GI.frame_key(*spec) + "_rgba8"])
     ring.destroy()
+
+
+# --- the next batch's prepass fused into this batch's k_trace (FusedPrepass, ABI 6) ----------------
+def test_fused_prepass_frame_ring_bitexact():
+    """FrameRing(lookahead=True) on RGBA8 devices (the bench's single-frame companion and --lookahead 1):
+    each batch's camerarays prepass runs inside the previous batch's k_trace as 8-ray tasks, and its
+    k_order waits for the rays.  Over 8 batches of 2 frames, 2 slot groups, cameras alternating per
+    batch: every frame equals its golden frame, and the CameraResults / CellDistance the fused prepass
+    produced equal the golden ones; rt_device_check reports no flag (no k_order wait timed out)."""
+    import gpgpuraytrace_amd as G
+    gold = GI.load()
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]  # nomadplains 64x48, reset / lookdown
+    cams = [(FixedCamera(GI.consts(*GI.unpack(s)[2:4], GI.unpack(s)[1])), GI.frame_key(*s)) for s in specs]
+    w, h = cams[0][0].width, cams[0][0].height
+    ring = G.FrameRing(w, h, depth=2, batch=2, camera=cams[0][0], lookahead=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cams[0][0].c["sun"])
+
+    def set_group(g, c):
+        for _, ter in ring.slots[g * 2:(g + 1) * 2]:
+            ter.set_camera(cams[c][0])
+            ter.update_terrain()
+
+    set_group(0, 0)
+    for b in range(8):
+        if b + 1 < 8:
+            set_group((b + 1) % 2, (b + 1) % 2)  # the next batch's cameras before its prepass is staged
+        ring.render_batch(ahead=b + 1 < 8)
+        if b >= 1:  # the previous batch (the other group) while this one runs
+            key = cams[(b - 1) % 2][1]
+            for dev, ter in ring.slots[((b - 1) % 2) * 2:((b - 1) % 2 + 1) * 2]:
+                assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), (b, key)
+    ring.synchronize()
+    for dev, ter in ring.slots[2:4]:  # batch 7: group 1, camera 1
+        assert np.array_equal(dev.readback(), gold[cams[1][1] + "_rgba8"])
+        assert np.array_equal(_device_cells(ter), gold[cams[1][1] + "_cell_distance"])
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, gold[cams[1][1] + "_camera_results"])
+    for dev, ter in ring.slots[0:2]:  # batch 6: group 0, camera 0 (its prepass fused into batch 5's k_trace)
+        assert np.array_equal(_device_cells(ter), gold[cams[0][1] + "_cell_distance"])
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, gold[cams[0][1] + "_camera_results"])
+    for dev, _ in ring.slots:
+        dev.check()
+    ring.destroy()
+
+
+def test_fused_prepass_camera_change_and_partial_batch():
+    """A batch whose prepass was already fused into the running k_trace gets a new camera before its own
+    trace: it waits for that kernel and prepasses again in line (golden frames of the new camera); a
+    partial batch traces from a fused prepass of the full group; a staged batch traced before any other
+    trace prepasses in line."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]
+    cams = [(FixedCamera(GI.consts(*GI.unpack(s)[2:4], GI.unpack(s)[1])), GI.frame_key(*s)) for s in specs]
+    w, h = cams[0][0].width, cams[0][0].height
+    ring = G.FrameRing(w, h, depth=2, batch=3, camera=cams[0][0], lookahead=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cams[0][0].c["sun"])
+    g0 = [t for _, t in ring.slots[:3]]
+    g1 = [t for _, t in ring.slots[3:]]
+    E.prepass_ahead(g0)            # staged, no trace before its own: in line
+    E.prepass_ahead(g1)            # staged, then fused into g0's k_trace
+    E.trace_ahead(g0)
+    for t in g1:                    # a real camera change after the fusing trace was queued
+        t.set_camera(cams[1][0])
+        t.update_terrain()
+    E.trace_ahead(g1)               # waits for g0's k_trace, prepasses again
+    ring.synchronize()
+    for dev, _ in ring.slots[:3]:
+        assert np.array_equal(dev.readback(), gold[cams[0][1] + "_rgba8"])
+    for dev, _ in ring.slots[3:]:
+        assert np.array_equal(dev.readback(), gold[cams[1][1] + "_rgba8"])
+    E.prepass_ahead(g0)            # g0 fused into g1's next trace, traced as a partial batch of 2
+    E.trace_ahead(g1)
+    E.trace_ahead(g0[:2])
+    ring.synchronize()
+    for dev, _ in ring.slots[:2]:
+        assert np.array_equal(dev.readback(), gold[cams[0][1] + "_rgba8"])
+    for dev, _ in ring.slots:
+        dev.check()
+    ring.destroy()
