@@ -1361,7 +1361,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             March<L, false> st;
             march_begin(cp, st, p, RT_CAMERA_NEAR, 2.0f, dir);
             const SegOctaves<LPR> g = seg_octaves<LPR>(cp, j);
-            __builtin_amdgcn_s_setprio(3); // latency-bound: the next batch's k_order waits for these rays
+            __builtin_amdgcn_s_setprio(RT_FUSE_PRIO); // latency-bound: the next batch's k_order waits for these rays
             while (march_live<L, false, true>(cp, st, RT_CAMERA_FAR, 0)) {
                 auto dens = [&](f3 q0) {
                     uint32_t used;

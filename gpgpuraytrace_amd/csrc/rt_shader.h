@@ -10,6 +10,7 @@
 
 #include "rt_math.h"
 #include "rt_types.h"
+#include "rt_variants.h"
 
 namespace rts {
 
@@ -317,7 +318,20 @@ template <bool FAST>
 __device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
 {
     float s = 0.0f;
-#ifndef RT_EXTRA_OCTAVE
+#if RT_OCT_SMEM && !defined(RT_EXTRA_OCTAVE)
+    // The octave constants by scalar loads from the launch's constant block: every lane inside the loop
+    // is at the same octave N, so N is uniform (an SGPR), and the loop reads no LDS for them (4 LDS-array
+    // cycles of ~40 per octave; rt_variants.h RT_OCT_SMEM)
+    const KPtr kc = (KPtr)c.k;
+    int N = 1;
+    #pragma unroll 1
+    do {
+        count_noise(c.nz);
+        const float sx = kc->np_scale[N], sy = kc->np_scale_y[N], w = kc->np_rcp[N];
+        s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * sx, q0.y * sy, q0.z * sx)), w, s);
+        ++N;
+    } while (N <= n_oct);
+#elif !defined(RT_EXTRA_OCTAVE)
     // The octave-table pointer is the trip counter: a per-lane register from the start (the asm
     // keeps it out of SGPRs, which would cost a v_mov per iteration for the LDS address), one
     // v_add and one v_cmp against the lane's end per octave.  n_oct >= 2, so a do-while is exact.

@@ -54,6 +54,17 @@
 #ifndef RT_LDS_SLOTS
 #define RT_LDS_SLOTS 16
 #endif
+// nomadplains FBM octave constants: 1 = scalar loads from the launch's constant block (every lane in
+// the octave loop is at the same octave), 0 = a ds_read_b128 of the LDS octave table per octave.  The
+// scalar form takes 4 of ~40 LDS-array cycles per octave off the CU's LDS (62% busy on k_trace):
+// +1.0% Mray/s same box (profiles/r04/oct_smem_ab.txt)
+#ifndef RT_OCT_SMEM
+#define RT_OCT_SMEM 1
+#endif
+// wave priority (s_setprio) of a fused prepass task (FusedPrepass) while it marches
+#ifndef RT_FUSE_PRIO
+#define RT_FUSE_PRIO 3
+#endif
 // k_order: RT_ORDER_BATCH forces the batch-wide (1) or frame-major (0) unit order; -1 = automatic
 // (batch-wide below kOrderBatchUnitsPerWave units per wave slot)
 #ifndef RT_ORDER_BATCH

@@ -12,3 +12,4 @@ BENCH_ARGS="--steps 20 --warmup 5 --lookahead 1" bash scripts/ab_bench.sh RT_LIB
 BENCH_ARGS="--steps 20 --warmup 5 --lookahead 0" bash scripts/ab_bench.sh RT_LIB_VARIANT= RT_LIB_VARIANT= || exit 1
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r4c5/bench.json 2> gpurun_out/r4c5/bench.err || { tail -20 gpurun_out/r4c5/bench.err; exit 1; }
 python3 -c "import json;d=json.load(open('gpurun_out/r4c5/bench.json'));c=d['config'];print(d['value'],d['roofline']['frac'],d['roofline'].get('traffic_per_frame_vs_rgba8'),c['single_frame']['primary_plus_shadow_mrays'],c['noise_lane_utilisation'],c['timed_capture_check'],c['parity']['timed_frames_all_equal'])"
+BENCH_ARGS="--steps 20 --warmup 5" bash scripts/ab_bench.sh RT_LIB_VARIANT=octsmem RT_LIB_VARIANT= RT_LIB_VARIANT=octsmem RT_LIB_VARIANT= || exit 1
