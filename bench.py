@@ -87,7 +87,7 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="batches (slot groups, one HIP stream each) kept in flight; 1 = one batch at a time")
     ap.add_argument("--batch", type=int, default=12,
-                    help="max frames per rt_terrain_render_batch launch sequence (1..16); the --steps frames are "
+                    help="max frames per rt_terrain_render_batch launch sequence (1..24); the --steps frames are "
                          "split into ceil(steps / batch) batches of near-equal size")
     ap.add_argument("--split-prepass", type=int, default=0,
                     help="N>1: 1 = each rank runs the prepass of B/N frames of a batch and an all-gather shares "
@@ -212,7 +212,7 @@ def traffic_child(a):
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
     euler = G.camera.INITIAL_ROTATION_EULER if a.pose == "reset" else G.camera.LOOKDOWN_ROTATION_EULER
-    B = max(1, min(16, a.batch))
+    B = max(1, min(24, a.batch))
     ring = E.FrameRing(a.width, a.height, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     for _ in range(2):
@@ -345,7 +345,7 @@ def main():
 
     euler = G.camera.INITIAL_ROTATION_EULER if a.pose == "reset" else G.camera.LOOKDOWN_ROTATION_EULER
     W, H = a.width, a.height
-    sizes = batch_sizes(a.steps, max(1, min(16, a.batch)))
+    sizes = batch_sizes(a.steps, max(1, min(24, a.batch)))
     B = sizes[0]
     n_full = sum(1 for s in sizes if s == B)
 

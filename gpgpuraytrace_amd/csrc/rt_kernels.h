@@ -17,7 +17,7 @@ enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_T
 // one sequence of launches (rt_terrain_render_batch).  Each frame keeps its own constant
 // block (camera, sun), CameraResults, CellDistance and framebuffer; the kernels find them
 // through this table in device memory.  A single frame is a batch of one.
-#define RT_MAX_BATCH 16
+#define RT_MAX_BATCH 24
 struct FrameTable {
     const RtConsts* k[RT_MAX_BATCH];    // tracescreen's constant block
     const RtConsts* kcam[RT_MAX_BATCH]; // camerarays' constant block (its own cbuffers)

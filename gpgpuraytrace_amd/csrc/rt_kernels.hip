@@ -1695,7 +1695,7 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
         // one LPR-lane group per ray.  A block holds the noise tables (one block per CU), so
         // a batch packs more rays per block to keep every frame's prepass in one dispatch
         // round: 8 rays of 32 lanes (256 threads) up to 2 frames, 16 up to 4, and beyond 64
-        // rays of 8 lanes (512 threads, <= 256 blocks for <= 16 frames).  Fewer lanes per ray
+        // rays of 8 lanes (512 threads, <= 256 blocks for <= 16 frames; 4 lanes up to 24 frames).  Fewer lanes per ray
         // lengthen a step (3 noise rounds instead of 1) but keep a 12-frame prepass in one
         // round: 1.4 -> 0.7 ms per batch, +1.8% at C3 (32 rays of 32 lanes took two rounds).
         auto go = [&](auto bs_tag, auto lpr_tag) {
@@ -1713,7 +1713,8 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
         using L32 = std::integral_constant<int, 32>;
         if (n <= 2) go(C256{}, L32{});
         else if (n <= 4) go(C512{}, L32{});
-        else go(C512{}, std::integral_constant<int, 8>{}); // 64 rays of 16 lanes per 1024 threads: same
+        else if (n <= 16) go(C512{}, std::integral_constant<int, 8>{}); // 64 rays of 16 lanes per 1024 threads: same
+        else go(C512{}, std::integral_constant<int, 4>{}); // > 16 frames: 128 rays of 4 lanes, <= 192 blocks for 24
         return;
     }
     dim3 grid(RT_CAMERA_RES * RT_CAMERA_RES / 64, n), block(64);

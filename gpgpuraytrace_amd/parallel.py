@@ -100,8 +100,8 @@ class BatchPlan:
     CAMERA_FLOATS = 1024 * 4  # CameraResults of one frame: float4[1024]
 
     def __init__(self, width, height, batch, world, split_prepass=False, lookahead=False):
-        if not 1 <= batch <= 16:
-            raise ValueError("batch must be 1..16 frames (RT_MAX_BATCH)")
+        if not 1 <= batch <= 24:
+            raise ValueError("batch must be 1..24 frames (RT_MAX_BATCH)")
         self.width, self.height, self.batch, self.world = int(width), int(height), int(batch), int(world)
         self.split_prepass = bool(split_prepass) and self.world > 1
         # the ahead prepass is the unsplit one's (the split one is gathered before its trace)

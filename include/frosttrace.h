@@ -209,7 +209,7 @@ int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank
  * copies it (1024 x float4: hit xyz, depth) to `camera_results`. */
 int rt_terrain_render_feed(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
 int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
-/* rt_terrain_render_batch: rt_terrain_render for n (1..16) frames at once -- frame i is
+/* rt_terrain_render_batch: rt_terrain_render for n (1..24; 16 before ABI 6) frames at once -- frame i is
  * (camera_cs[i], screen_cs[i]), each with its own constants (camera, sun), CameraResults,
  * CellDistance and device framebuffer.  All frames must share one GPU, resolution,
  * landscape, macro set and noise tables.  Every frame's prepass runs in one launch, and one

@@ -262,7 +262,7 @@ def test_batch_plan_bookkeeping():
     assert P.BatchPlan(64, 48, 3, 3).max_bytes == 2 * 32 * 32 * 4  # shards of 2, 1, 1 tiles
     assert P.frame_shard(5, 0, 1) == 0
     with pytest.raises(ValueError):
-        P.BatchPlan(64, 48, 17, 2)
+        P.BatchPlan(64, 48, 25, 2)  # RT_MAX_BATCH 24 (ABI 6)
 
 
 def test_phase_summary_leaves_out_unreadable_pairs():

@@ -787,7 +787,7 @@ def _check_frames(frames, specs):
         assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), key
 
 
-@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("n", [2, 3, 5, 8, 17, 24])
 def test_batch_mixed_cameras_bitexact(n):
     """n frames of two cameras in one batch (hits and long rays of different frames share
     the kernel's shading batches and rings): every frame equals its golden frame, and the
