@@ -89,7 +89,7 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, ui
 #define RT_TILE 32
 #define RT_FIN_SLOTS 1536 // k_trace's fin pool slots per block
 // k_trace's queue capacities per block (1024 threads = 16 waves): the hit queue and the long-ray
-// spill ring.  A wave starts a primary unit only while fewer than 64 hits are queued and starts
+// spill stack.  A wave starts a primary unit only while fewer than 64 hits are queued and starts
 // shading only while fewer than 128 long rays are (k_trace's work priority), so a block never
 // queues more than 64 + 16 * 64 * aa hits or 128 + 16 * 64 * (1 + ao) long rays plus 16 compaction
 // hand-backs of < 64: the rings cannot fill.

@@ -844,7 +844,7 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
 // per-block LDS lock.  Every hand-off stays on one CU: the producer's global stores
 // (hit records, fin) complete (s_waitcnt) before the push publishes them, and the consumer
 // reads them with L1-bypassing loads from the XCD's L2.  A full long ring spills to the block's
-// spill ring in HBM (the same block consumes it, so the hand-off stays on one CU like the LDS
+// spill stack in HBM (the same block consumes it, so the hand-off stays on one CU like the LDS
 // ring's own): a block never hands work to another kernel.
 constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 KiB plane + the ring
 // A block's fin pool: slots of FinRec<L>::N float4 in HBM for the finishing inputs of its long
@@ -883,12 +883,8 @@ struct TraceQueues {
     uint32_t active;  // waves inside a primary unit or a shading batch (they may still push)
     uint32_t drained; // the global unit queue is exhausted
     uint32_t pad;
-    union { // the block's long-ray spill ring (HBM)
-        struct {
-            uint32_t ls_head, ls_tail;
-        };
-        uint64_t ls_ht;
-    };
+    uint32_t ls_top; // the block's long-ray spill stack (HBM, long_spill_cap records): [0, ls_top) queued
+    uint32_t pad1;
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
     float4 longs[kLongRing * kShadowRec];
@@ -964,7 +960,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.l_head = q.l_tail = 0;
         q.active = 0;
         q.drained = 0;
-        q.ls_head = q.ls_tail = 0;
+        q.ls_top = 0;
         q.f_top = fin_slots;
         q.overflow = 0;
         if constexpr (STATS) s_st = BlockStats{};
@@ -976,13 +972,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     if constexpr (STATS) c.nz.lds_calls = (__attribute__((address_space(3))) unsigned long long*)&s_st.v[BlockStats::NOISE];
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
-    // this block's hit stack and long-ray spill ring (hit_cap / long_spill_cap records per block)
+    // this block's hit stack and long-ray spill stack (hit_cap / long_spill_cap records per block)
     constexpr uint32_t HR = HitRec<L>::N;
     float4* const hq = hitq + (size_t)blockIdx.x * hit_cap * HR;
     float4* const finp = finpool + (size_t)blockIdx.x * kFinSlots * FinRec<L>::N;
     float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
-    // queued work of the block: long rays in the LDS ring + spill ring, hits in the hit queue
-    auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_tail) - vload(q.ls_head); };
+    // queued work of the block: long rays in the LDS ring + spill stack, hits in the hit queue
+    auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_top); };
     auto queued_hits = [&]() { return vload(q.h_top); };
     // STATS: march steps and hits go to the block's LDS counters (no VGPRs held across the loops)
     auto stat = [&](int i, uint32_t v) {
@@ -994,7 +990,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     WT(unsigned long long wt[RT_WT_FIELDS] = {}; wt[10] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
-    // block's spill ring when the LDS ring is full (stored before the tail publishes them)
+    // block's spill stack when the LDS ring is full (stored before the tail publishes them)
     auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
@@ -1005,15 +1001,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
         } else {
-            // the spill ring's bound (rt_spill_caps) holds by the work priorities; a push past it is
+            // the spill stack's bound (rt_spill_caps) holds by the work priorities; a push past it is
             // dropped and flagged (rt_device_check), never written over queued rays
-            const uint64_t ht = vload(q.ls_ht); // (tail << 32) | head, one LDS read
-            const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(ht >> 32));
-            const bool fits = stl - (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ht) + n <= long_spill_cap;
-            if (want && fits) long_pack(st, t, aux, lspill + (size_t)((stl + rank) % long_spill_cap) * kShadowRec);
+            const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane(vload(q.ls_top));
+            const bool fits = stl + n <= long_spill_cap;
+            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec);
             __builtin_amdgcn_s_waitcnt(0);
             if (lane == 0) {
-                q.ls_tail = fits ? stl + n : stl;
+                q.ls_top = fits ? stl + n : stl;
                 q.overflow |= fits ? 0u : RT_FLAG_SPILL_OVERFLOW;
             }
         }
@@ -1057,9 +1052,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
-                // the block's spill ring tops up what the LDS ring cannot give
-                const uint32_t sh = vload(q.ls_head), sl = vload(q.ls_tail);
-                const uint32_t more = (sl - sh) < nidle - take ? (sl - sh) : nidle - take;
+                // the block's spill stack tops up what the LDS ring cannot give (from its top)
+                const uint32_t sl = vload(q.ls_top);
+                const uint32_t more = sl < nidle - take ? sl : nidle - take;
                 const uint32_t rank = lane_rank(idle);
                 const bool mine = ((idle >> lane) & 1ull) && rank < take + more;
                 auto take_ray = [&](float4 r0, float4 r1, float4 r2) {
@@ -1073,12 +1068,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
                     take_ray(r[0], r[1], r[2]);
                 } else if (mine) {
-                    const uint32_t ri = ((sh + rank - take) % long_spill_cap) * kShadowRec;
+                    const uint32_t ri = (sl - more + rank - take) * kShadowRec;
                     take_ray(ld_rec(lspill, ri), ld_rec(lspill, ri + 1u), ld_rec(lspill, ri + 2u));
                 }
+                if (more) __builtin_amdgcn_s_waitcnt(0); // the spill records are read before a push reuses them
                 if (lane == 0) {
                     q.l_head = head + take;
-                    q.ls_head = sh + more;
+                    q.ls_top = sl - more;
                 }
                 q_unlock(&q.lock, lane);
             }
@@ -1128,8 +1124,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             q_lock(&q.lock, lane);
             const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
             const uint32_t take = (tail - head) < RPW ? (tail - head) : RPW;
-            const uint32_t sh = vload(q.ls_head), sl = vload(q.ls_tail);
-            const uint32_t more = (sl - sh) < RPW - take ? (sl - sh) : RPW - take;
+            const uint32_t sl = vload(q.ls_top);
+            const uint32_t more = sl < RPW - take ? sl : RPW - take;
             if (grp < take + more) { // every lane of the segment unpacks the same record
                 float4 r0, r1, r2;
                 if (grp < take) {
@@ -1138,7 +1134,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     r1 = r[1];
                     r2 = r[2];
                 } else {
-                    const uint32_t ri = ((sh + grp - take) % long_spill_cap) * kShadowRec;
+                    const uint32_t ri = (sl - more + grp - take) * kShadowRec;
                     r0 = ld_rec(lspill, ri);
                     r1 = ld_rec(lspill, ri + 1u);
                     r2 = ld_rec(lspill, ri + 2u);
@@ -1152,7 +1148,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
             if (lane == 0) {
                 q.l_head = head + take;
-                q.ls_head = sh + more;
+                q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
@@ -1765,7 +1761,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue,
                        a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
-    // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill rings
+    // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill stacks
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];

@@ -117,7 +117,7 @@ struct rt_device_s {
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
     float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
-    float4* hitq = nullptr;       // k_trace's per-block hit queues and long-ray spill rings (rt_spill_caps per block)
+    float4* hitq = nullptr;       // k_trace's per-block hit queues and long-ray spill stacks (rt_spill_caps per block)
     float4* spill_long = nullptr;
     size_t hitq_n = 0, spill_long_n = 0; // records allocated (all blocks)
     uint32_t* order = nullptr;
@@ -524,7 +524,7 @@ int check_texture(Shader* s)
 // Per-sample buffers: per AA sample of every whole 32x32 tile, one shaded colour (16 B; 12 B used
 // with one sample per pixel), the shading inputs of a long shadow ray (48 B; 32 B used without
 // fog), an AO occlusion count (1 B) and a hit bit (the 64-lane ballot per 8x8 unit and AA sample).
-// Per block (one per CU): k_trace's hit stack (hit records of up to 48 B) and long-ray spill ring
+// Per block (one per CU): k_trace's hit stack (hit records of up to 48 B) and long-ray spill stack
 // (48 B records), rt_spill_caps records each, and its fin pool (RT_FIN_SLOTS records of up to 48 B).
 int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
 {
@@ -902,7 +902,7 @@ int rt_device_check(rt_device d)
     HIP_TRY(hipMemset(reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 0, 4));
     return fail(RT_ERR_STATE, "device flags 0x%x:%s%s%s", flags,
                 (flags & RT_FLAG_HIT_OVERFLOW) ? " k_trace hit stack overflow (a push past rt_spill_caps' bound was dropped)" : "",
-                (flags & RT_FLAG_SPILL_OVERFLOW) ? " k_trace long-ray spill ring overflow" : "",
+                (flags & RT_FLAG_SPILL_OVERFLOW) ? " k_trace long-ray spill stack overflow" : "",
                 (flags & RT_FLAG_PREPASS_TIMEOUT) ? " k_order timed out waiting for a fused prepass" : "");
 }
 
