@@ -5,12 +5,13 @@
 
 #include "rt_types.h"
 
-// work counters (one 64-byte block, zeroed by k_order before every k_trace), then the device's
-// sticky flags (zeroed at device creation and by rt_device_check only): a k_trace queue push that
-// would exceed its bound raises a flag instead of storing (rt_spill_caps)
-enum { RT_CTR_PRIMARY = 0 };
-#define RT_CTR_BYTES 64
-#define RT_QUEUE_BYTES 128
+// work counters (one 128-byte block, zeroed by k_order before every k_trace: the unit queue, then one
+// first-unit counter per wave slot of a k_trace block), then the device's sticky flags (zeroed at
+// device creation and by rt_device_check only): a k_trace queue push that would exceed its bound
+// raises a flag instead of storing (rt_spill_caps)
+enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1 };
+#define RT_CTR_BYTES 128
+#define RT_QUEUE_BYTES 192
 enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_TIMEOUT = 4u };
 
 // A frame batch: up to RT_MAX_BATCH frames of one resolution, landscape and shard traced by

@@ -315,11 +315,13 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask)
 }
 
 // Per-sample RayResult of the primary march: 3 float4 (pd, fcolord, density).
-// the unit index a wave takes first: wave-slot-major over the grid, see k_trace
-__device__ __forceinline__ uint32_t first_unit_index()
+// the unit index a wave takes first: wave-slot-major over the grid (row w holds order indices
+// w * blocks .. w * blocks + blocks - 1, and wave slot w of each block takes the next one of its row in
+// the order the blocks START), see k_trace
+__device__ __forceinline__ uint32_t first_unit_index(uint32_t* __restrict__ counters, uint32_t lane)
 {
-    // wave-uniform: computed in scalar registers, so no VGPR has to carry threadIdx to the first unit
-    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) * gridDim.x + blockIdx.x;
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    return w * gridDim.x + wave_fetch(&counters[RT_CTR_FIRST + w], lane);
 }
 
 // A hit's record in its block's hit queue (the shading input; misses store none): the primary
@@ -929,6 +931,8 @@ template <int L>
 struct TraceThreads {
     static constexpr uint32_t value = 64u * ((L == RT_GREENROCKS || L == RT_SIMPLE) ? RT_TRACE_WAVES_WIDE : RT_TRACE_WAVES_FAST);
 };
+static_assert(RT_CTR_FIRST + RT_TRACE_WAVES_FAST <= RT_CTR_BYTES / 4 && RT_CTR_FIRST + RT_TRACE_WAVES_WIDE <= RT_CTR_BYTES / 4,
+              "a first-unit counter per wave slot inside the zeroed work counters");
 
 template <int L, bool STATS>
 __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
@@ -1469,12 +1473,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         c.nz.calls = cf.nz.calls;
     };
 
-    // First unit of every wave is dealt statically, wave-slot-major (wave w of block b takes
-    // order index w * blocks + b): the costliest units (k_order puts them first) land one per
-    // SIMD instead of filling the first few CUs' SIMDs four deep, which sets the frame time
-    // when there are barely more units than waves (an 8-way shard has ~4k units for 4k waves).
+    // First unit of every wave is dealt wave-slot-major (wave slot w takes the next order index of row
+    // w, w * blocks + j, j counted in the order the blocks start): the costliest units (k_order puts
+    // them first) land one per SIMD instead of filling the first few CUs' SIMDs four deep, which sets
+    // the frame time when there are barely more units than waves (an 8-way shard has ~4k units for 4k
+    // waves); and a block that starts late (its CU still held by the other batch's k_trace tail, a
+    // copy or a collective kernel) takes the cheapest units of each row, not a fixed set of the costliest.
     const uint32_t n_static = gridDim.x * (blockDim.x >> 6);
-    const uint32_t first_qi = first_unit_index(); // scalar, formed before the loop
+    const uint32_t first_qi = first_unit_index(counters, lane); // scalar, formed before the loop
     bool first_unit = true;
     bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
@@ -1748,6 +1754,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.n_frames = a.n_frames;
     m.frame_samples = m.n_units * 64u * (uint32_t)a.aa;
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
+    // a shard (N > 1) may leave CUs to the transport of the other batch in flight (rt_variants.h)
+    if (stride > 1u && blocks > 2u * RT_SHARD_RESERVE_CUS) blocks -= RT_SHARD_RESERVE_CUS;
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     m.order_batch = RT_ORDER_BATCH >= 0 ? (uint32_t)RT_ORDER_BATCH

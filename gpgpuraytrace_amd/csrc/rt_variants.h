@@ -65,6 +65,11 @@
 #ifndef RT_FUSE_PRIO
 #define RT_FUSE_PRIO 3
 #endif
+// a sharded k_trace (N > 1) leaves this many CUs without a block, so that the other batch in flight's
+// k_finish, shard pack, RCCL gather and unpack find a CU while it runs (instead of queueing behind it)
+#ifndef RT_SHARD_RESERVE_CUS
+#define RT_SHARD_RESERVE_CUS 0
+#endif
 // k_order: RT_ORDER_BATCH forces the batch-wide (1) or frame-major (0) unit order; -1 = automatic
 // (batch-wide below kOrderBatchUnitsPerWave units per wave slot)
 #ifndef RT_ORDER_BATCH

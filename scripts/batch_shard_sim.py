@@ -53,6 +53,16 @@ def main():
                     help="diagnostic: K torch streams kept busy-free but alive (HW queue sharing study)")
     ap.add_argument("--gather-us", type=float, default=40.0,
                     help="modelled all-gather latency per batch (16 KiB per frame over xGMI)")
+    ap.add_argument("--transport-us", type=float, default=0.0,
+                    help="N > 1: after each batch, on its stream, bench.py's transport as a stand-in: the rank's "
+                         "rt_shard_pack_batch, a one-block spin kernel of this many us for the RCCL gather (it "
+                         "needs a CU like RCCL's kernels do; 200 us ~ rank 0 receiving 7 x 10 frames' shards "
+                         "over xGMI), and rank 0's rt_shard_unpack_batch of the other ranks' (N-1) x B shards")
+    ap.add_argument("--gate", type=int, default=0,
+                    help="with --transport-us: each batch's prepass (rt_terrain_prepass_batch) is queued at once, its "
+                         "trace (rt_terrain_trace_batch) after an event recorded behind the previous batch's pack, "
+                         "so the previous batch's finish and pack run before this k_trace takes the CUs and its "
+                         "gather finds a CU beside it")
     a = ap.parse_args()
     if a.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)  # before HIP starts (torch below)
@@ -78,7 +88,52 @@ def main():
             G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
         torch.cuda.synchronize()
 
+        plan_n = {}
+
+        def transport(r, n):
+            from gpgpuraytrace_amd import parallel as P
+            if n == 1 or a.transport_us <= 0:
+                return
+            if n not in plan_n:
+                plan = P.BatchPlan(W, H, B, n)
+                plan_n[n] = (plan, [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0")
+                                    for _ in range(a.depth)])
+                torch.cuda.synchronize()
+            plan, packed = plan_n[n]
+            g = ((ring.frame - B) // B) % ring.depth  # the batch just queued
+            grp = ring.slots[g * B:(g + 1) * B]
+            devs = [d for d, _ in grp]
+            base = packed[g].data_ptr()
+            items = plan.packs(r)
+            G.engine.shard_pack_batch([devs[f] for f, _, _ in items], [s for _, s, _ in items], n,
+                                      [base + off for _, _, off in items])
+            with torch.cuda.stream(torch.cuda.ExternalStream(devs[0].stream(), device="cuda:0")):
+                if a.gate:
+                    gate[0] = torch.cuda.Event()
+                    gate[0].record()
+                torch.cuda._sleep(int(a.transport_us * 2400))  # clock64 ticks ~2.4 per ns (tests: 50e6 ~ 20 ms)
+            if r == 0:
+                ups = plan.unpacks()
+                G.engine.shard_unpack_batch([devs[f] for _, f, _, _ in ups], [s for _, _, s, _ in ups], n,
+                                            [base + off for _, _, _, off in ups])
+
         def step(r, n, ahead=True):
+            step_(r, n, ahead)
+            transport(r, n)
+
+        gate = [None]
+
+        def step_(r, n, ahead=True):
+            if a.gate and n > 1 and not a.split_prepass and not a.no_prepass:
+                g = (ring.frame // B) % ring.depth
+                grp = ring.slots[g * B:(g + 1) * B]
+                ters = [t for _, t in grp]
+                G.engine.prepass_batch(ters, 0, B, bufs[g].data_ptr())
+                if gate[0] is not None:
+                    grp[0][0].wait_event(gate[0].cuda_event)
+                G.engine.trace_batch(ters, r, n, bufs[g].data_ptr())
+                ring.frame += B
+                return
             if a.no_prepass:
                 g = (ring.frame // B) % ring.depth
                 G.engine.trace_batch([t for _, t in ring.slots[g * B:(g + 1) * B]], r, n, bufs[g].data_ptr())
@@ -110,6 +165,7 @@ def main():
             if base is None:
                 base = worst
             print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "no_prepass": a.no_prepass,
+                              "transport_us": a.transport_us, "gate": a.gate,
                               "lookahead": int(ring.lookahead), "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()
