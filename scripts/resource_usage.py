@@ -1,12 +1,14 @@
-"""Per-kernel VGPR / scratch / occupancy / LDS of the HIP kernels (compile-time report)."""
+"""Per-kernel VGPR / scratch / occupancy / LDS of the HIP kernels (compile-time report).
+usage: python3 scripts/resource_usage.py [-DKNOB=value ...]  (an A/B build's rt_variants.h overrides)"""
 import os
 import re
 import subprocess
+import sys
 
 CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpgpuraytrace_amd", "csrc")
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
        "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-fast-math", "--cuda-device-only", "-c", "rt_kernels.hip",
-       "-o", "/tmp/rt_kernels_dev.o", "-Rpass-analysis=kernel-resource-usage"]
+       "-o", "/tmp/rt_kernels_dev.o", "-Rpass-analysis=kernel-resource-usage"] + sys.argv[1:]
 out = subprocess.run(cmd, cwd=CSRC, capture_output=True, text=True).stderr
 rows, cur = [], None
 for line in out.splitlines():
