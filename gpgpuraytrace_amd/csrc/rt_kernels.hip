@@ -336,7 +336,9 @@ __device__ __forceinline__ uint32_t first_unit_index(uint32_t* __restrict__ coun
 // per block stays in L2, 64 KiB per block is written back on every pass).
 template <int L>
 struct HitRec {
-    static constexpr uint32_t N = FogLive<L>::value ? 3u : 1u; // float4 per record
+    // float4 per record (RT_DIAG_HITPAD: a fog-free record padded to 2 with a zero float4, to see what the
+    // hit stack's bytes cost in HBM writes)
+    static constexpr uint32_t N = FogLive<L>::value ? 3u : (RT_DIAG_HITPAD ? 2u : 1u);
 };
 template <int L>
 __device__ __forceinline__ void hit_store(float4* __restrict__ r, uint32_t t, const RayResult& rr)
@@ -347,6 +349,7 @@ __device__ __forceinline__ void hit_store(float4* __restrict__ r, uint32_t t, co
         r[2] = make_float4(rr.density, rr.steps, 0.0f, __uint_as_float(t));
     } else {
         r[0] = make_float4(rr.sd, rr.pd.w, rr.density, __uint_as_float(t));
+        if constexpr (RT_DIAG_HITPAD) r[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
 }
 

@@ -89,6 +89,10 @@
 #ifndef RT_DIAG_SKIP
 #define RT_DIAG_SKIP 0
 #endif
+// RT_DIAG_HITPAD=1        fog-free hit records padded from 16 to 32 B (the hit stack's HBM write cost)
+#ifndef RT_DIAG_HITPAD
+#define RT_DIAG_HITPAD 0
+#endif
 #ifdef RT_WAVE_TRACE
 #define RT_WT_FIELDS 21
 #define RT_WT_MAX_WAVES 8192

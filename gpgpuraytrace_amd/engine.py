@@ -524,7 +524,7 @@ class Terrain:
 
 
 def render_batch(terrains, shard_rank=0, shard_count=1):
-    """rt_terrain_render_batch: Terrain.render_device for up to 16 Terrains at once (one GPU,
+    """rt_terrain_render_batch: Terrain.render_device for up to 24 Terrains at once (RT_MAX_BATCH) (one GPU,
     one resolution, landscape, macro set and noise).  Each frame lands in its own Device's
     framebuffer; the work is enqueued on the first terrain's device stream and the others'
     streams wait for it."""
