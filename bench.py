@@ -792,8 +792,8 @@ def main():
                 # the timed batch's noise3d lane-calls / (64 x their wave iterations): SIMD lane
                 # utilisation of the noise work, counted by the instrumented kernels
                 "noise_lane_utilisation": round(counts["noise_lane_util"], 4) if counts["noise_lane_util"] else None,
-                "noise_lane_utilisation_scope": "instrumented (STATS) kernels: they march a unit's last rays on "
-                                                "64 lanes, the product kernels on lane segments (k_trace primary_seg)",
+                "noise_lane_utilisation_scope": "instrumented (STATS) kernels, which take the product's code paths "
+                                                "(the primary segment tail included: RT_STATS_PRIMARY_SEG)",
                 "parallelism": "single GPU" if world == 1 else (
                     f"tile-cyclic 32x32 shards x{world} (rotated per frame) + RCCL gather per batch"
                     + (" + prepass split over ranks (RCCL all-gather of CameraResults)" if plan.split_prepass
