@@ -38,6 +38,7 @@ at N=1 only; its frame is also compared with the GPU's: config.parity).
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -206,6 +207,11 @@ def cpu_baseline(consts, landscape, max_steps, ao, row_step, row_step_1t, thread
 TRAFFIC_KERNELS = ("k_order", "k_trace", "k_finish")
 
 
+def instrumented_kernel(name):
+    """The STATS instantiations (k_trace<L, true, ...>, k_camerarays_group<true, ...>): not the timed path."""
+    return re.match(r"k_trace<\d+, true|k_camerarays_group<true", name) is not None
+
+
 def traffic_child(a):
     """--traffic-child: what the PMC passes profile: two B-frame batches, one in flight (the first
     warms up; the second is the launch measured)."""
@@ -260,7 +266,7 @@ def measure_traffic(a, B):
                 return None, f"rocprofv3 --pmc {counter}: {len(orders)} tracescreen launches in the trace"
             last = orders[len(orders) // 2]  # k_order of the second (measured) launch; one workgroup per frame
             kib[counter] = sum(v for (d, n), v in per.items()
-                               if d >= last and n.startswith(TRAFFIC_KERNELS) and "true" not in n)
+                               if d >= last and n.startswith(TRAFFIC_KERNELS) and not instrumented_kernel(n))
     except (subprocess.TimeoutExpired, OSError, KeyError, ValueError) as e:
         return None, f"traffic pass failed: {type(e).__name__}: {e}"
     finally:

@@ -574,9 +574,11 @@ __device__ __forceinline__ void ao_count(uint32_t* __restrict__ aocc, uint32_t t
 {
     atomicAdd(&aocc[t >> 2], 1u << ((t & 3u) * 8u));
 }
+// UnitMap::fit with AO: a sample k_finish finishes carries kFinFlag in its byte (plain stores, k_trace)
+constexpr uint32_t kFinFlag = 0x80u;
 __device__ __forceinline__ uint32_t ao_occluded(const uint32_t* __restrict__ aocc, uint32_t t)
 {
-    return (aocc[t >> 2] >> ((t & 3u) * 8u)) & 0xffu;
+    return (aocc[t >> 2] >> ((t & 3u) * 8u)) & 0x7fu;
 }
 
 struct ShadeHit {
@@ -707,6 +709,13 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, fl
 // (< kFinSlots), or at fin[t] when the pool was empty (kAuxFinT).
 constexpr uint32_t kAuxAO = 0xffffffffu, kAuxAOCand = 0x80000000u, kAuxFinT = 0x7ffffffeu;
 __device__ __forceinline__ bool aux_ao(uint32_t aux) { return (int32_t)aux < 0; }
+// With AO_SAMPLES >= 2 (RT_AO_CHAIN) a hit's AO rays march one after another on one lane: kAuxChain |
+// k << 8 | occluded so far.  The record carries the hit's normal and shadow stepmod (the next ray's
+// start) in place of the direction, which is formed again from them (ao_chain_dir); the last ray
+// stores the count, one plain byte store per hit instead of a device atomic per occluded ray (a
+// device-scope atomic costs a 32-B HBM write on gfx950, in L2 or not: scripts/ubench_atomic.hip).
+constexpr uint32_t kAuxChain = 0xa0000000u;
+__device__ __forceinline__ bool aux_chain(uint32_t aux) { return (aux & 0xf0000000u) == kAuxChain; }
 
 // Long-ray record (48 B): (p, dist), (step, aux, iters, t), (shadow fog | AO dir; a fog-free
 // landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
@@ -715,11 +724,12 @@ __device__ __forceinline__ bool aux_ao(uint32_t aux) { return (int32_t)aux < 0; 
 // ray is live, so its next step overwrites d before anything reads it; nor is lastStep, which only
 // the refinement after a hit reads (tracing.hlsl:76-79) and SKIPREFINE rays break before it.
 template <int L>
-__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t aux, float4* r)
+__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t aux, float4* r, float4 chain)
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
     r[1] = make_float4(st.step, __uint_as_float(aux), __uint_as_float((uint32_t)st.iters), __uint_as_float(t));
-    if (aux_ao(aux)) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
+    if (aux_chain(aux)) r[2] = chain; // (normal, stepmod): ao_chain_dir
+    else if (aux_ao(aux)) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
     else if constexpr (March<L, true>::FOG) r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
     // no fog: a shadow ray's f is +0 throughout (march_step), so r2 is neither written nor read
 }
@@ -755,6 +765,22 @@ template <int L>
 __device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32_t kk, March<L, true>& st)
 {
     march_begin(c, st, h.hp, 0.4f, h.prec, ao_dir(h.n, h.px, h.py, h.a, kk), false);
+}
+
+// AO ray kk of sample t's hit with normal n, as ao_begin formed its direction (unnormalised: march_begin
+// normalises it; ao_chain_unit: the normalised direction a marching chain ray carries)
+__device__ __forceinline__ f3 ao_chain_dir(const RtConsts* k, const UnitMap& m, uint32_t t, f3 n, uint32_t kk)
+{
+    const uint32_t f = frame_of(m, t);
+    uint32_t px, py, a;
+    sample_pixel(m, m.frame_rot ? f : 0u, t - f * m.frame_samples, (uint32_t)k->aa_samples, (uint32_t)k->width,
+                 (uint32_t)k->height, &px, &py, &a);
+    return ao_dir(n, px, py, a, kk);
+}
+__device__ __forceinline__ f3 ao_chain_unit(const RtConsts* k, const UnitMap& m, uint32_t t, f3 n, uint32_t kk)
+{
+    const f3 d = ao_chain_dir(k, m, t, n, kk);
+    return rtm::scale(d, rtm::rcp(rtm::length(d)));
 }
 
 // The inputs a long shadow ray needs to finish its sample: (albedo + specular, brightness), fcolord
@@ -807,7 +833,11 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
     if (aux_ao(aux)) {
         if (st.d > 0.0f) {
             if (aux == kAuxAO) {
-                if (!(RT_DIAG_SKIP & 8)) ao_count(aocc, t);
+                // fit: the hit's one AO ray, after the shading's kFinFlag store (ordered by the push)
+                if (m.fit) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)(kFinFlag | 1u);
+                // one AO ray per hit: its count has one writer, a plain byte store (no device atomic)
+                else if (k->ao_samples == 1) reinterpret_cast<uint8_t*>(aocc)[late(t)] = 1u;
+                else if (!(RT_DIAG_SKIP & 8)) ao_count(aocc, t);
             } else if (!(RT_DIAG_SKIP & 2)) {
                 fit_store(k, m, fr, t, aux | 0xff000000u);
             }
@@ -868,6 +898,8 @@ constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSe
 // still marching, they continue as segments of 64 / kPrimarySeg lanes per ray (primary_seg in
 // k_trace) instead of keeping 64 lanes on a few rays' octave loops.  0: off.
 constexpr uint32_t kPrimarySeg = RT_PRIMARY_SEG;
+// AO_SAMPLES >= 2: a hit's AO rays as one chain on a lane (kAuxChain); 0: independent rays, atomic counts
+constexpr bool kAoChainBuild = RT_AO_CHAIN != 0;
 static_assert(kPrimarySeg == 0u || kPrimarySeg == 4u || kPrimarySeg == 8u || kPrimarySeg == 16u, "lanes per ray");
 // The instrumented (STATS) kernels take the same segment tail (their counters cost registers there:
 // they spill, the product does not), so their march and noise counts pass through the product's code.
@@ -937,7 +969,9 @@ struct TraceThreads {
 static_assert(RT_CTR_FIRST + RT_TRACE_WAVES_FAST <= RT_CTR_BYTES / 4 && RT_CTR_FIRST + RT_TRACE_WAVES_WIDE <= RT_CTR_BYTES / 4,
               "a first-unit counter per wave slot inside the zeroed work counters");
 
-template <int L, bool STATS>
+// CHAIN: AO_SAMPLES >= 2 with RT_AO_CHAIN (a separate instantiation: the chain state costs registers the
+// one-AO-ray configurations do not carry)
+template <int L, bool STATS, bool CHAIN>
 __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
@@ -952,6 +986,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                                                 uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots,
                                                 FusedPrepass np)
 {
+    constexpr bool kAoChain = CHAIN; // AO chains (ao_chain_next), AO_SAMPLES >= 2 only
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
     __shared__ __attribute__((aligned(16))) uint32_t
@@ -998,21 +1033,21 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
     // block's spill stack when the LDS ring is full (stored before the tail publishes them)
-    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
+    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux, float4 chain) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
         const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
         if (lt - lh + n <= long_ring_cap) {
-            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
+            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec], chain);
             if (lane == 0) q.l_tail = lt + n;
         } else {
             // the spill stack's bound (rt_spill_caps) holds by the work priorities; a push past it is
             // dropped and flagged (rt_device_check), never written over queued rays
             const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane(vload(q.ls_top));
             const bool fits = stl + n <= long_spill_cap;
-            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec);
+            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec, chain);
             __builtin_amdgcn_s_waitcnt(0);
             if (lane == 0) {
                 q.ls_top = fits ? stl + n : stl;
@@ -1036,6 +1071,20 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if (lane == 0) q.f_top = top + (uint32_t)__popcll(pb);
     };
 
+    // an AO chain's ray left the march (AO_SAMPLES >= 2): the hit's next AO ray starts in its place
+    // (true), or the last one stores the hit's occluded count, one byte that only this lane writes, and
+    // the chain ends (false); `store`: this lane writes (one lane of a segment)
+    auto ao_chain_next = [&](March<L, true>& st, uint32_t t, uint32_t& aux, const float4& chain, bool store = true) {
+        const uint32_t kk = ((aux >> 8) & 15u) + 1u, occ = (aux & 255u) + (st.d > 0.0f ? 1u : 0u);
+        if (kk < (uint32_t)k->ao_samples) {
+            march_begin(c, st, st.p, 0.4f, chain.w, ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), kk), false);
+            aux = kAuxChain | (kk << 8) | occ;
+            return true;
+        }
+        if (store && occ != 0u) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ;
+        return false;
+    };
+
     // ---- a batch of long rays, lane refill from the ring ----
     auto do_shadow = [&]() {
         March<L, true> st;
@@ -1043,14 +1092,20 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         st.iters = 0;
         bool live = false;
         uint32_t t = 0, aux = kAuxAO; // aux: the lane's ray (long_pack); on an idle lane, a fin slot to free
+        float4 chain = make_float4(0.0f, 0.0f, 0.0f, 0.0f); // an AO chain's (normal, stepmod)
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
-            if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
-                long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
+            // a ray that left the march finishes, or (an AO chain) the hit's next AO ray starts in its place
+            while (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
-                live = false;
                 stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                if (kAoChain && aux_chain(aux)) {
+                    if (ao_chain_next(st, t, aux, chain)) continue; // the chain's next ray, or its count stored
+                } else {
+                    long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
+                }
+                live = false;
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
@@ -1069,6 +1124,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     const float* fr = s_fr.v[frame_of(m, t)];
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                     if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                    if (kAoChain && aux_chain(aux)) {
+                        chain = r2;
+                        st.dir = ao_chain_unit(k, m, t, rtm::mk(r2.x, r2.y, r2.z), (aux >> 8) & 15u);
+                    }
                     live = true;
                 };
                 if (mine && rank < take) {
@@ -1100,7 +1159,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     free_fin_locked(live, aux);
                     q_unlock(&q.lock, lane);
                 }
-                if (hand_back) push_long(live, st, t, aux);
+                if (hand_back) push_long(live, st, t, aux, chain);
                 c.nz.calls = cl.nz.calls;
                 return;
             }
@@ -1125,6 +1184,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             st.d = 0.0f;
             st.iters = 0;
             uint32_t t = 0, aux = kAuxAO;
+            float4 chain = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             bool live = false;
             Ctx cl = c;
             cl.nz.phase = RT_PHASE_LONG;
@@ -1150,6 +1210,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 const float* fr = s_fr.v[frame_of(m, t)];
                 cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                 if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+                if (kAoChain && aux_chain(aux)) {
+                    chain = r2;
+                    st.dir = ao_chain_unit(k, m, t, rtm::mk(r2.x, r2.y, r2.z), (aux >> 8) & 15u);
+                }
                 live = true;
             }
             __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
@@ -1160,10 +1224,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             q_unlock(&q.lock, lane);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
             for (;;) {
-                if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
-                    if (j == 0u) {
+                // every lane of the segment holds the same ray: all of them start a chain's next AO ray
+                while (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
+                    if (j == 0u) stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                    if (kAoChain && aux_chain(aux)) {
+                        if (ao_chain_next(st, t, aux, chain, j == 0u)) continue;
+                    } else if (j == 0u) {
                         long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
-                        stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
                     }
                     live = false;
                 }
@@ -1320,20 +1387,32 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (more && !(RT_DIAG_SKIP & 16)) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
             }
         });
-        // fit with AO: the hits whose long shadow races their AO ray are k_finish's (their bit in the
-        // unit's hitmask word t >> 6, zero from the unit)
-        if (m.fit && k->ao_samples && valid && more) atomicOr((unsigned long long*)&hitmask[t >> 6], 1ull << (t & 63u));
+        // fit with AO: the hits whose long shadow races their AO ray are k_finish's.  Plain stores, no
+        // atomics (a device-scope atomic costs a 32-B HBM write on gfx950, L2 or not:
+        // scripts/ubench_atomic.hip): the sample's aocc byte becomes kFinFlag (its AO ray adds 1 if
+        // occluded) and the unit's hitmask word, zero from the unit, becomes nonzero (every writer
+        // stores the same value)
+        if (m.fit && k->ao_samples && valid && more) {
+            reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)kFinFlag;
+            hitmask[t >> 6] = 1ull;
+        }
         if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // the fin record is in L2 before the ray is visible
-            push_long(more, st, t, aux);
+            push_long(more, st, t, aux, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
         }
         // AO extension: the hit's AO rays start as long rays (fit: after its unoccluded pixel is stored,
         // which an occluded AO ray overwrites)
         if (m.fit) __builtin_amdgcn_s_waitcnt(0);
-        for (int kk = 0; kk < k->ao_samples; ++kk) {
+        if (kAoChain && k->ao_samples >= 2) { // the first AO ray of the hit's chain (ao_chain_next)
             March<L, true> ao;
-            if (valid) ao_begin(c, h, (uint32_t)kk, ao);
-            push_long(valid, ao, t, ao_aux);
+            if (valid) ao_begin(c, h, 0u, ao);
+            push_long(valid, ao, t, kAuxChain, make_float4(h.n.x, h.n.y, h.n.z, h.prec));
+        } else {
+            for (int kk = 0; kk < k->ao_samples; ++kk) {
+                March<L, true> ao;
+                if (valid) ao_begin(c, h, (uint32_t)kk, ao);
+                push_long(valid, ao, t, ao_aux, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            }
         }
     };
 
@@ -1594,8 +1673,15 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         float4* out32 = ft->out32[f];
         uint32_t px, py;
         if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
-        // one sample per pixel: k_trace wrote the misses' pixels, only the hits remain
-        if (aa == 1u && !((hitmask[f * m.n_units + u] >> lane) & 1ull)) continue;
+        // one sample per pixel: k_trace wrote the misses' pixels, only the hits remain (fit: only the
+        // units whose hitmask word is nonzero, and in them the samples flagged kFinFlag)
+        if (m.fit) {
+            if (hitmask[f * m.n_units + u] == 0ull) continue;
+            const uint32_t t = f * m.frame_samples + u * 64u + lane;
+            if (!((aocc[t >> 2] >> ((t & 3u) * 8u)) & kFinFlag)) continue; // (its word is cleared by a flagged lane or is 0)
+        } else if (aa == 1u && !((hitmask[f * m.n_units + u] >> lane) & 1ull)) {
+            continue;
+        }
         float c0 = 0.0f, c1 = 0.0f, c2 = 0.0f;
         for (uint32_t a = 0; a < aa; ++a) {
             const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
@@ -1773,10 +1859,10 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                        a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill stacks
-    auto primary = [&](auto stats_tag) {
-        constexpr bool S = decltype(stats_tag)::value;
+    auto primary = [&](auto stats_tag, auto chain_tag) {
+        constexpr bool S = decltype(stats_tag)::value, CH = decltype(chain_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
+        hipLaunchKernelGGL((k_trace<L, S, CH>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
                            a.perm2d, a.grad, m,
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
@@ -1785,8 +1871,14 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
         if (!(m.fit && a.ao_samples == 0))
             hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
-    if (a.stats) primary(std::true_type{});
-    else primary(std::false_type{});
+    const bool chain = kAoChainBuild && a.ao_samples >= 2;
+    if (a.stats) {
+        if (chain) primary(std::true_type{}, std::true_type{});
+        else primary(std::true_type{}, std::false_type{});
+    } else {
+        if (chain) primary(std::false_type{}, std::true_type{});
+        else primary(std::false_type{}, std::false_type{});
+    }
 }
 
 } // namespace

@@ -10,12 +10,12 @@ for v in "$@"; do
   RT_LIB_VARIANT=$v timeout -k 10 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
     --output-format csv -d $O/$tag -o run -- python3 scripts/with_variant.py bench.py --steps 10 --warmup 1 --no-cpu-baseline --traffic off --no-companions --frames-in-flight 1 > $O/$tag.log 2>&1 || { echo "pmc $tag failed"; exit 1; }
   python3 - $O/$tag $tag <<'PY'
-import csv, glob, sys, collections
+import csv, glob, re, sys, collections
 per = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-        if n.startswith("k_trace") and "true" not in n:
+        if n.startswith("k_trace") and not re.match(r"k_trace<\d+, true", n):
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
 d = {c: sum(x[c] for x in per.values()) / len(per) for c in next(iter(per.values()))}
 cyc = d["GRBM_GUI_ACTIVE"] / 8

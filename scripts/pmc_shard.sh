@@ -9,12 +9,12 @@ for n in 1 8; do
   timeout -k 10 240 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
     --output-format csv -d $O/n$n -o run -- python3 scripts/batch_shard_sim.py --batches 10 --frames 20 --ns $n --ranks first > $O/n$n.log 2>&1 || { echo "pmc n$n failed"; tail -3 $O/n$n.log; exit 1; }
   python3 - $O/n$n $n <<'PY'
-import csv, glob, sys, collections
+import csv, glob, re, sys, collections
 per = collections.defaultdict(lambda: collections.defaultdict(float))
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         nm = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-        if nm.startswith("k_trace") and "true" not in nm:
+        if nm.startswith("k_trace") and not re.match(r"k_trace<\d+, true", nm):
             per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
 n = int(sys.argv[2])
 d = {c: sum(x[c] for x in per.values()) / len(per) for c in next(iter(per.values()))}

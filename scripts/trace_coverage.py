@@ -6,6 +6,7 @@ they wait for CUs that the other batch's persistent k_trace holds.
   python3 scripts/trace_coverage.py <kernel_trace.csv> <out.md> [title]
 """
 import csv
+import re
 import sys
 from collections import defaultdict
 
@@ -20,7 +21,7 @@ def main(path, out, title="kernel trace"):
     per = defaultdict(list)
     for s, e, n in ev:
         per[n].append((e - s) / 1e6)
-    tr = [(s, e) for s, e, n in ev if n.startswith("k_trace") and "true" not in n]
+    tr = [(s, e) for s, e, n in ev if n.startswith("k_trace") and not re.match(r"k_trace<\d+, true", n)]
     # the throughput loop: the longest stretch of k_trace launches separated by less than 2 ms
     # (the bench's warm-up, roofline and stats passes are separated by host work)
     runs, run = [], [tr[0]]
