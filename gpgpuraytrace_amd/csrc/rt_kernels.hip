@@ -1093,30 +1093,39 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         bool live = false;
         uint32_t t = 0, aux = kAuxAO; // aux: the lane's ray (long_pack); on an idle lane, a fin slot to free
         float4 chain = make_float4(0.0f, 0.0f, 0.0f, 0.0f); // an AO chain's (normal, stepmod)
+        bool fresh = false; // a chain ray just taken: its direction is still to be formed
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
-            // a ray that left the march finishes, or (an AO chain) the hit's next AO ray starts in its place
+            // a ray that left the march finishes; an AO chain's lane waits (`fresh`) for its next ray
             while (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
                 if (kAoChain && aux_chain(aux)) {
-                    if (ao_chain_next(st, t, aux, chain)) continue; // the chain's next ray, or its count stored
+                    const uint32_t kk = ((aux >> 8) & 15u) + 1u, occ = (aux & 255u) + (st.d > 0.0f ? 1u : 0u);
+                    if (kk < (uint32_t)k->ao_samples) {
+                        aux = kAuxChain | (kk << 8) | occ;
+                        fresh = true;
+                    } else if (occ != 0u) {
+                        reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ; // this lane's hit only
+                    }
                 } else {
                     long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                 }
                 live = false;
             }
-            const uint64_t idle = __ballot(!live);
-            const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= refill_idle && queued_long() != 0u) {
+            const uint32_t nidle = (uint32_t)__popcll(__ballot(!live));
+            bool start = nidle >= refill_idle; // the chains' next rays start with a refill (lanes batched)
+            if (start && queued_long() != 0u) {
+                const uint64_t idle = __ballot(!live && !fresh);
+                const uint32_t nfree = (uint32_t)__popcll(idle);
                 q_lock(&q.lock, lane);
                 free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
-                const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
+                const uint32_t take = (tail - head) < nfree ? (tail - head) : nfree;
                 // the block's spill stack tops up what the LDS ring cannot give (from its top)
                 const uint32_t sl = vload(q.ls_top);
-                const uint32_t more = sl < nidle - take ? sl : nidle - take;
+                const uint32_t more = sl < nfree - take ? sl : nfree - take;
                 const uint32_t rank = lane_rank(idle);
                 const bool mine = ((idle >> lane) & 1ull) && rank < take + more;
                 auto take_ray = [&](float4 r0, float4 r1, float4 r2) {
@@ -1125,8 +1134,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                     if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     if (kAoChain && aux_chain(aux)) {
-                        chain = r2;
-                        st.dir = ao_chain_unit(k, m, t, rtm::mk(r2.x, r2.y, r2.z), (aux >> 8) & 15u);
+                        chain = r2; // its direction is formed after the lock is released
+                        fresh = true;
                     }
                     live = true;
                 };
@@ -1144,7 +1153,23 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 }
                 q_unlock(&q.lock, lane);
             }
-            const uint64_t lv = __ballot(live);
+            uint64_t lv = __ballot(live);
+            if (lv == 0ull) start = true; // nothing else marches: the waiting chains go on now
+            if (kAoChain && start && __ballot(fresh)) {
+                // chain rays taken from the ring get their direction, waiting chains their next ray:
+                // one pass for every such lane (the direction is a hash and a basis, ao_dir)
+                if (fresh) {
+                    const f3 d = ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u);
+                    if (live) {
+                        st.dir = rtm::scale(d, rtm::rcp(rtm::length(d)));
+                    } else {
+                        march_begin(c, st, st.p, 0.4f, chain.w, d, false);
+                        live = true;
+                    }
+                    fresh = false;
+                }
+                lv = __ballot(live);
+            }
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
@@ -1153,6 +1178,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) // after the drain: few rays go to segment waves
                 hand_back = hand_back || (drained_now && lv != 0ull && (uint32_t)__popcll(lv) <= kSegHandBack &&
                                           queued_long() == 0u);
+            if (kAoChain && hand_back && __ballot(fresh)) { // waiting chains go back with the others: start them
+                if (fresh) {
+                    march_begin(c, st, st.p, 0.4f, chain.w,
+                                ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u), false);
+                    live = true;
+                    fresh = false;
+                }
+            }
             if (lv == 0ull || hand_back) {
                 if (__ballot(!live && aux < kFinSlots)) {
                     q_lock(&q.lock, lane);
@@ -1210,10 +1243,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 const float* fr = s_fr.v[frame_of(m, t)];
                 cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                 if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
-                if (kAoChain && aux_chain(aux)) {
-                    chain = r2;
-                    st.dir = ao_chain_unit(k, m, t, rtm::mk(r2.x, r2.y, r2.z), (aux >> 8) & 15u);
-                }
+                if (kAoChain && aux_chain(aux)) chain = r2;
                 live = true;
             }
             __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
@@ -1222,6 +1252,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
+            if (kAoChain && live && aux_chain(aux)) // outside the lock
+                st.dir = ao_chain_unit(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
             for (;;) {
                 // every lane of the segment holds the same ray: all of them start a chain's next AO ray

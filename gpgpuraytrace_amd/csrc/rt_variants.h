@@ -39,7 +39,7 @@
 // AO_SAMPLES >= 2: a hit's AO rays march as one chain on a lane, its occluded count stored once (1), or
 // as independent rays counted by device atomics (0)
 #ifndef RT_AO_CHAIN
-#define RT_AO_CHAIN 1
+#define RT_AO_CHAIN 0
 #endif
 // the instrumented (STATS) kernels take the product's primary segment tail too (1), so their march and
 // noise counts are asserted through the timed kernel's code path; 0 keeps a 64-lane tail there
