@@ -716,6 +716,13 @@ __device__ __forceinline__ bool aux_ao(uint32_t aux) { return (int32_t)aux < 0; 
 // device-scope atomic costs a 32-B HBM write on gfx950, in L2 or not: scripts/ubench_atomic.hip).
 constexpr uint32_t kAuxChain = 0xa0000000u;
 __device__ __forceinline__ bool aux_chain(uint32_t aux) { return (aux & 0xf0000000u) == kAuxChain; }
+// With AO_SAMPLES >= 2 (and no chains) a hit's AO rays count their occlusion in a slot of the block's AO
+// counters in LDS (kAuxAOSlot | slot, TraceQueues::ao_ctr): the ray that completes the count stores it,
+// one plain byte store per hit; an idle lane holding kAuxSlotFree | slot returns the slot to the free list
+// at its wave's next refill.  No free slot: the hit's rays count by device atomics (kAuxAO).
+constexpr uint32_t kAuxAOSlot = 0xc0000000u, kAuxSlotFree = 0x60000000u;
+__device__ __forceinline__ bool aux_ao_slot(uint32_t aux) { return (aux & 0xff000000u) == kAuxAOSlot; }
+__device__ __forceinline__ bool aux_slot_free(uint32_t aux) { return (aux & 0xff000000u) == kAuxSlotFree; }
 
 // Long-ray record (48 B): (p, dist), (step, aux, iters, t), (shadow fog | AO dir; a fog-free
 // landscape's shadow leaves the third float4 unwritten).  A shadow ray's direction is SunDirection /
@@ -887,6 +894,11 @@ constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 Ki
 // are the same lines over and over and stay in the XCD's L2 (fin[t] instead: a sparse write and a
 // re-fetch per long shadow).  An empty pool falls back to fin[t].
 constexpr uint32_t kFinSlots = RT_FIN_SLOTS;
+// AO counter slots per block (AO_SAMPLES >= 2; the LDS the ring and the tables leave)
+constexpr uint32_t kAoSlots = RT_AO_SLOTS;
+// AO_SAMPLES >= 2: shading batches reserve LDS ring room for the long rays they push (RT_SHADE_RESERVE)
+constexpr bool kShadeReserve = RT_SHADE_RESERVE != 0;
+static_assert(kAoSlots % 2u == 0u && kAoSlots <= 256u, "AO slots: pairs of u16 counters, u8 indices");
 constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a wave switch to them
 constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
 // After the unit queue drains (nomadplains): a long-ray wave left with at most kSegHandBack live rays
@@ -923,9 +935,13 @@ struct TraceQueues {
     uint32_t ls_top; // the block's long-ray spill stack (HBM, long_spill_cap records): [0, ls_top) queued
     uint32_t pad1;
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
+    uint32_t l_res;            // LDS ring slots reserved by shading batches in progress (AO_SAMPLES >= 2)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
+    uint32_t ao_ctr[kAoSlots / 2]; // AO slot s: bits 16 (s & 1) + 0..4 rays finished, + 5..9 occluded
+    uint8_t ao_free[kAoSlots];     // free AO slots: ao_free[0, ao_top)
+    uint32_t ao_top;
 };
 
 // A fresh read of a ring field another wave may have written: a relaxed workgroup-scope atomic
@@ -1004,10 +1020,16 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.drained = 0;
         q.ls_top = 0;
         q.f_top = fin_slots;
+        q.l_res = 0;
         q.overflow = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
+    for (uint32_t i = threadIdx.x; i < kAoSlots; i += blockDim.x) {
+        q.ao_free[i] = (uint8_t)i;
+        if (i < kAoSlots / 2u) q.ao_ctr[i] = 0u;
+    }
+    if (threadIdx.x == 0) q.ao_top = kAoSlots;
     load_noise_lds(lds, perm2d, grad, k);
     const uint32_t lane = __lane_id(); // v_mbcnt of constants: rematerialisable (threadIdx & 63 spilled)
     Ctx c = make_ctx(k, lds); // k: frame-invariant constants (per-frame ones: frame_ctx / s_fr)
@@ -1062,13 +1084,41 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     auto free_fin_locked = [&](bool live, uint32_t& aux) {
         const bool pend = !live && aux < kFinSlots;
         const uint64_t pb = __ballot(pend);
-        if (!pb) return;
-        const uint32_t top = vload(q.f_top);
-        if (pend) {
-            q.fin_free[top + lane_rank(pb)] = (uint16_t)aux;
+        if (pb) {
+            const uint32_t top = vload(q.f_top);
+            if (pend) {
+                q.fin_free[top + lane_rank(pb)] = (uint16_t)aux;
+                aux = kAuxAO;
+            }
+            if (lane == 0) q.f_top = top + (uint32_t)__popcll(pb);
+        }
+        if constexpr (kAoSlots > 0u) { // and the AO slots of completed counts
+            const bool pa = !live && aux_slot_free(aux);
+            const uint64_t ab = __ballot(pa);
+            if (ab) {
+                const uint32_t top = vload(q.ao_top);
+                if (pa) {
+                    q.ao_free[top + lane_rank(ab)] = (uint8_t)(aux & 255u);
+                    aux = kAuxAO;
+                }
+                if (lane == 0) q.ao_top = top + (uint32_t)__popcll(ab);
+            }
+        }
+    };
+    // an AO ray with a counter slot left the march: count it; the ray that completes the hit's count stores
+    // it (one byte that only this lane writes), clears the slot and keeps it to free (kAuxSlotFree)
+    auto ao_slot_finish = [&](const March<L, true>& st, uint32_t t, uint32_t& aux) {
+        const uint32_t sl = aux & 255u, sh = (sl & 1u) * 16u;
+        const uint32_t occ1 = st.d > 0.0f ? 1u : 0u;
+        const uint32_t old = atomicAdd(&q.ao_ctr[sl >> 1], (1u | (occ1 << 5)) << sh) >> sh;
+        if ((old & 31u) + 1u == (uint32_t)k->ao_samples) {
+            const uint32_t occ = ((old >> 5) & 31u) + occ1;
+            if (occ != 0u) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ;
+            atomicAnd(&q.ao_ctr[sl >> 1], ~(0xffffu << sh));
+            aux = kAuxSlotFree | sl;
+        } else {
             aux = kAuxAO;
         }
-        if (lane == 0) q.f_top = top + (uint32_t)__popcll(pb);
     };
 
     // an AO chain's ray left the march (AO_SAMPLES >= 2): the hit's next AO ray starts in its place
@@ -1109,6 +1159,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     } else if (occ != 0u) {
                         reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ; // this lane's hit only
                     }
+                } else if (kAoSlots > 0u && aux_ao_slot(aux)) {
+                    ao_slot_finish(st, t, aux);
                 } else {
                     long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                 }
@@ -1187,7 +1239,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 }
             }
             if (lv == 0ull || hand_back) {
-                if (__ballot(!live && aux < kFinSlots)) {
+                if (__ballot(!live && (aux < kFinSlots || aux_slot_free(aux)))) {
                     q_lock(&q.lock, lane);
                     free_fin_locked(live, aux);
                     q_unlock(&q.lock, lane);
@@ -1261,6 +1313,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     if (j == 0u) stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
                     if (kAoChain && aux_chain(aux)) {
                         if (ao_chain_next(st, t, aux, chain, j == 0u)) continue;
+                    } else if (kAoSlots > 0u && aux_ao_slot(aux)) {
+                        if (j == 0u) ao_slot_finish(st, t, aux);
                     } else if (j == 0u) {
                         long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                     }
@@ -1283,7 +1337,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             }
             // the segments' finished shadows return their fin pool slots (one lane per segment holds it)
             uint32_t fa = j == 0u ? aux : kAuxAO;
-            if (__ballot(fa < kFinSlots)) {
+            if (__ballot(fa < kFinSlots || aux_slot_free(fa))) {
                 q_lock(&q.lock, lane);
                 free_fin_locked(false, fa);
                 q_unlock(&q.lock, lane);
@@ -1440,6 +1494,17 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (valid) ao_begin(c, h, 0u, ao);
             push_long(valid, ao, t, kAuxChain, make_float4(h.n.x, h.n.y, h.n.z, h.prec));
         } else {
+            if (kAoSlots > 0u && k->ao_samples >= 2) { // a counter slot per hit, popped from the free list
+                const uint64_t vb = __ballot(valid);
+                if (vb) {
+                    q_lock(&q.lock, lane);
+                    const uint32_t top = vload(q.ao_top), n = (uint32_t)__popcll(vb), rank = lane_rank(vb);
+                    const uint32_t got = n < top ? n : top;
+                    if (valid && rank < got) ao_aux = kAuxAOSlot | (uint32_t)q.ao_free[top - 1u - rank];
+                    if (lane == 0) q.ao_top = top - got;
+                    q_unlock(&q.lock, lane);
+                }
+            }
             for (int kk = 0; kk < k->ao_samples; ++kk) {
                 March<L, true> ao;
                 if (valid) ao_begin(c, h, (uint32_t)kk, ao);
@@ -1629,9 +1694,29 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             continue;
         }
         if (hp >= 64u || (drained && hp > 0u)) {
+            // AO_SAMPLES >= 2: a batch pushes up to 64 x (1 + AO) long rays; it starts only once the LDS
+            // ring has room for them beside what other shading batches reserved, so its pushes do not go to
+            // the spill stack (HBM) (an empty ring always takes one batch: progress for any AO count)
+            const uint32_t need = kShadeReserve && k->ao_samples >= 2 ? 64u * (1u + (uint32_t)k->ao_samples) : 0u;
+            if (need) {
+                q_lock(&q.lock, lane);
+                const uint32_t used = vload(q.l_tail) - vload(q.l_head) + vload(q.l_res);
+                const bool ok = used == 0u || used + need <= long_ring_cap;
+                if (lane == 0 && ok) q.l_res = vload(q.l_res) + need;
+                q_unlock(&q.lock, lane);
+                if (!ok) { // the ring is taken: march long rays meanwhile
+                    do_shadow();
+                    continue;
+                }
+            }
             if (lane == 0) atomicAdd(&q.active, 1u);
             do_shade();
             if (lane == 0) atomicSub(&q.active, 1u);
+            if (need) {
+                q_lock(&q.lock, lane);
+                if (lane == 0) q.l_res = vload(q.l_res) - need;
+                q_unlock(&q.lock, lane);
+            }
             WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }

@@ -41,6 +41,15 @@
 #ifndef RT_AO_CHAIN
 #define RT_AO_CHAIN 0
 #endif
+// AO counter slots per k_trace block in LDS (AO_SAMPLES >= 2 without chains; 0: device atomics count)
+#ifndef RT_AO_SLOTS
+#define RT_AO_SLOTS 256
+#endif
+// AO_SAMPLES >= 2: a shading batch starts only when the LDS ring has room for its long rays (1), or
+// whenever fewer than RT_LONG_BATCH long rays are queued (0)
+#ifndef RT_SHADE_RESERVE
+#define RT_SHADE_RESERVE 1
+#endif
 // the instrumented (STATS) kernels take the product's primary segment tail too (1), so their march and
 // noise counts are asserted through the timed kernel's code path; 0 keeps a 64-lane tail there
 #ifndef RT_STATS_PRIMARY_SEG
