@@ -48,7 +48,7 @@
 // AO_SAMPLES >= 2: a shading batch starts only when the LDS ring has room for its long rays (1), or
 // whenever fewer than RT_LONG_BATCH long rays are queued (0)
 #ifndef RT_SHADE_RESERVE
-#define RT_SHADE_RESERVE 1
+#define RT_SHADE_RESERVE 0
 #endif
 // the instrumented (STATS) kernels take the product's primary segment tail too (1), so their march and
 // noise counts are asserted through the timed kernel's code path; 0 keeps a 64-lane tail there

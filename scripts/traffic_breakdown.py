@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -73,7 +74,7 @@ def main():
         # tracescreen kernels from its k_order on
         cam = max((d for d, n, _ in per if n.startswith("k_camerarays") and d < last), default=last)
         for (d, n, c), v in per.items():
-            if "true" in n or not n.startswith(KERNELS):
+            if re.match(r"k_trace<\d+, true|k_camerarays_group<true", n) or not n.startswith(KERNELS):  # STATS kernels
                 continue
             if d >= last or d == cam:
                 kk = n.split("<")[0]
