@@ -62,6 +62,8 @@ struct RtLaunch {
     int fit;                  // hit pixels finish in k_trace (aa 1, <= 1 AO ray, no float output; UnitMap::fit)
     float4* fin;              // 3 float4 per sample: shading inputs a long shadow ray needs to finish
     float4* finpool;          // the same per block in a pool of RT_FIN_SLOTS slots of 3 float4 (fin is the fallback)
+    float4* cpool;            // per block RT_AO_POOL_SLOTS colours: a multi-AO hit's colour for its last AO ray (fitm)
+    int fitm;                 // hit pixels without a long shadow finish in k_trace with >= 2 AO rays (UnitMap::fitm)
     uint32_t* aocc;           // per sample: occluded AO rays (AO extension), a byte each, 4 per word
     int ao_samples;           // AO rays per primary hit (0 = off)
     int aa;                   // AA samples per pixel
@@ -89,6 +91,7 @@ void rt_launch_tracescreen(const RtLaunch& a, uint32_t off_x, uint32_t off_y, ui
 
 #define RT_TILE 32
 #define RT_FIN_SLOTS 1536 // k_trace's fin pool slots per block
+#define RT_AO_POOL_SLOTS 256 // k_trace's AO counter slots per block (LDS) and their colours (cpool)
 // k_trace's queue capacities per block (1024 threads = 16 waves): the hit queue and the long-ray
 // spill stack.  A wave starts a primary unit only while fewer than 64 hits are queued and starts
 // shading only while fewer than 128 long rays are (k_trace's work priority), so a block never

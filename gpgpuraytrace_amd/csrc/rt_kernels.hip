@@ -276,6 +276,11 @@ struct UnitMap {
     // where their last ray ends (fit_pixel), and k_finish only finishes the hits whose long shadow and
     // AO ray race (their bit in hitmask); with no AO, no k_finish at all
     uint32_t fit;
+    // 1: one sample per pixel, no float output, >= 2 AO rays per hit: a hit whose shadow ends at its first
+    // step (no long shadow) keeps its colour in its block's colour pool beside its AO counter slot, and the
+    // AO ray that completes the count stores the pixel (fitm in k_trace); the rest go through k_finish,
+    // flagged as with fit
+    uint32_t fitm;
 };
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
@@ -898,7 +903,8 @@ constexpr uint32_t kFinSlots = RT_FIN_SLOTS;
 constexpr uint32_t kAoSlots = RT_AO_SLOTS;
 // AO_SAMPLES >= 2: shading batches reserve LDS ring room for the long rays they push (RT_SHADE_RESERVE)
 constexpr bool kShadeReserve = RT_SHADE_RESERVE != 0;
-static_assert(kAoSlots % 2u == 0u && kAoSlots <= 256u, "AO slots: pairs of u16 counters, u8 indices");
+static_assert(kAoSlots % 2u == 0u && kAoSlots <= 256u && kAoSlots <= RT_AO_POOL_SLOTS,
+              "AO slots: pairs of u16 counters, u8 indices, a colour each in the pool");
 constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a wave switch to them
 constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a dry wave hands its rays back
 // After the unit queue drains (nomadplains): a long-ray wave left with at most kSegHandBack live rays
@@ -994,6 +1000,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                                                 UnitMap m, const uint32_t* __restrict__ order,
                                                 uint64_t* __restrict__ hitmask, float4* __restrict__ samples,
                                                 float4* __restrict__ fin, float4* __restrict__ finpool,
+                                                float4* __restrict__ cpool,
                                                 float4* __restrict__ hitq,
                                                 float4* __restrict__ spill_long, uint32_t hit_cap,
                                                 uint32_t long_spill_cap,
@@ -1040,6 +1047,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     constexpr uint32_t HR = HitRec<L>::N;
     float4* const hq = hitq + (size_t)blockIdx.x * hit_cap * HR;
     float4* const finp = finpool + (size_t)blockIdx.x * kFinSlots * FinRec<L>::N;
+    float4* const cpl = cpool + (size_t)blockIdx.x * RT_AO_POOL_SLOTS; // fitm: the AO slots' hit colours
     float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
     // queued work of the block: long rays in the LDS ring + spill stack, hits in the hit queue
     auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_top); };
@@ -1113,7 +1121,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         const uint32_t old = atomicAdd(&q.ao_ctr[sl >> 1], (1u | (occ1 << 5)) << sh) >> sh;
         if ((old & 31u) + 1u == (uint32_t)k->ao_samples) {
             const uint32_t occ = ((old >> 5) & 31u) + occ1;
-            if (occ != 0u) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ;
+            if (m.fitm && !(old & (1u << 10))) { // no long shadow: the pixel, from the colour the shading left
+                const float4 v = ld_rec(cpl, sl);
+                const uint32_t at = __float_as_uint(v.w);
+                if (!(RT_DIAG_SKIP & 2)) gptr(s_fr.out8[at >> 23])[at & 0x7fffffu] = fit_pixel(v, ao_factor(occ, k->ao_samples));
+            } else if (occ != 0u) { // k_finish's count (fitm: after the shading's kFinFlag)
+                reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)((m.fitm ? kFinFlag : 0u) | occ);
+            }
             atomicAnd(&q.ao_ctr[sl >> 1], ~(0xffffu << sh));
             aux = kAuxSlotFree | sl;
         } else {
@@ -1440,6 +1454,18 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         uint32_t aux = kAuxAO;
         uint32_t ao_aux = kAuxAO; // the hit's AO ray: counted (kAuxAO) or carrying its occluded pixel (fit)
         const bool valid = lane < take;
+        // AO_SAMPLES >= 2: a counter slot per hit (LDS), popped from the free list (none left: kAuxAO)
+        if (!kAoChain && kAoSlots > 0u && k->ao_samples >= 2) {
+            const uint64_t vb = __ballot(valid);
+            if (vb) {
+                q_lock(&q.lock, lane);
+                const uint32_t top = vload(q.ao_top), n = (uint32_t)__popcll(vb), rank = lane_rank(vb);
+                const uint32_t got = n < top ? n : top;
+                if (valid && rank < got) ao_aux = kAuxAOSlot | (uint32_t)q.ao_free[top - 1u - rank];
+                if (lane == 0) q.ao_top = top - got;
+                q_unlock(&q.lock, lane);
+            }
+        }
         ShadeHit h;
         per_frame(valid, valid ? frame_of(m, t) : 0u, [&](uint32_t f) {
             Ctx cf = frame_ctx(c, ft, f);
@@ -1454,6 +1480,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     // the AO ray carries the occluded one (ao_factor(1, 1)); no sample, no k_finish
                     if (!(RT_DIAG_SKIP & 2)) gptr(ft->out8[f])[(size_t)late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
                     if (k->ao_samples) ao_aux = kAuxAOCand | (fit_pixel(v, ao_factor(1u, 1)) & 0xffffffu);
+                } else if (m.fitm && aux_ao_slot(ao_aux)) {
+                    // the colour the AO ray completing the count finishes with, and where: frame << 23 | pixel
+                    cpl[late(ao_aux & 255u)] = make_float4(v.x, v.y, v.z, __uint_as_float((f << 23) | (h.py * W + h.px)));
                 } else if (!(RT_DIAG_SKIP & 4)) {
                     sample_store(k, samples, t, v);
                 }
@@ -1478,33 +1507,27 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         // scripts/ubench_atomic.hip): the sample's aocc byte becomes kFinFlag (its AO ray adds 1 if
         // occluded) and the unit's hitmask word, zero from the unit, becomes nonzero (every writer
         // stores the same value)
-        if (m.fit && k->ao_samples && valid && more) {
+        // fitm: the same for every hit whose pixel the AO counter's completion does not store (a long
+        // shadow, or no slot); a long shadow's slot marks it (bit 10: its completion stores the flagged count)
+        const bool kfin = valid && ((m.fit && k->ao_samples && more) || (m.fitm && (more || !aux_ao_slot(ao_aux))));
+        if (kfin) {
             reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)kFinFlag;
             hitmask[t >> 6] = 1ull;
         }
+        if (m.fitm && more && aux_ao_slot(ao_aux))
+            atomicOr(&q.ao_ctr[(ao_aux & 255u) >> 1], (1u << 10) << ((ao_aux & 1u) * 16u));
         if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // the fin record is in L2 before the ray is visible
             push_long(more, st, t, aux, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
         }
         // AO extension: the hit's AO rays start as long rays (fit: after its unoccluded pixel is stored,
         // which an occluded AO ray overwrites)
-        if (m.fit) __builtin_amdgcn_s_waitcnt(0);
+        if (m.fit || m.fitm) __builtin_amdgcn_s_waitcnt(0);
         if (kAoChain && k->ao_samples >= 2) { // the first AO ray of the hit's chain (ao_chain_next)
             March<L, true> ao;
             if (valid) ao_begin(c, h, 0u, ao);
             push_long(valid, ao, t, kAuxChain, make_float4(h.n.x, h.n.y, h.n.z, h.prec));
         } else {
-            if (kAoSlots > 0u && k->ao_samples >= 2) { // a counter slot per hit, popped from the free list
-                const uint64_t vb = __ballot(valid);
-                if (vb) {
-                    q_lock(&q.lock, lane);
-                    const uint32_t top = vload(q.ao_top), n = (uint32_t)__popcll(vb), rank = lane_rank(vb);
-                    const uint32_t got = n < top ? n : top;
-                    if (valid && rank < got) ao_aux = kAuxAOSlot | (uint32_t)q.ao_free[top - 1u - rank];
-                    if (lane == 0) q.ao_top = top - got;
-                    q_unlock(&q.lock, lane);
-                }
-            }
             for (int kk = 0; kk < k->ao_samples; ++kk) {
                 March<L, true> ao;
                 if (valid) ao_begin(c, h, (uint32_t)kk, ao);
@@ -1629,7 +1652,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             }
             const uint64_t hb = __ballot(hit);
             // k_finish skips the misses; with fit it finishes only the hits the shading marks
-            if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = m.fit ? 0ull : hb;
+            if (lane == 0) hitmask[(f * m.n_units + u) * aa + a] = (m.fit || m.fitm) ? 0ull : hb;
             if (hb) {
                 // the hits' records go on the block's hit stack in rank order (dense lines), stored
                 // before the top publishes them.  The stack does not overflow: a wave starts a unit
@@ -1792,7 +1815,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         if (!unit_pixel(m, f, u, lane, W, H, &px, &py)) continue;
         // one sample per pixel: k_trace wrote the misses' pixels, only the hits remain (fit: only the
         // units whose hitmask word is nonzero, and in them the samples flagged kFinFlag)
-        if (m.fit) {
+        if (m.fit || m.fitm) {
             if (hitmask[f * m.n_units + u] == 0ull) continue;
             const uint32_t t = f * m.frame_samples + u * 64u + lane;
             if (!((aocc[t >> 2] >> ((t & 3u) * 8u)) & kFinFlag)) continue; // (its word is cleared by a flagged lane or is 0)
@@ -1971,6 +1994,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     dim3 blk(1024);
     m.cells_from_cam = (uint32_t)a.cells_from_cam;
     m.fit = (uint32_t)a.fit;
+    m.fitm = kAoSlots > 0u ? (uint32_t)a.fitm : 0u;
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue,
                        a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
@@ -1981,7 +2005,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
         const RtConsts* k0 = a.frames_host.k[0];
         hipLaunchKernelGGL((k_trace<L, S, CH>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
                            a.perm2d, a.grad, m,
-                           a.order, a.hitmask, a.samples, a.fin, a.finpool, a.hitq, a.spill_long, a.hit_cap,
+                           a.order, a.hitmask, a.samples, a.fin, a.finpool, a.cpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
                            a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots, a.fuse_next);
         // fit without AO: every hit pixel is final in k_trace

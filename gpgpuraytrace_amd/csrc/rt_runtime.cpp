@@ -124,6 +124,7 @@ struct rt_device_s {
     uint64_t* hitmask = nullptr; // per unit and AA sample: the primary-hit ballot (k_trace -> k_finish)
     float4* fin = nullptr;
     float4* finpool = nullptr; // k_trace's per-block fin pools (RT_FIN_SLOTS slots of 3 float4 per block)
+    float4* cpool = nullptr;   // k_trace's per-block AO colour pools (RT_AO_POOL_SLOTS float4 per block)
     uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
@@ -487,6 +488,8 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.fit = 0;
     a.fin = dev->fin;
     a.finpool = dev->finpool;
+    a.cpool = dev->cpool;
+    a.fitm = 0;
     a.aocc = dev->aocc;
     a.ao_samples = s->ao;
     a.aa = s->aa;
@@ -536,6 +539,8 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         if (dev->hitq) HIP_TRY(hipFree(dev->hitq));
         if (dev->spill_long) HIP_TRY(hipFree(dev->spill_long));
         if (dev->finpool) HIP_TRY(hipFree(dev->finpool));
+        if (dev->cpool) HIP_TRY(hipFree(dev->cpool));
+        dev->cpool = nullptr;
         dev->hitq = nullptr;
         dev->spill_long = nullptr;
         dev->finpool = nullptr;
@@ -543,6 +548,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         HIP_TRY(hipMalloc(&dev->hitq, hq_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->finpool, (size_t)dev->num_cus * RT_FIN_SLOTS * 3 * sizeof(float4)));
+        HIP_TRY(hipMalloc(&dev->cpool, (size_t)dev->num_cus * RT_AO_POOL_SLOTS * sizeof(float4)));
         dev->hitq_n = hq_need;
         dev->spill_long_n = ls_need;
     }
@@ -670,7 +676,7 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)hitq, (void*)finpool, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
+                    (void*)hitq, (void*)finpool, (void*)cpool, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
@@ -1248,7 +1254,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)(uintptr_t)a.queue, (uint64_t)a.num_cus, (uint64_t)(uintptr_t)a.hitmask,
                           (uint64_t)(uintptr_t)a.samples, (uint64_t)(uintptr_t)a.hitq,
                           (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_cap, (uint64_t)a.long_spill_cap,
-                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)a.fit, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool,
+                          (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)a.fit, (uint64_t)a.fitm, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool, (uint64_t)(uintptr_t)a.cpool,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
     k.insert(k.end(), std::begin(v), std::end(v));
@@ -1468,7 +1474,12 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     // one sample per pixel, at most one AO ray and no float output: hit pixels finish where their last
     // ray ends (k_trace), not through a per-sample colour and k_finish
     la_scr.fit = b.s0->aa == 1 && b.s0->ao <= 1;
-    for (int f = 0; f < n; ++f) la_scr.fit = la_scr.fit && ft.out32[f] == nullptr;
+    // (the colour pool packs frame << 23 | pixel: frames of < 2^23 pixels)
+    la_scr.fitm = b.s0->aa == 1 && b.s0->ao >= 2 && (size_t)dev->width * (size_t)dev->height < ((size_t)1 << 23);
+    for (int f = 0; f < n; ++f) {
+        la_scr.fit = la_scr.fit && ft.out32[f] == nullptr;
+        la_scr.fitm = la_scr.fitm && ft.out32[f] == nullptr;
+    }
     auto pre = [&] {
         if (phases & PH_PRE) rt_launch_camerarays_batch(la_cam);
     };
