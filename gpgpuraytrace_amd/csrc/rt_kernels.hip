@@ -714,14 +714,7 @@ __device__ __forceinline__ ShadeHit shade_hit(const Ctx& c, const UnitMap& m, fl
 // (< kFinSlots), or at fin[t] when the pool was empty (kAuxFinT).
 constexpr uint32_t kAuxAO = 0xffffffffu, kAuxAOCand = 0x80000000u, kAuxFinT = 0x7ffffffeu;
 __device__ __forceinline__ bool aux_ao(uint32_t aux) { return (int32_t)aux < 0; }
-// With AO_SAMPLES >= 2 (RT_AO_CHAIN) a hit's AO rays march one after another on one lane: kAuxChain |
-// k << 8 | occluded so far.  The record carries the hit's normal and shadow stepmod (the next ray's
-// start) in place of the direction, which is formed again from them (ao_chain_dir); the last ray
-// stores the count, one plain byte store per hit instead of a device atomic per occluded ray (a
-// device-scope atomic costs a 32-B HBM write on gfx950, in L2 or not: scripts/ubench_atomic.hip).
-constexpr uint32_t kAuxChain = 0xa0000000u;
-__device__ __forceinline__ bool aux_chain(uint32_t aux) { return (aux & 0xf0000000u) == kAuxChain; }
-// With AO_SAMPLES >= 2 (and no chains) a hit's AO rays count their occlusion in a slot of the block's AO
+// With AO_SAMPLES >= 2 a hit's AO rays count their occlusion in a slot of the block's AO
 // counters in LDS (kAuxAOSlot | slot, TraceQueues::ao_ctr): the ray that completes the count stores it,
 // one plain byte store per hit; an idle lane holding kAuxSlotFree | slot returns the slot to the free list
 // at its wave's next refill.  No free slot: the hit's rays count by device atomics (kAuxAO).
@@ -736,12 +729,11 @@ __device__ __forceinline__ bool aux_slot_free(uint32_t aux) { return (aux & 0xff
 // ray is live, so its next step overwrites d before anything reads it; nor is lastStep, which only
 // the refinement after a hit reads (tracing.hlsl:76-79) and SKIPREFINE rays break before it.
 template <int L>
-__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t aux, float4* r, float4 chain)
+__device__ __forceinline__ void long_pack(const March<L, true>& st, uint32_t t, uint32_t aux, float4* r)
 {
     r[0] = make_float4(st.p.x, st.p.y, st.p.z, st.dist);
     r[1] = make_float4(st.step, __uint_as_float(aux), __uint_as_float((uint32_t)st.iters), __uint_as_float(t));
-    if (aux_chain(aux)) r[2] = chain; // (normal, stepmod): ao_chain_dir
-    else if (aux_ao(aux)) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
+    if (aux_ao(aux)) r[2] = make_float4(st.dir.x, st.dir.y, st.dir.z, 0.0f);
     else if constexpr (March<L, true>::FOG) r[2] = make_float4(st.f.x, st.f.y, st.f.z, st.f.w);
     // no fog: a shadow ray's f is +0 throughout (march_step), so r2 is neither written nor read
 }
@@ -777,22 +769,6 @@ template <int L>
 __device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32_t kk, March<L, true>& st)
 {
     march_begin(c, st, h.hp, 0.4f, h.prec, ao_dir(h.n, h.px, h.py, h.a, kk), false);
-}
-
-// AO ray kk of sample t's hit with normal n, as ao_begin formed its direction (unnormalised: march_begin
-// normalises it; ao_chain_unit: the normalised direction a marching chain ray carries)
-__device__ __forceinline__ f3 ao_chain_dir(const RtConsts* k, const UnitMap& m, uint32_t t, f3 n, uint32_t kk)
-{
-    const uint32_t f = frame_of(m, t);
-    uint32_t px, py, a;
-    sample_pixel(m, m.frame_rot ? f : 0u, t - f * m.frame_samples, (uint32_t)k->aa_samples, (uint32_t)k->width,
-                 (uint32_t)k->height, &px, &py, &a);
-    return ao_dir(n, px, py, a, kk);
-}
-__device__ __forceinline__ f3 ao_chain_unit(const RtConsts* k, const UnitMap& m, uint32_t t, f3 n, uint32_t kk)
-{
-    const f3 d = ao_chain_dir(k, m, t, n, kk);
-    return rtm::scale(d, rtm::rcp(rtm::length(d)));
 }
 
 // The inputs a long shadow ray needs to finish its sample: (albedo + specular, brightness), fcolord
@@ -901,8 +877,6 @@ constexpr uint32_t kLongRing = 570; // fills the CU's LDS: 128 KiB tables + 4 Ki
 constexpr uint32_t kFinSlots = RT_FIN_SLOTS;
 // AO counter slots per block (AO_SAMPLES >= 2; the LDS the ring and the tables leave)
 constexpr uint32_t kAoSlots = RT_AO_SLOTS;
-// AO_SAMPLES >= 2: shading batches reserve LDS ring room for the long rays they push (RT_SHADE_RESERVE)
-constexpr bool kShadeReserve = RT_SHADE_RESERVE != 0;
 static_assert(kAoSlots % 2u == 0u && kAoSlots <= 256u && kAoSlots <= RT_AO_POOL_SLOTS,
               "AO slots: pairs of u16 counters, u8 indices, a colour each in the pool");
 constexpr uint32_t kLongBatch = RT_LONG_BATCH; // queued long rays that make a wave switch to them
@@ -916,8 +890,6 @@ constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSe
 // still marching, they continue as segments of 64 / kPrimarySeg lanes per ray (primary_seg in
 // k_trace) instead of keeping 64 lanes on a few rays' octave loops.  0: off.
 constexpr uint32_t kPrimarySeg = RT_PRIMARY_SEG;
-// AO_SAMPLES >= 2: a hit's AO rays as one chain on a lane (kAuxChain); 0: independent rays, atomic counts
-constexpr bool kAoChainBuild = RT_AO_CHAIN != 0;
 static_assert(kPrimarySeg == 0u || kPrimarySeg == 4u || kPrimarySeg == 8u || kPrimarySeg == 16u, "lanes per ray");
 // The instrumented (STATS) kernels take the same segment tail (their counters cost registers there:
 // they spill, the product does not), so their march and noise counts pass through the product's code.
@@ -941,7 +913,6 @@ struct TraceQueues {
     uint32_t ls_top; // the block's long-ray spill stack (HBM, long_spill_cap records): [0, ls_top) queued
     uint32_t pad1;
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
-    uint32_t l_res;            // LDS ring slots reserved by shading batches in progress (AO_SAMPLES >= 2)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
@@ -991,9 +962,7 @@ struct TraceThreads {
 static_assert(RT_CTR_FIRST + RT_TRACE_WAVES_FAST <= RT_CTR_BYTES / 4 && RT_CTR_FIRST + RT_TRACE_WAVES_WIDE <= RT_CTR_BYTES / 4,
               "a first-unit counter per wave slot inside the zeroed work counters");
 
-// CHAIN: AO_SAMPLES >= 2 with RT_AO_CHAIN (a separate instantiation: the chain state costs registers the
-// one-AO-ray configurations do not carry)
-template <int L, bool STATS, bool CHAIN>
+template <int L, bool STATS>
 __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
@@ -1009,7 +978,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                                                 uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots,
                                                 FusedPrepass np)
 {
-    constexpr bool kAoChain = CHAIN; // AO chains (ao_chain_next), AO_SAMPLES >= 2 only
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
     __shared__ __attribute__((aligned(16))) uint32_t
@@ -1027,7 +995,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.drained = 0;
         q.ls_top = 0;
         q.f_top = fin_slots;
-        q.l_res = 0;
         q.overflow = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
@@ -1063,21 +1030,21 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
     // block's spill stack when the LDS ring is full (stored before the tail publishes them)
-    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux, float4 chain) {
+    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
         const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
         if (lt - lh + n <= long_ring_cap) {
-            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec], chain);
+            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
         } else {
             // the spill stack's bound (rt_spill_caps) holds by the work priorities; a push past it is
             // dropped and flagged (rt_device_check), never written over queued rays
             const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane(vload(q.ls_top));
             const bool fits = stl + n <= long_spill_cap;
-            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec, chain);
+            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec);
             __builtin_amdgcn_s_waitcnt(0);
             if (lane == 0) {
                 q.ls_top = fits ? stl + n : stl;
@@ -1135,20 +1102,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
     };
 
-    // an AO chain's ray left the march (AO_SAMPLES >= 2): the hit's next AO ray starts in its place
-    // (true), or the last one stores the hit's occluded count, one byte that only this lane writes, and
-    // the chain ends (false); `store`: this lane writes (one lane of a segment)
-    auto ao_chain_next = [&](March<L, true>& st, uint32_t t, uint32_t& aux, const float4& chain, bool store = true) {
-        const uint32_t kk = ((aux >> 8) & 15u) + 1u, occ = (aux & 255u) + (st.d > 0.0f ? 1u : 0u);
-        if (kk < (uint32_t)k->ao_samples) {
-            march_begin(c, st, st.p, 0.4f, chain.w, ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), kk), false);
-            aux = kAuxChain | (kk << 8) | occ;
-            return true;
-        }
-        if (store && occ != 0u) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ;
-        return false;
-    };
-
     // ---- a batch of long rays, lane refill from the ring ----
     auto do_shadow = [&]() {
         March<L, true> st;
@@ -1156,42 +1109,26 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         st.iters = 0;
         bool live = false;
         uint32_t t = 0, aux = kAuxAO; // aux: the lane's ray (long_pack); on an idle lane, a fin slot to free
-        float4 chain = make_float4(0.0f, 0.0f, 0.0f, 0.0f); // an AO chain's (normal, stepmod)
-        bool fresh = false; // a chain ray just taken: its direction is still to be formed
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
         for (;;) {
-            // a ray that left the march finishes; an AO chain's lane waits (`fresh`) for its next ray
-            while (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
+            if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
-                if (kAoChain && aux_chain(aux)) {
-                    const uint32_t kk = ((aux >> 8) & 15u) + 1u, occ = (aux & 255u) + (st.d > 0.0f ? 1u : 0u);
-                    if (kk < (uint32_t)k->ao_samples) {
-                        aux = kAuxChain | (kk << 8) | occ;
-                        fresh = true;
-                    } else if (occ != 0u) {
-                        reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)occ; // this lane's hit only
-                    }
-                } else if (kAoSlots > 0u && aux_ao_slot(aux)) {
-                    ao_slot_finish(st, t, aux);
-                } else {
-                    long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
-                }
+                if (kAoSlots > 0u && aux_ao_slot(aux)) ao_slot_finish(st, t, aux);
+                else long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                 live = false;
             }
-            const uint32_t nidle = (uint32_t)__popcll(__ballot(!live));
-            bool start = nidle >= refill_idle; // the chains' next rays start with a refill (lanes batched)
-            if (start && queued_long() != 0u) {
-                const uint64_t idle = __ballot(!live && !fresh);
-                const uint32_t nfree = (uint32_t)__popcll(idle);
+            const uint64_t idle = __ballot(!live);
+            const uint32_t nidle = (uint32_t)__popcll(idle);
+            if (nidle >= refill_idle && queued_long() != 0u) {
                 q_lock(&q.lock, lane);
                 free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
-                const uint32_t take = (tail - head) < nfree ? (tail - head) : nfree;
+                const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
                 // the block's spill stack tops up what the LDS ring cannot give (from its top)
                 const uint32_t sl = vload(q.ls_top);
-                const uint32_t more = sl < nfree - take ? sl : nfree - take;
+                const uint32_t more = sl < nidle - take ? sl : nidle - take;
                 const uint32_t rank = lane_rank(idle);
                 const bool mine = ((idle >> lane) & 1ull) && rank < take + more;
                 auto take_ray = [&](float4 r0, float4 r1, float4 r2) {
@@ -1199,10 +1136,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     const float* fr = s_fr.v[frame_of(m, t)];
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                     if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
-                    if (kAoChain && aux_chain(aux)) {
-                        chain = r2; // its direction is formed after the lock is released
-                        fresh = true;
-                    }
                     live = true;
                 };
                 if (mine && rank < take) {
@@ -1219,23 +1152,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 }
                 q_unlock(&q.lock, lane);
             }
-            uint64_t lv = __ballot(live);
-            if (lv == 0ull) start = true; // nothing else marches: the waiting chains go on now
-            if (kAoChain && start && __ballot(fresh)) {
-                // chain rays taken from the ring get their direction, waiting chains their next ray:
-                // one pass for every such lane (the direction is a hash and a basis, ao_dir)
-                if (fresh) {
-                    const f3 d = ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u);
-                    if (live) {
-                        st.dir = rtm::scale(d, rtm::rcp(rtm::length(d)));
-                    } else {
-                        march_begin(c, st, st.p, 0.4f, chain.w, d, false);
-                        live = true;
-                    }
-                    fresh = false;
-                }
-                lv = __ballot(live);
-            }
+            const uint64_t lv = __ballot(live);
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
             // them with new rays) and go do other work, while there still is some.
@@ -1244,21 +1161,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) // after the drain: few rays go to segment waves
                 hand_back = hand_back || (drained_now && lv != 0ull && (uint32_t)__popcll(lv) <= kSegHandBack &&
                                           queued_long() == 0u);
-            if (kAoChain && hand_back && __ballot(fresh)) { // waiting chains go back with the others: start them
-                if (fresh) {
-                    march_begin(c, st, st.p, 0.4f, chain.w,
-                                ao_chain_dir(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u), false);
-                    live = true;
-                    fresh = false;
-                }
-            }
             if (lv == 0ull || hand_back) {
                 if (__ballot(!live && (aux < kFinSlots || aux_slot_free(aux)))) {
                     q_lock(&q.lock, lane);
                     free_fin_locked(live, aux);
                     q_unlock(&q.lock, lane);
                 }
-                if (hand_back) push_long(live, st, t, aux, chain);
+                if (hand_back) push_long(live, st, t, aux);
                 c.nz.calls = cl.nz.calls;
                 return;
             }
@@ -1283,7 +1192,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             st.d = 0.0f;
             st.iters = 0;
             uint32_t t = 0, aux = kAuxAO;
-            float4 chain = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             bool live = false;
             Ctx cl = c;
             cl.nz.phase = RT_PHASE_LONG;
@@ -1309,7 +1217,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 const float* fr = s_fr.v[frame_of(m, t)];
                 cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                 if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
-                if (kAoChain && aux_chain(aux)) chain = r2;
                 live = true;
             }
             __builtin_amdgcn_s_waitcnt(0); // the spill records are read before their slots can be reused
@@ -1318,19 +1225,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
-            if (kAoChain && live && aux_chain(aux)) // outside the lock
-                st.dir = ao_chain_unit(k, m, t, rtm::mk(chain.x, chain.y, chain.z), (aux >> 8) & 15u);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
             for (;;) {
-                // every lane of the segment holds the same ray: all of them start a chain's next AO ray
-                while (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
-                    if (j == 0u) stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
-                    if (kAoChain && aux_chain(aux)) {
-                        if (ao_chain_next(st, t, aux, chain, j == 0u)) continue;
-                    } else if (kAoSlots > 0u && aux_ao_slot(aux)) {
-                        if (j == 0u) ao_slot_finish(st, t, aux);
-                    } else if (j == 0u) {
-                        long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
+                if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
+                    if (j == 0u) { // every lane of the segment holds the same ray: its first lane finishes it
+                        stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
+                        if (kAoSlots > 0u && aux_ao_slot(aux)) ao_slot_finish(st, t, aux);
+                        else long_finish<L>(k, m, s_fr, fin, finp, samples, aocc, t, aux, st);
                     }
                     live = false;
                 }
@@ -1455,7 +1356,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         uint32_t ao_aux = kAuxAO; // the hit's AO ray: counted (kAuxAO) or carrying its occluded pixel (fit)
         const bool valid = lane < take;
         // AO_SAMPLES >= 2: a counter slot per hit (LDS), popped from the free list (none left: kAuxAO)
-        if (!kAoChain && kAoSlots > 0u && k->ao_samples >= 2) {
+        if (kAoSlots > 0u && k->ao_samples >= 2) {
             const uint64_t vb = __ballot(valid);
             if (vb) {
                 q_lock(&q.lock, lane);
@@ -1518,21 +1419,15 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             atomicOr(&q.ao_ctr[(ao_aux & 255u) >> 1], (1u << 10) << ((ao_aux & 1u) * 16u));
         if (__ballot(more)) {
             __builtin_amdgcn_s_waitcnt(0); // the fin record is in L2 before the ray is visible
-            push_long(more, st, t, aux, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+            push_long(more, st, t, aux);
         }
         // AO extension: the hit's AO rays start as long rays (fit: after its unoccluded pixel is stored,
         // which an occluded AO ray overwrites)
         if (m.fit || m.fitm) __builtin_amdgcn_s_waitcnt(0);
-        if (kAoChain && k->ao_samples >= 2) { // the first AO ray of the hit's chain (ao_chain_next)
+        for (int kk = 0; kk < k->ao_samples; ++kk) {
             March<L, true> ao;
-            if (valid) ao_begin(c, h, 0u, ao);
-            push_long(valid, ao, t, kAuxChain, make_float4(h.n.x, h.n.y, h.n.z, h.prec));
-        } else {
-            for (int kk = 0; kk < k->ao_samples; ++kk) {
-                March<L, true> ao;
-                if (valid) ao_begin(c, h, (uint32_t)kk, ao);
-                push_long(valid, ao, t, ao_aux, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-            }
+            if (valid) ao_begin(c, h, (uint32_t)kk, ao);
+            push_long(valid, ao, t, ao_aux);
         }
     };
 
@@ -1717,29 +1612,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             continue;
         }
         if (hp >= 64u || (drained && hp > 0u)) {
-            // AO_SAMPLES >= 2: a batch pushes up to 64 x (1 + AO) long rays; it starts only once the LDS
-            // ring has room for them beside what other shading batches reserved, so its pushes do not go to
-            // the spill stack (HBM) (an empty ring always takes one batch: progress for any AO count)
-            const uint32_t need = kShadeReserve && k->ao_samples >= 2 ? 64u * (1u + (uint32_t)k->ao_samples) : 0u;
-            if (need) {
-                q_lock(&q.lock, lane);
-                const uint32_t used = vload(q.l_tail) - vload(q.l_head) + vload(q.l_res);
-                const bool ok = used == 0u || used + need <= long_ring_cap;
-                if (lane == 0 && ok) q.l_res = vload(q.l_res) + need;
-                q_unlock(&q.lock, lane);
-                if (!ok) { // the ring is taken: march long rays meanwhile
-                    do_shadow();
-                    continue;
-                }
-            }
             if (lane == 0) atomicAdd(&q.active, 1u);
             do_shade();
             if (lane == 0) atomicSub(&q.active, 1u);
-            if (need) {
-                q_lock(&q.lock, lane);
-                if (lane == 0) q.l_res = vload(q.l_res) - need;
-                q_unlock(&q.lock, lane);
-            }
             WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }
@@ -1983,8 +1858,6 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.n_frames = a.n_frames;
     m.frame_samples = m.n_units * 64u * (uint32_t)a.aa;
     uint32_t blocks = (uint32_t)(a.num_cus > 0 ? a.num_cus : 256);
-    // a shard (N > 1) may leave CUs to the transport of the other batch in flight (rt_variants.h)
-    if (stride > 1u && blocks > 2u * RT_SHARD_RESERVE_CUS) blocks -= RT_SHARD_RESERVE_CUS;
     uint32_t need = (m.n_units * m.n_frames + 15u) / 16u;
     uint32_t pblocks = need < blocks ? need : blocks;
     m.order_batch = RT_ORDER_BATCH >= 0 ? (uint32_t)RT_ORDER_BATCH
@@ -2000,10 +1873,10 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                        a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill stacks
-    auto primary = [&](auto stats_tag, auto chain_tag) {
-        constexpr bool S = decltype(stats_tag)::value, CH = decltype(chain_tag)::value;
+    auto primary = [&](auto stats_tag) {
+        constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        hipLaunchKernelGGL((k_trace<L, S, CH>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
+        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
                            a.perm2d, a.grad, m,
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.cpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
@@ -2012,14 +1885,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
         if (!(m.fit && a.ao_samples == 0))
             hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
-    const bool chain = kAoChainBuild && a.ao_samples >= 2;
-    if (a.stats) {
-        if (chain) primary(std::true_type{}, std::true_type{});
-        else primary(std::true_type{}, std::false_type{});
-    } else {
-        if (chain) primary(std::false_type{}, std::true_type{});
-        else primary(std::false_type{}, std::false_type{});
-    }
+    if (a.stats) primary(std::true_type{});
+    else primary(std::false_type{});
 }
 
 } // namespace

@@ -36,19 +36,9 @@
 #ifndef RT_PRIMARY_SEG
 #define RT_PRIMARY_SEG 8
 #endif
-// AO_SAMPLES >= 2: a hit's AO rays march as one chain on a lane, its occluded count stored once (1), or
-// as independent rays counted by device atomics (0)
-#ifndef RT_AO_CHAIN
-#define RT_AO_CHAIN 0
-#endif
-// AO counter slots per k_trace block in LDS (AO_SAMPLES >= 2 without chains; 0: device atomics count)
+// AO counter slots per k_trace block in LDS (AO_SAMPLES >= 2; 0: device atomics count)
 #ifndef RT_AO_SLOTS
 #define RT_AO_SLOTS 256
-#endif
-// AO_SAMPLES >= 2: a shading batch starts only when the LDS ring has room for its long rays (1), or
-// whenever fewer than RT_LONG_BATCH long rays are queued (0)
-#ifndef RT_SHADE_RESERVE
-#define RT_SHADE_RESERVE 0
 #endif
 // the instrumented (STATS) kernels take the product's primary segment tail too (1), so their march and
 // noise counts are asserted through the timed kernel's code path; 0 keeps a 64-lane tail there
@@ -78,11 +68,6 @@
 // wave priority (s_setprio) of a fused prepass task (FusedPrepass) while it marches
 #ifndef RT_FUSE_PRIO
 #define RT_FUSE_PRIO 3
-#endif
-// a sharded k_trace (N > 1) leaves this many CUs without a block, so that the other batch in flight's
-// k_finish, shard pack, RCCL gather and unpack find a CU while it runs (instead of queueing behind it)
-#ifndef RT_SHARD_RESERVE_CUS
-#define RT_SHARD_RESERVE_CUS 0
 #endif
 // k_order: RT_ORDER_BATCH forces the batch-wide (1) or frame-major (0) unit order; -1 = automatic
 // (batch-wide below kOrderBatchUnitsPerWave units per wave slot)
