@@ -24,3 +24,19 @@ def test_gpus_without_launcher_starts_torchrun_child(monkeypatch):
     assert any(c.startswith("--master-port=") for c in cmd)
     i = cmd.index(os.path.join(ROOT, "bench.py"))
     assert cmd[i + 1:] == ["--gpus", "4", "--steps", "8", "--warmup", "2"]
+
+
+def test_traffic_counts_the_product_kernels_only():
+    """The HBM traffic pass sums the uninstrumented tracescreen launch: the STATS instantiations are
+    recognised by their template argument (k_trace<L, STATS>, k_camerarays_group<STATS, ...>), not by
+    the word `true` anywhere in the name."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.instrumented_kernel("k_trace<0, true>")
+    assert bench.instrumented_kernel("k_trace<3, true>")
+    assert bench.instrumented_kernel("k_camerarays_group<true, 512, 8>")
+    assert not bench.instrumented_kernel("k_trace<0, false>")
+    assert not bench.instrumented_kernel("k_trace<0, false, true>")  # a later template flag is not STATS
+    assert not bench.instrumented_kernel("k_camerarays_group<false, 512, 4>")
+    assert not bench.instrumented_kernel("k_finish")

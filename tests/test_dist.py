@@ -263,6 +263,9 @@ def test_batch_plan_bookkeeping():
     assert P.frame_shard(5, 0, 1) == 0
     with pytest.raises(ValueError):
         P.BatchPlan(64, 48, 25, 2)  # RT_MAX_BATCH 24 (ABI 6)
+    big = P.BatchPlan(1920, 1080, 24, 8)  # the largest batch: every (frame, shard) pair still once
+    seen = {(f, s) for f, s, _ in big.packs(0)} | {(f, s) for _, f, s, _ in big.unpacks()}
+    assert seen == {(f, s) for f in range(24) for s in range(8)}
 
 
 def test_phase_summary_leaves_out_unreadable_pairs():
