@@ -58,7 +58,7 @@ PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, =
 # BASELINE.json configs (GPU ones): resolution, primary step cap, AO rays per hit, and the
 # CPU baseline's row samples (all host cores: parity + value; one thread: single_thread)
 CONFIGS = {
-    "c1": {"width": 256, "height": 256, "max_steps": 64, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 1,
+    "c1": {"width": 256, "height": 256, "max_steps": 64, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 1, "batch": 24,
            "name": "C1: 256x256, 64-step primary + shadow (the reference's CPU-scale plumbing case)"},
     "c2": {"width": 1280, "height": 720, "max_steps": 256, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 8,
            "name": "C2: 1280x720, 256-step primary + 1 shadow ray"},
@@ -87,9 +87,10 @@ def parse():
     ap.add_argument("--ao", type=int, default=None, help="AO rays per primary hit (build extension); 0 = off")
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="batches (slot groups, one HIP stream each) kept in flight; 1 = one batch at a time")
-    ap.add_argument("--batch", type=int, default=12,
-                    help="max frames per rt_terrain_render_batch launch sequence (1..24); the --steps frames are "
-                         "split into ceil(steps / batch) batches of near-equal size")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="max frames per rt_terrain_render_batch launch sequence (1..24; default 12, 24 for C1 whose "
+                         "256x256 frames underfill the chip at 12: 855-871 against 703 Mray/s, DESIGN.md section 5); "
+                         "the --steps frames are split into ceil(steps / batch) batches of near-equal size")
     ap.add_argument("--split-prepass", type=int, default=0,
                     help="N>1: 1 = each rank runs the prepass of B/N frames of a batch and an all-gather shares "
                          "them (a second collective and a cross-rank barrier per batch); 0 (default, SURVEY 8e and "
@@ -125,6 +126,8 @@ def parse():
     for key in ("width", "height", "max_steps", "ao"):
         if getattr(a, key) is None:
             setattr(a, key, preset[key])
+    if a.batch is None:
+        a.batch = preset.get("batch", 12)
     if a.graph is None:
         a.graph = 1 if a.config == "c5" else 0
     if a.lookahead and a.graph:
