@@ -1354,10 +1354,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         bool more = false;
         uint32_t aux = kAuxAO;
         uint32_t ao_aux = kAuxAO; // the hit's AO ray: counted (kAuxAO) or carrying its occluded pixel (fit)
-        bool valid = lane < take;
-        // AO_SAMPLES >= 2: a counter slot per hit (LDS), popped from the free list.  Hits beyond the free
-        // slots go back on the hit stack unshaded, so every AO count is an LDS counter (no device atomic
-        // on `aocc` beside the plain stores, whose L2 copy it could race)
+        const bool valid = lane < take;
+        // AO_SAMPLES >= 2: a counter slot per hit (LDS), popped from the free list (none left: kAuxAO)
         if (kAoSlots > 0u && k->ao_samples >= 2) {
             const uint64_t vb = __ballot(valid);
             if (vb) {
@@ -1366,21 +1364,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 const uint32_t got = n < top ? n : top;
                 if (valid && rank < got) ao_aux = kAuxAOSlot | (uint32_t)q.ao_free[top - 1u - rank];
                 if (lane == 0) q.ao_top = top - got;
-                if (got < n) { // (the stack holds them: they were on it)
-                    const uint32_t ht = vload(q.h_top);
-                    if (valid && rank >= got) {
-                        float4* rec = hq + (size_t)(ht + rank - got) * HR;
-                        rec[0] = r0;
-                        if constexpr (HR == 3u) {
-                            rec[1] = r1;
-                            rec[2] = r2;
-                        }
-                    }
-                    __builtin_amdgcn_s_waitcnt(0);
-                    if (lane == 0) q.h_top = ht + (n - got);
-                }
                 q_unlock(&q.lock, lane);
-                valid = valid && rank < got;
             }
         }
         ShadeHit h;
@@ -1628,11 +1612,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             continue;
         }
         if (hp >= 64u || (drained && hp > 0u)) {
-            // AO_SAMPLES >= 2 with every AO slot taken: march the long rays that hold them instead
-            if (kAoSlots > 0u && k->ao_samples >= 2 && vload(q.ao_top) == 0u && queued_long() != 0u) {
-                do_shadow();
-                continue;
-            }
             if (lane == 0) atomicAdd(&q.active, 1u);
             do_shade();
             if (lane == 0) atomicSub(&q.active, 1u);
