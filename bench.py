@@ -52,6 +52,9 @@ sys.path.insert(0, ROOT)
 # (RT_BENCH_HW_QUEUES overrides the count for A/B runs)
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
 
+# A/B runs only: RT_BENCH_PREPASS_INLINE=1 renders with RT_DEVICE_PREPASS_INLINE (the prepass as its own launch
+# before the trace, the ABI <= 6 sequence) instead of the default gated launch
+PREPASS_INLINE = os.environ.get("RT_BENCH_PREPASS_INLINE") == "1"
 METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
 PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, = FP32 MFMA dense)
@@ -69,7 +72,7 @@ CONFIGS = {
     "ref": {"width": 1920, "height": 1080, "max_steps": 0, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 16,
             "name": "1920x1080, reference semantics (uncapped march, shadow, no AO)"},
 }
-TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_finish"
+TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_finish (the gated launch: the prepass runs inside k_trace)"
 
 
 def parse():
@@ -102,6 +105,10 @@ def parse():
                          "batch's trace (rt_terrain_prepass_ahead, DESIGN.md section 7); 0 (default) = each batch's "
                          "prepass in line on its slot group's stream (measured 0.6%% faster at B=12: "
                          "profiles/r03/hw_queues.md).  config.single_frame always runs it (B=1: +1.3%%)")
+    ap.add_argument("--direct-pack", type=int, default=1,
+                    help="N>1, in-line prepass: 1 (default) = ranks > 0 render their shards straight into the packed "
+                         "gather buffer (rt_terrain_render_batch_packed, no pack launch) and rank 0 packs nothing; "
+                         "0 = render, then rt_shard_pack_batch (round 4)")
     ap.add_argument("--graph", type=int, default=None,
                     help="1 = every slot replays its frame as captured hipGraphs (RT_DEVICE_GRAPH), 0 = direct "
                          "launches; default: on for c5 (BASELINE's hipGraph-captured frame loop), off otherwise")
@@ -222,7 +229,7 @@ def traffic_child(a):
     from gpgpuraytrace_amd import engine as E
     euler = G.camera.INITIAL_ROTATION_EULER if a.pose == "reset" else G.camera.LOOKDOWN_ROTATION_EULER
     B = max(1, min(24, a.batch))
-    ring = E.FrameRing(a.width, a.height, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
+    ring = E.FrameRing(a.width, a.height, prepass_inline=PREPASS_INLINE, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     for _ in range(2):
         ring.render_batch()
@@ -359,7 +366,8 @@ def main():
     n_full = sum(1 for s in sizes if s == B)
 
     def make(stats, max_steps=a.max_steps, ao=a.ao, float_output=False):
-        dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=local, stats=stats, float_output=float_output)
+        dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=local, stats=stats, float_output=float_output,
+                                        prepass_inline=PREPASS_INLINE)
         if dev is None:
             raise RuntimeError("device create failed: " + G.lib().rt_last_error().decode())
         ter = G.Terrain(dev, a.landscape, max_steps=max_steps, ao_samples=ao)
@@ -375,7 +383,7 @@ def main():
         it on this rank (rt_terrain_render_batch, rotated shards): its tracescreen noise3d and the
         wave iterations of that noise (SIMD lane utilisation); (2) one whole frame: hits, rays,
         noise per frame and (keep_frame) its pixels."""
-        out = {"batch_noise": None, "noise_lane_util": None}
+        out = {"batch_noise": None, "noise_lane_util": None, "prepass_noise": None}
         if batch_stats:
             devs, ters = [], []
             for _ in range(B):
@@ -399,6 +407,7 @@ def main():
                 d.synchronize()
             c, w = total()
             out["batch_noise"], out["noise_lane_util"] = c - pc, (c - pc) / (64.0 * (w - pw)) if w > pw else None
+            out["prepass_noise"] = pc
             for d in devs:
                 d.destroy()
         sdev, ster = make(stats=True, max_steps=max_steps, ao=ao, float_output=keep_frame)
@@ -422,9 +431,10 @@ def main():
 
     # --- timed: batches of B frames, D batches in flight (FrameRing slot groups) ---
     camera = G.Camera(W, H, euler=euler)
-    ring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+    ring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
-    plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass, lookahead=a.lookahead)
+    plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass, lookahead=a.lookahead,
+                       direct_pack=bool(a.direct_pack))
     coll = P.Collectives(dist, backend, rank, world)
     dev_str = f"cuda:{local}"
     # a batch's devices share its stream (FrameRing): every op of a batch rides on it
@@ -469,6 +479,12 @@ def main():
 
         def render(self):
             E.render_batch(self.ters, rank if world > 1 else 0, world)
+
+        def render_packed(self, items):
+            # frame f's shard at base + f * max_bytes (items' offsets): the gather's send buffer, written by the
+            # trace kernels themselves
+            assert [off for _, _, off in items] == [plan.pack_offset(f) for f, _, _ in items]
+            E.render_batch_packed(self.ters, rank, world, self.b["packed"].data_ptr(), plan.max_bytes)
 
         def prepass_ahead(self):
             if self.g not in ahead:
@@ -636,7 +652,7 @@ def main():
         # B = 1 with three frames in flight (D3D11's default maximum frame latency, the reference
         # frame loop's own queue depth): each frame is its own prepass -> k_order -> k_trace ->
         # k_finish on its slot's stream, and the next frame's prepass overlaps this one's tail
-        sring = E.FrameRing(W, H, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
+        sring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
                             max_steps=a.max_steps, ao_samples=a.ao, batch=1, lookahead=True)
         for i in range(sring.depth + 1):
             sring.render_batch(ahead=i < sring.depth)
@@ -662,7 +678,7 @@ def main():
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)
-        rring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        rring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=0, ao_samples=0, batch=B, lookahead=bool(a.lookahead))
         for i in range(rring.depth + 1):
             rring.render_batch(ahead=i < rring.depth)
@@ -696,7 +712,7 @@ def main():
             if i + 1 == len(path):
                 want_last = cdev.readback()
         cdev.destroy()
-        mring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        mring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
 
         def path_batch(first, n):
@@ -726,7 +742,7 @@ def main():
         # sustained rate: the timed loop's batches back to back for ~--sustained-s seconds (clocks and
         # power under a long load), a HIP event after every batch on its stream, read once at the end
         n_sus = max(2, int(a.sustained_s * 1e3 / (elapsed / a.steps * 1e3 * B) + 0.5))
-        uring = E.FrameRing(W, H, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        uring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
         for _ in range(uring.depth + 1):
             uring.render_batch()
@@ -770,7 +786,10 @@ def main():
 
     ms_per_frame = elapsed / a.steps * 1e3
     value = rays_per_frame * a.steps / elapsed / 1e6
-    batch_noise = counts["batch_noise"]
+    # the timed launch's noise3d: tracescreen's, plus (the gated launch, the default for nomadplains) the
+    # batch's prepass rays, which run inside the same trace kernel
+    gated = not PREPASS_INLINE and a.landscape == "nomadplains"
+    batch_noise = counts["batch_noise"] + (counts["prepass_noise"] if gated else 0)
     achieved = batch_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
     traffic, traffic_how = None, "not measured (N>1: a rank's launch traces a shard; or --traffic off)"
     if world == 1 and a.traffic == "pmc":
@@ -805,6 +824,7 @@ def main():
                                                 "(the primary segment tail included: RT_STATS_PRIMARY_SEG)",
                 "parallelism": "single GPU" if world == 1 else (
                     f"tile-cyclic 32x32 shards x{world} (rotated per frame) + RCCL gather per batch"
+                    + (" (shards rendered straight into the packed send buffer)" if plan.direct_pack else "")
                     + (" + prepass split over ranks (RCCL all-gather of CameraResults)" if plan.split_prepass
                        else "")),
                 "batch": B, "batches": sizes, "batches_in_flight": a.frames_in_flight,
@@ -834,7 +854,9 @@ def main():
                 "timing": "HIP events per launch on its stream, one batch in flight (the last "
                           f"{kn} tracescreen launches of the run; one launch = {B} frames)",
                 "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {batch_noise} noise3d per launch ({B} "
-                             f"frame(s); frame f traces shard (rank + f) % world)",
+                             f"frame(s); frame f traces shard (rank + f) % world"
+                             + (f"; incl. their {counts['prepass_noise']} prepass noise3d: the gated launch runs the "
+                                "prepass inside the trace kernel)" if gated else ")"),
                 "note": "FP32 vector-ALU bound (no MFMA-shaped or HBM-bound work); gfx950 vector FP32 peak "
                         "= FP32 dense matrix peak = 157.3 TFLOP/s",
             },

@@ -18,7 +18,9 @@ RT_DEVICE_FLOAT_OUTPUT = 1
 RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
-ABI_VERSION = 6  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
+RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the next batch's prepass tasks (timeout test)
+RT_DEVICE_PREPASS_INLINE = 128  # ABI 7: the prepass as its own launch before the trace (the ABI <= 6 sequence)
+ABI_VERSION = 7  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -60,6 +62,7 @@ SIGNATURES = {
     "rt_device_set_profiling": (_i, [_vp, _i]),
     "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
+    "rt_device_info": (_i, [_vp, _i, C.POINTER(C.c_ulonglong)]),
     "rt_device_wait_event": (_i, [_vp, _vp]),
     "rt_device_record_event": (_i, [_vp, _vp]),
     "rt_device_check": (_i, [_vp]),
@@ -88,6 +91,7 @@ SIGNATURES = {
     "rt_terrain_render": (_i, [_vp, _vp, _i, _i]),
     "rt_terrain_render_feed": (_i, [_vp, _vp, _i, _i]),
     "rt_terrain_render_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i]),
+    "rt_terrain_render_batch_packed": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp, _sz]),
     "rt_terrain_prepass_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
     "rt_terrain_trace_batch": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i, _i, _i, _vp]),
     "rt_terrain_prepass_ahead": (_i, [C.POINTER(_vp), C.POINTER(_vp), _i]),

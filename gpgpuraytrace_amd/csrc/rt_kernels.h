@@ -9,7 +9,7 @@
 // first-unit counter per wave slot of a k_trace block), then the device's sticky flags (zeroed at
 // device creation and by rt_device_check only): a k_trace queue push that would exceed its bound
 // raises a flag instead of storing (rt_spill_caps)
-enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1 };
+enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1, RT_CTR_GATE = 24 }; // RT_CTR_GATE: the in-launch prepass's task counter
 #define RT_CTR_BYTES 128
 #define RT_QUEUE_BYTES 192
 enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_TIMEOUT = 4u };
@@ -38,6 +38,24 @@ struct FrameTable {
 struct FusedPrepass {
     const FrameTable* ft;
     uint32_t* ctl;
+    uint32_t tasks;
+};
+
+// The batch's OWN camerarays prepass inside its k_trace (the gated launch, nomadplains; DESIGN.md
+// section 7): `tasks` = frames x RT_FUSE_TASKS_PER_FRAME tasks of 8 rays, taken first by the waves
+// (top priority), each storing its 8 CameraResults as one whole 128-B line (sc1) and then, per frame
+// (RT_GATE_WORDS words at gate + f * RT_GATE_WORDS, zeroed by k_order), its task flag (sc1 store) and
+// the frame's ray counter (agent add; the task that completes the frame derives its CellDistance).  A
+// primary unit starts only once the tasks of every CameraResults ray its cells' setTargetDepths reads
+// (the 5x5 neighbourhood) have flagged, so units start while the prepass's long rays still march
+// instead of after the whole prepass.  Not-yet-ready units wait in their block's deferred list
+// (defer_cap entries per block in HBM).  tasks == 0: off (the prepass ran before; cells from k_order).
+#define RT_GATE_WORDS 160 // per frame: 128 task flags, the ray counter on its own 128-B line
+#define RT_GATE_CTR 128
+#define RT_DEFER_CAP 1024 // deferred units per k_trace block
+struct GatedPrepass {
+    uint32_t* gate;  // RT_MAX_BATCH x RT_GATE_WORDS
+    uint32_t* defer; // num_cus x RT_DEFER_CAP unit indices
     uint32_t tasks;
 };
 
@@ -76,6 +94,12 @@ struct RtLaunch {
     FusedPrepass fuse_next;   // the next batch's prepass, run inside this k_trace (tasks 0: none); k_order zeroes its ctl
     const uint32_t* wait_ctl; // this batch's prepass ran inside the previous k_trace: k_order waits for wait_ctl[1]
     uint32_t wait_total;      //   to reach this many rays
+    hipEvent_t after_order_fuse; // recorded after k_order when set: fuse_next's counters are zeroed (its batch's
+                                 // own k_order, on another stream, polls them only after this event)
+    uint32_t* host_flag;      // host-mapped word of the GPU: k_order stores RT_FLAG_PREPASS_TIMEOUT there when its
+                              // wait for a fused prepass times out (every later C-ABI call on the GPU fails)
+    GatedPrepass gated;       // this batch's prepass inside its own k_trace (tasks 0: off)
+    int packed;               // frames.out8[f] are packed shard buffers (UnitMap::packed; no float output)
 };
 
 void rt_launch_camerarays(const RtLaunch& a, float4* camera_results);

@@ -197,14 +197,18 @@ __global__ void __launch_bounds__(BS) k_camerarays_group(const RtConsts* __restr
 }
 
 // ---------------------------------------------------------------------------
-// Terrain.cpp:356-439 with the host's std::min/std::max argument order.
-__device__ __forceinline__ float cd_get_depth(const float* d, int x, int y)
+// Terrain.cpp:356-439 with the host's std::min/std::max argument order.  `depth(x, y)` reads the
+// CameraResults depth of prepass ray (x, y) (coordinates already clamped to the 32 x 32 grid): from an
+// LDS copy (k_order) or straight from the frame's CameraResults (the gated launch's lanes).
+template <class Depth>
+__device__ __forceinline__ float cd_get_depth(Depth depth, int x, int y)
 {
     x = x < 0 ? 0 : (x >= RT_CAMERA_RES ? RT_CAMERA_RES - 1 : x);
     y = y < 0 ? 0 : (y >= RT_CAMERA_RES ? RT_CAMERA_RES - 1 : y);
-    return d[y * RT_CAMERA_RES + x];
+    return depth(x, y);
 }
-__device__ __forceinline__ float cd_interp(const float* d, int x, int y)
+template <class Depth>
+__device__ __forceinline__ float cd_interp(Depth d, int x, int y)
 {
     if (x < 0) {
         float m = cd_get_depth(d, x + 1, y);
@@ -229,22 +233,16 @@ __device__ __forceinline__ float cd_interp(const float* d, int x, int y)
     return cd_get_depth(d, x, y);
 }
 
-// setTargetDepths of one frame by a 1024-thread block (thread = cell), depth scratch in LDS
-__device__ __forceinline__ void cell_depths_frame(const float4* __restrict__ cam, float2* __restrict__ cells,
-                                                  float* s_d)
+// setTargetDepths (Terrain.cpp:398-439) of cell (xpos, ypos): its (dmin, dmax) bracket from the 5 x 5
+// neighbourhood of prepass depths
+template <class Depth>
+__device__ __forceinline__ float2 cell_bracket(Depth depth, int xpos, int ypos)
 {
-    const int i = threadIdx.x;
-    __syncthreads(); // s_d's previous frame is no longer read
-    // sc1 (L1-bypassing) load: a fused prepass wrote these in another kernel (FusedPrepass; the
-    // hand-off's loads are all global_load_dword sc1 after k_order's poll and barrier)
-    s_d[i] = __hip_atomic_load(reinterpret_cast<const float*>(cam + i) + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    int xpos = i % RT_CAMERA_RES, ypos = i / RT_CAMERA_RES;
-    float dmin = cd_interp(s_d, xpos, ypos);
+    float dmin = cd_interp(depth, xpos, ypos);
     float dmax = dmin;
     for (int xp = -2; xp <= 2; ++xp) {
         for (int yp = -2; yp <= 2; ++yp) {
-            float d = cd_interp(s_d, xpos + xp, ypos + yp);
+            float d = cd_interp(depth, xpos + xp, ypos + yp);
             dmin = (dmin < d) ? dmin : d;
             dmax = (d < dmax) ? dmax : d;
         }
@@ -253,7 +251,30 @@ __device__ __forceinline__ void cell_depths_frame(const float4* __restrict__ cam
     dmax = dmax * 1.22f + 0.4f;
     dmin = (RT_CAMERA_NEAR < dmin) ? dmin : RT_CAMERA_NEAR;
     dmax = (dmax < RT_CAMERA_FAR) ? dmax : RT_CAMERA_FAR;
-    cells[i] = make_float2(dmin, dmax);
+    return make_float2(dmin, dmax);
+}
+
+// a prepass depth read straight from CameraResults another wave stored with sc1 (FusedPrepass, the
+// gated launch): an sc1 global_load_dword, after the poll of the writers' flag or counter matched
+__device__ __forceinline__ float cam_depth_sc1(const float4* cam, int x, int y)
+{
+    typedef const float __attribute__((address_space(1))) gfloat;
+    return __hip_atomic_load((gfloat*)(reinterpret_cast<const float*>(cam + y * RT_CAMERA_RES + x) + 3),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// setTargetDepths of one frame by a 1024-thread block (thread = cell), depth scratch in LDS
+__device__ __forceinline__ void cell_depths_frame(const float4* __restrict__ cam, float2* __restrict__ cells,
+                                                  float* s_d)
+{
+    const int i = threadIdx.x;
+    __syncthreads(); // s_d's previous frame is no longer read
+    // sc1 (L1-bypassing) load: a fused prepass wrote these in another kernel (FusedPrepass; the
+    // hand-off's loads are all global_load_dword sc1 after k_order's poll and barrier)
+    s_d[i] = cam_depth_sc1(cam, i % RT_CAMERA_RES, i / RT_CAMERA_RES);
+    __syncthreads();
+    cells[i] = cell_bracket([&](int x, int y) { return s_d[y * RT_CAMERA_RES + x]; }, i % RT_CAMERA_RES,
+                            i / RT_CAMERA_RES);
 }
 
 // ===========================================================================
@@ -281,7 +302,28 @@ struct UnitMap {
     // AO ray that completes the count stores the pixel (fitm in k_trace); the rest go through k_finish,
     // flagged as with fit
     uint32_t fitm;
+    // 1: out8[f] is this rank's PACKED shard buffer of frame f (k_shard_copy's layout: the shard's k-th tile
+    // at k * 1024 pixels, rows of 32 within the tile), written in place of the framebuffer, so a sharded
+    // batch needs no pack launch before its gather (RGBA8 only; rt_terrain_render_batch_packed)
+    uint32_t packed;
 };
+
+// Where pixel (px, py) of lane `lane` of unit u goes in its frame's RGBA8 output: the framebuffer row-major,
+// or (UnitMap::packed) the unit's tile u >> 4 of the shard at 1024 pixels each, row (sub >> 2) * 8 +
+// (lane >> 3) and column (sub & 3) * 8 + (lane & 7) of the tile (sub = u & 15; unit_pixel's mapping)
+__device__ __forceinline__ uint32_t out_index(const UnitMap& m, uint32_t u, uint32_t lane, uint32_t px, uint32_t py,
+                                              uint32_t W)
+{
+    if (m.packed)
+        return (u >> 4) * 1024u + ((u & 15u) >> 2) * 256u + (lane >> 3) * 32u + (u & 3u) * 8u + (lane & 7u);
+    return py * W + px;
+}
+// the same from a frame's sample id tl = u * 64 + lane (one sample per pixel): its bits 0-2 (lane & 7) stay,
+// 6-7 (u & 3) -> 3-4, 3-5 (lane >> 3) -> 5-7, 8-9 -> 8-9 (sub >> 2), 10.. (the shard's tile) stay
+__device__ __forceinline__ uint32_t packed_index(uint32_t tl)
+{
+    return (tl & ~0xf8u) | ((tl >> 3) & 0x18u) | ((tl << 2) & 0xe0u);
+}
 
 __device__ __forceinline__ bool unit_pixel(const UnitMap& m, uint32_t f, uint32_t u, uint32_t lane, uint32_t W,
                                            uint32_t H, uint32_t* px, uint32_t* py)
@@ -376,7 +418,8 @@ constexpr uint32_t kOrderLdsBuckets = 144u * 1024u;
 constexpr uint32_t kOrderBatchUnitsPerWave = 4u;
 __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
                                                 uint32_t* __restrict__ order, uint32_t* __restrict__ counters,
-                                                const uint32_t* wait_ctl, uint32_t wait_total, uint32_t* zero_ctl)
+                                                const uint32_t* wait_ctl, uint32_t wait_total, uint32_t* zero_ctl,
+                                                uint32_t* host_flag, uint32_t* gate)
 {
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
@@ -385,6 +428,10 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
     // of the next batch's prepass that k_trace runs (FusedPrepass)
     if (blockIdx.x == 0 && threadIdx.x < RT_CTR_BYTES / 4) counters[threadIdx.x] = 0u;
     if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 2) zero_ctl[threadIdx.x] = 0u;
+    if (gate) { // the gated launch: this workgroup's frames' task flags and ray counters start at zero
+        const uint32_t g0 = m.order_batch ? 0u : blockIdx.x, g1 = m.order_batch ? m.n_frames : blockIdx.x + 1u;
+        for (uint32_t i = g0 * RT_GATE_WORDS + threadIdx.x; i < g1 * RT_GATE_WORDS; i += blockDim.x) gate[i] = 0u;
+    }
     if (wait_ctl) {
         // this batch's prepass runs inside the previous batch's k_trace (FusedPrepass): wait until its
         // rays are in (each task stored its line with sc1, waited, then added to ctl[1]).  The tasks are
@@ -396,7 +443,12 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
             while (__hip_atomic_load(wait_ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < wait_total) {
                 __builtin_amdgcn_s_sleep(8);
                 if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+                    // fail safe: the frames of this batch may trace from incomplete CameraResults.  The
+                    // device's sticky flag (rt_device_check) and the GPU's host-mapped word, which every
+                    // later C-ABI call on this GPU reads (RT_ERR_STATE until rt_device_check clears it)
                     atomicOr(counters + RT_CTR_BYTES / 4, RT_FLAG_PREPASS_TIMEOUT);
+                    if (host_flag) __hip_atomic_store(host_flag, RT_FLAG_PREPASS_TIMEOUT, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_SYSTEM);
                     break;
                 }
             }
@@ -539,6 +591,12 @@ __device__ __forceinline__ float4 ld_rec(const float4* base, uint32_t i)
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(base), (short)0, 0x7fffffff, 0x00020000);
     const v4f_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 16 /* sc1 */);
     return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i)
+{
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), (short)0, 0x7fffffff, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 16 /* sc1 */);
 }
 __device__ __forceinline__ float4 ld_fresh(const float4* p)
 {
@@ -805,8 +863,13 @@ __device__ __forceinline__ void fit_store(const RtConsts* k, const UnitMap& m, c
                                           uint32_t px8)
 {
     const uint32_t f = frame_of(m, t), W = (uint32_t)k->width;
+    const uint32_t tl = t - f * m.frame_samples;
+    if (m.packed) { // out_index's packed position is a bit permutation of the sample id (one sample per pixel)
+        gptr(fr.out8[f])[late(packed_index(tl))] = px8;
+        return;
+    }
     uint32_t px, py;
-    unit_pixel(m, f, (t - f * m.frame_samples) >> 6, t & 63u, W, (uint32_t)k->height, &px, &py);
+    unit_pixel(m, f, tl >> 6, t & 63u, W, (uint32_t)k->height, &px, &py);
     gptr(fr.out8[f])[(size_t)late(py) * W + px] = px8;
 }
 
@@ -914,6 +977,7 @@ struct TraceQueues {
     uint32_t pad1;
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
+    uint32_t d_head, d_tail;   // the gated launch: the block's deferred units, defer[d_head, d_tail) in HBM
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
     uint32_t ao_ctr[kAoSlots / 2]; // AO slot s: bits 16 (s & 1) + 0..4 rays finished, + 5..9 occluded
@@ -976,7 +1040,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                                                 uint32_t* __restrict__ aocc, uint32_t* __restrict__ counters,
                                                 RtStats* stats, uint32_t long_batch, uint32_t refill_idle,
                                                 uint32_t compact_live, uint32_t long_ring_cap, uint32_t fin_slots,
-                                                FusedPrepass np)
+                                                FusedPrepass np, GatedPrepass gp)
 {
     // one LDS array (the noise image at address 0, then the frame table, the rings and the STATS
     // kernels' block counters)
@@ -996,6 +1060,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.ls_top = 0;
         q.f_top = fin_slots;
         q.overflow = 0;
+        q.d_head = q.d_tail = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
@@ -1379,11 +1444,16 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (m.fit) {
                     // the pixel is final now (no AO), or its unoccluded value is (ao_factor(0, 1) = 1) and
                     // the AO ray carries the occluded one (ao_factor(1, 1)); no sample, no k_finish
-                    if (!(RT_DIAG_SKIP & 2)) gptr(ft->out8[f])[(size_t)late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
+                    if (!(RT_DIAG_SKIP & 2)) {
+                        const uint32_t tl = t - f * m.frame_samples; // (one sample per pixel)
+                        gptr(ft->out8[f])[m.packed ? late(packed_index(tl)) : late(h.py) * W + h.px] = fit_pixel(v, 1.0f);
+                    }
                     if (k->ao_samples) ao_aux = kAuxAOCand | (fit_pixel(v, ao_factor(1u, 1)) & 0xffffffu);
                 } else if (m.fitm && aux_ao_slot(ao_aux)) {
                     // the colour the AO ray completing the count finishes with, and where: frame << 23 | pixel
-                    cpl[late(ao_aux & 255u)] = make_float4(v.x, v.y, v.z, __uint_as_float((f << 23) | (h.py * W + h.px)));
+                    const uint32_t tl = t - f * m.frame_samples;
+                    cpl[late(ao_aux & 255u)] =
+                        make_float4(v.x, v.y, v.z, __uint_as_float((f << 23) | (m.packed ? packed_index(tl) : h.py * W + h.px)));
                 } else if (!(RT_DIAG_SKIP & 4)) {
                     sample_store(k, samples, t, v);
                 }
@@ -1437,7 +1507,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // bit-identical to density_nomadplains), that frame's camerarays constants, frame 0's launch
     // constants.  The 8 results form one 128-B line of CameraResults, stored whole by one sc1
     // instruction; after the store is acknowledged the task adds 8 to ctl[1] (the next k_order polls it).
-    auto do_prepass = [&](uint32_t qt) {
+    // own (the gated launch, GatedPrepass): a task of THIS batch's prepass (pft = ft); after its line it
+    // flags the task (sc1 store) and adds 8 to its frame's ray counter; the frame's last task derives the
+    // frame's CellDistance (the API's array: units compute their own cells' brackets, gate_ready)
+    auto do_prepass = [&](const FrameTable* __restrict__ pft, uint32_t qt, bool own) {
         if constexpr (L == RT_NOMADPLAINS) {
             constexpr uint32_t LPR = RT_FUSE_RAYS_PER_TASK;
             const uint32_t f = qt / RT_FUSE_TASKS_PER_FRAME;
@@ -1445,8 +1518,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             const uint32_t lid = late(lane);
             const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
             Ctx cp = c;
-            cp.k = np.ft->kcam[0];
-            cp.kf = (KPtr)np.ft->kcam[f];
+            cp.k = pft->kcam[0];
+            cp.kf = (KPtr)pft->kcam[f];
             cp.eye = rtm::mk(uniform_f(cp.kf->eye[0]), uniform_f(cp.kf->eye[1]), uniform_f(cp.kf->eye[2]));
             cp.sun = rtm::mk(uniform_f(cp.kf->sun[0]), uniform_f(cp.kf->sun[1]), uniform_f(cp.kf->sun[2]));
             const uint32_t tx = ray % RT_CAMERA_RES, ty = ray / RT_CAMERA_RES;
@@ -1472,13 +1545,100 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (j == 0u) {
                 typedef float v4f __attribute__((ext_vector_type(4)));
                 const v4f v = {rr.pd.x, rr.pd.y, rr.pd.z, rr.pd.w};
-                float4* dst = np.ft->cam[f] + ray;
+                float4* dst = pft->cam[f] + ray;
                 asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(v) : "memory");
             }
             asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-            if (lane == 0) __hip_atomic_fetch_add(np.ctl + 1, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
+            if (!own) {
+                if (lane == 0) __hip_atomic_fetch_add(np.ctl + 1, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+                return;
+            }
+            typedef uint32_t __attribute__((address_space(1))) guint;
+            guint* gf = (guint*)(gp.gate + f * RT_GATE_WORDS);
+            uint32_t old = 0;
+            if (lane == 0) {
+                __hip_atomic_store(gf + (qt - f * RT_FUSE_TASKS_PER_FRAME), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                old = __hip_atomic_fetch_add(gf + RT_GATE_CTR, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if ((uint32_t)__builtin_amdgcn_readfirstlane(old) == RT_CAMERA_RES * RT_CAMERA_RES - RT_FUSE_RAYS_PER_TASK) {
+                // the frame's last task (its add returned last): every ray is in
+                const float4* cam = pft->cam[f];
+                float2* cells = pft->cells[f];
+                for (uint32_t c = late(lane); c < RT_CAMERA_RES * RT_CAMERA_RES; c += 64u)
+                    cells[c] = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); },
+                                                  (int)(c % RT_CAMERA_RES), (int)(c / RT_CAMERA_RES));
+            }
         }
+    };
+
+    // ---- the gated launch (GatedPrepass): may unit (f, u) start? ----
+    // Its lanes' cells (the corner pixels' cells bound them: the cell index grows with the pixel) read
+    // CameraResults rays of rows cy0 - 2 .. cy1 + 2 and columns cx0 - 2 .. cx1 + 2 (setTargetDepths'
+    // 5 x 5 taps, clamped; its edge extrapolation reads inside that range).  Ready when the frame's ray
+    // counter is complete, or every task (8 rays of a row) covering that range has flagged.  sc1 polls
+    // (the hand-off: each task wave stored its line sc1 and waited before its flag store / counter add).
+    typedef const uint32_t __attribute__((address_space(1))) gcuint;
+    uint32_t gate_done = 0u; // frames whose ray counter this wave has seen complete (wave-uniform)
+    auto gate_ready = [&](uint32_t f, uint32_t u) -> bool {
+        if ((gate_done >> f) & 1u) return true;
+        const uint32_t* gf = gp.gate + f * RT_GATE_WORDS;
+        if (__hip_atomic_load((gcuint*)(gf + RT_GATE_CTR), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+            (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES)) {
+            gate_done |= 1u << f;
+            return true;
+        }
+        uint32_t px0, py0;
+        unit_pixel(m, f, u, 0u, W, H, &px0, &py0);
+        if (px0 >= W || py0 >= H) return true; // no lane of the unit is in the frame
+        const uint32_t px1 = px0 + 7u < W ? px0 + 7u : W - 1u, py1 = py0 + 7u < H ? py0 + 7u : H - 1u;
+        auto cell_of = [&](uint32_t p, float r) {
+            return __builtin_amdgcn_readfirstlane((int)rtm::floor(((float)p * r) * 32.0f));
+        };
+        const int cx0 = cell_of(px0, k->rcp_w), cx1 = cell_of(px1, k->rcp_w);
+        const int cy0 = cell_of(py0, k->rcp_h), cy1 = cell_of(py1, k->rcp_h);
+        const int xlo = cx0 - 2 < 0 ? 0 : cx0 - 2, xhi = cx1 + 2 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cx1 + 2;
+        const int ylo = cy0 - 2 < 0 ? 0 : cy0 - 2, yhi = cy1 + 2 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cy1 + 2;
+        constexpr int kTaskRow = RT_CAMERA_RES / RT_FUSE_RAYS_PER_TASK; // 4 tasks per prepass row
+        const int tlo = xlo / RT_FUSE_RAYS_PER_TASK, thi = xhi / RT_FUSE_RAYS_PER_TASK;
+        // lane p: row ylo + p / 4, task p % 4 of that row (rows <= 32: two rounds at most)
+        const uint32_t gbase = f * RT_GATE_WORDS + (uint32_t)ylo * kTaskRow;
+        const uint32_t nflags = (uint32_t)(yhi - ylo + 1) * kTaskRow;
+        bool ok = true;
+        for (uint32_t p = lane; p < nflags; p += 64u) {
+            const int t = (int)(p & (kTaskRow - 1));
+            if (t >= tlo && t <= thi)
+                ok = ok && __hip_atomic_load((gcuint*)(gp.gate + gbase + p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        }
+        return __ballot(!ok) == 0ull;
+    };
+    // the block's deferred units (not ready when taken): a FIFO in HBM under the block's lock, retried
+    // before new units are taken.  A full list (never expected: 1024 per block) makes the wave wait instead.
+    uint32_t* const dq = gp.defer + (size_t)blockIdx.x * RT_DEFER_CAP;
+    auto defer_push = [&](uint32_t qi) -> bool {
+        q_lock(&q.lock, lane);
+        const uint32_t t = vload(q.d_tail), h = vload(q.d_head);
+        const bool ok = t - h < (uint32_t)RT_DEFER_CAP;
+        if (ok && lane == 0) dq[t % RT_DEFER_CAP] = qi;
+        __builtin_amdgcn_s_waitcnt(0);
+        if (ok && lane == 0) q.d_tail = t + 1u;
+        q_unlock(&q.lock, lane);
+        return ok;
+    };
+    auto defer_pop = [&](uint32_t* qi) -> bool {
+        if (vload(q.d_tail) == vload(q.d_head)) return false;
+        q_lock(&q.lock, lane);
+        const uint32_t t = vload(q.d_tail), h = vload(q.d_head);
+        uint32_t v = 0;
+        if (t != h) {
+            v = ld_u32(dq, h % RT_DEFER_CAP); // another wave of this block stored it: L1-bypassing
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) q.d_head = h + 1u;
+        }
+        q_unlock(&q.lock, lane);
+        *qi = (uint32_t)__builtin_amdgcn_readfirstlane(v);
+        return t != h;
     };
 
     // ---- one 8x8 primary unit ----
@@ -1491,7 +1651,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         float plane_x = 0.0f;
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
-            plane_x = gptr(ft->cells[f])[(uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f))].x;
+            const uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
+            if (gp.tasks) { // the gated launch: the cell's setTargetDepths from its CameraResults (gate_ready passed)
+                const float4* cam = ft->cam[f];
+                plane_x = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); }, (int)(cell % RT_CAMERA_RES),
+                                       (int)(cell / RT_CAMERA_RES)).x;
+            } else {
+                plane_x = gptr(ft->cells[f])[cell].x;
+            }
         }
         for (uint32_t a = 0; a < aa; ++a) {
             const uint32_t t = f * m.frame_samples + (u * 64u + lane) * aa + a;
@@ -1536,10 +1703,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (!hit) {
                     const float4 v = miss_sample(cf, pxf + k->aa_off[a][0], pyf + k->aa_off[a][1], rr.pd.w, rr.fc);
                     if (aa == 1u) { // the pixel is final (k_finish's sum of one sample times rcp(1) is v itself)
-                        const size_t o = (size_t)py * W + px;
-                        if (!(RT_DIAG_SKIP & 1))
-                            gptr(ft->out8[f])[o] = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
-                        if (float4* o32 = ft->out32[f]) gstore(o32 + o, make_float4(v.x, v.y, v.z, 1.0f));
+                        const uint32_t px8 = unorm8(v.x) | (unorm8(v.y) << 8) | (unorm8(v.z) << 16) | 0xff000000u;
+                        if (m.packed) { // a packed shard buffer (no float output then)
+                            if (!(RT_DIAG_SKIP & 1)) gptr(ft->out8[f])[packed_index(late(u * 64u + lane))] = px8;
+                        } else {
+                            const size_t o = (size_t)py * W + px;
+                            if (!(RT_DIAG_SKIP & 1)) gptr(ft->out8[f])[o] = px8;
+                            if (float4* o32 = ft->out32[f]) gstore(o32 + o, make_float4(v.x, v.y, v.z, 1.0f));
+                        }
                     } else {
                         samples[t] = v;
                     }
@@ -1580,15 +1751,27 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     const uint32_t first_qi = first_unit_index(counters, lane); // scalar, formed before the loop
     bool first_unit = true;
     bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
+    bool gp_open = gp.tasks != 0u; // this batch's own prepass tasks may remain (GatedPrepass)
+    const uint32_t n_total = m.n_units * m.n_frames;
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
-        // the next batch's prepass first (after a wave's static first unit): its k_order waits for it.
-        // A wave leaves only after it found no task left, so every task is taken by a resident wave.
         if constexpr (L == RT_NOMADPLAINS) {
+            // the gated launch: this batch's own prepass before anything else (every unit waits for some
+            // of its rays).  Tasks are taken by resident waves, so every taken task finishes.
+            if (gp_open) {
+                const uint32_t qt = wave_fetch(&counters[RT_CTR_GATE], lane);
+                if (qt < gp.tasks) {
+                    do_prepass(ft, qt, true);
+                    continue;
+                }
+                gp_open = false;
+            }
+            // the next batch's prepass first (after a wave's static first unit): its k_order waits for it.
+            // A wave leaves only after it found no task left, so every task is taken by a resident wave.
             if (np_open && !first_unit) {
                 const uint32_t qt = wave_fetch(np.ctl, lane);
                 if (qt < np.tasks) {
-                    do_prepass(qt);
+                    do_prepass(np.ft, qt, false);
                     continue;
                 }
                 np_open = false;
@@ -1618,21 +1801,48 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }
-        if (!drained || first_unit) { // a wave's static first unit is taken even after the queue drained
+        // the gated launch: units that were not ready when taken wait in the block's deferred list
+        const bool deferred = gp.tasks != 0u && vload(q.d_tail) != vload(q.d_head);
+        if (!drained || first_unit || deferred) { // a wave's static first unit is taken even after the queue drained
             if (lane == 0) atomicAdd(&q.active, 1u);
-            const uint32_t qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
-            first_unit = false;
-            if (qi < m.n_units * m.n_frames) {
-                // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
+            // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
+            auto unit_of = [&](uint32_t qi, uint32_t* f, uint32_t* u) {
                 const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);
-                do_unit(e >> 24, (e & 0xffffffu) * 16u + (qi & 15u));
+                *f = e >> 24;
+                *u = (e & 0xffffffu) * 16u + (qi & 15u);
+            };
+            // one unit to run, from the deferred list or the queue (do_unit is inlined once)
+            bool run = false;
+            uint32_t qi = 0, f = 0, u = 0;
+            // try: unit qi may run now, or goes (back) to the deferred list, or (the list is full) is waited for
+            bool wait = false;
+            auto try_unit = [&]() {
+                unit_of(qi, &f, &u);
+                if (gp.tasks == 0u || gate_ready(f, u)) run = true;
+                else if (!defer_push(qi)) run = wait = true;
+            };
+            if (deferred && defer_pop(&qi)) try_unit(); // the oldest deferred unit first, if its rays are in
+            if (!run && (!drained || first_unit)) {
+                qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+                first_unit = false;
+                if (qi < n_total) try_unit();
+                else if (lane == 0) q.drained = 1u;
+            } else if (!run) {
+                __builtin_amdgcn_s_sleep(4); // drained: only deferred units whose rays are still marching
+            }
+            if (run) {
+                if (wait)
+                    while (!gate_ready(f, u)) __builtin_amdgcn_s_sleep(8);
+                do_unit(f, u);
                 WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
-            } else if (lane == 0) q.drained = 1u;
+            }
             if (lane == 0) atomicSub(&q.active, 1u);
             continue;
         }
         // drained and nothing queued: leave once no wave of the block can still push
-        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) break;
+        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u &&
+            (gp.tasks == 0u || vload(q.d_tail) == vload(q.d_head)))
+            break;
         __builtin_amdgcn_s_sleep(2);
         WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
     }
@@ -1728,7 +1938,7 @@ __global__ void __launch_bounds__(1024) k_finish(const RtConsts* __restrict__ k,
         c0 = c0 * ia;
         c1 = c1 * ia;
         c2 = c2 * ia;
-        size_t o = (size_t)py * (size_t)k->width + px;
+        size_t o = out_index(m, u, lane, px, py, (uint32_t)k->width);
         if (!(RT_DIAG_SKIP & 64)) out8[o] = unorm8(c0) | (unorm8(c1) << 8) | (unorm8(c2) << 16) | 0xff000000u;
         if (out32) gstore(out32 + o, make_float4(c0, c1, c2, 1.0f));
     }
@@ -1868,10 +2078,13 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     m.cells_from_cam = (uint32_t)a.cells_from_cam;
     m.fit = (uint32_t)a.fit;
     m.fitm = kAoSlots > 0u ? (uint32_t)a.fitm : 0u;
+    m.packed = (uint32_t)a.packed;
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
+    // (fuse_next.ctl is zeroed even with no tasks: RT_DEVICE_DEBUG_WITHHOLD_FUSE's timeout test)
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue,
-                       a.wait_ctl, a.wait_total, a.fuse_next.tasks ? a.fuse_next.ctl : nullptr);
+                       a.wait_ctl, a.wait_total, a.fuse_next.ctl, a.host_flag, a.gated.tasks ? a.gated.gate : nullptr);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
+    if (a.after_order_fuse) (void)hipEventRecord(a.after_order_fuse, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill stacks
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
@@ -1880,7 +2093,7 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                            a.perm2d, a.grad, m,
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.cpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
-                           a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots, a.fuse_next);
+                           a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots, a.fuse_next, a.gated);
         // fit without AO: every hit pixel is final in k_trace
         if (!(m.fit && a.ao_samples == 0))
             hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);

@@ -125,6 +125,8 @@ struct rt_device_s {
     float4* fin = nullptr;
     float4* finpool = nullptr; // k_trace's per-block fin pools (RT_FIN_SLOTS slots of 3 float4 per block)
     float4* cpool = nullptr;   // k_trace's per-block AO colour pools (RT_AO_POOL_SLOTS float4 per block)
+    uint32_t* gate = nullptr;  // the gated launch (GatedPrepass): per frame task flags + ray counter
+    uint32_t* defer = nullptr; //   and k_trace's per-block deferred units (RT_DEFER_CAP per block)
     uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
@@ -138,6 +140,8 @@ struct rt_device_s {
         hipGraphExec_t exec = nullptr;
     } graph_pre, graph_trace;
     unsigned long long graph_captures = 0, graph_launches = 0;
+    // renders this device led: gated launches (prepass inside the trace) and prepass launches (rt_device_info)
+    unsigned long long gated_launches = 0, prepass_launches = 0;
     // frame tables (rt_kernels.h FrameTable): the batch's, and the split prepass's frame subset
     struct DevTable {
         FrameTable* d = nullptr;
@@ -165,6 +169,9 @@ struct rt_device_s {
     uint32_t* fctl = nullptr;
     std::vector<rt_device_s*> fuse_devs; // the devices of its frames
     hipEvent_t ev_fuser_done = nullptr;
+    // recorded after the fusing launch's k_order, which zeroes fctl: this batch's own k_order (its poll of
+    // fctl) waits for it, so it can never pass on the previous fused round's count
+    hipEvent_t ev_fuse_order = nullptr;
     // output path: BGRX staging for the recorder / rt_device_readback_bgrx (allocated on first use)
     uint32_t* bgrx = nullptr;
     struct rt_recorder_s* recorder = nullptr; // DeviceDirect3D::recorder (setRecorder), not owned
@@ -466,6 +473,50 @@ int sync_shader(rt_device dev, Shader* s)
     return RT_OK;
 }
 
+// The GPU's host-mapped flag word (one per GPU ordinal, allocated on first use): k_order stores
+// RT_FLAG_PREPASS_TIMEOUT there when its bounded wait for a fused prepass gives up, so the frames of
+// that batch may be wrong.  Every C-ABI call that launches on or reads from a device of that GPU checks
+// it (host_flag_check) and fails with RT_ERR_STATE until rt_device_check clears it: a host that follows
+// the reference's call sequence and never calls rt_device_check still cannot read such a frame.
+std::mutex g_host_flag_mu;
+std::map<int, std::pair<uint32_t*, uint32_t*>> g_host_flags; // ordinal -> (host pointer, device pointer)
+
+uint32_t* host_flag_device(int ordinal)
+{
+    std::lock_guard<std::mutex> lk(g_host_flag_mu);
+    auto it = g_host_flags.find(ordinal);
+    if (it != g_host_flags.end()) return it->second.second;
+    void* h = nullptr;
+    void* dptr = nullptr;
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    if (hipHostGetDevicePointer(&dptr, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return nullptr;
+    }
+    std::memset(h, 0, 64);
+    g_host_flags[ordinal] = {(uint32_t*)h, (uint32_t*)dptr};
+    return (uint32_t*)dptr;
+}
+
+uint32_t host_flag_read(int ordinal, bool clear)
+{
+    std::lock_guard<std::mutex> lk(g_host_flag_mu);
+    auto it = g_host_flags.find(ordinal);
+    if (it == g_host_flags.end()) return 0;
+    volatile uint32_t* w = it->second.first;
+    const uint32_t v = *w;
+    if (clear) *w = 0;
+    return v;
+}
+
+int host_flag_check(rt_device d)
+{
+    if (d && host_flag_read(d->ordinal, false))
+        return fail(RT_ERR_STATE, "GPU %d: a k_order wait for a fused prepass timed out; frames traced since may be "
+                    "wrong (rt_device_check reports and clears it)", d->ordinal);
+    return RT_OK;
+}
+
 RtLaunch make_launch(rt_device dev, Shader* s)
 {
     RtLaunch a;
@@ -500,6 +551,10 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.fuse_next = FusedPrepass{nullptr, nullptr, 0u};
     a.wait_ctl = nullptr;
     a.wait_total = 0;
+    a.after_order_fuse = nullptr;
+    a.host_flag = host_flag_device(dev->ordinal);
+    a.gated = GatedPrepass{nullptr, nullptr, 0u};
+    a.packed = 0;
     return a;
 }
 
@@ -549,6 +604,8 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->finpool, (size_t)dev->num_cus * RT_FIN_SLOTS * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->cpool, (size_t)dev->num_cus * RT_AO_POOL_SLOTS * sizeof(float4)));
+        if (!dev->gate) HIP_TRY(hipMalloc(&dev->gate, (size_t)RT_MAX_BATCH * RT_GATE_WORDS * sizeof(uint32_t)));
+        if (!dev->defer) HIP_TRY(hipMalloc(&dev->defer, (size_t)dev->num_cus * RT_DEFER_CAP * sizeof(uint32_t)));
         dev->hitq_n = hq_need;
         dev->spill_long_n = ls_need;
     }
@@ -676,13 +733,13 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)hitq, (void*)finpool, (void*)cpool, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
+                    (void*)hitq, (void*)finpool, (void*)cpool, (void*)gate, (void*)defer, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
     if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
-    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in, ev_fuser_done})
+    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in, ev_fuser_done, ev_fuse_order})
         if (e) (void)hipEventDestroy(e);
     for (auto& pr : ev_pool) {
         (void)hipEventDestroy(pr.first);
@@ -696,7 +753,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
 {
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
-    const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS;
+    const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS |
+                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_PREPASS_INLINE;
     if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -745,6 +803,7 @@ int rt_device_present(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
     HIP_TRY(hipGetLastError());
+    if (int rc = host_flag_check(d)) return rc;
     // DeviceDirect3D.cpp:242-256: while recording, the frame goes to the recorder
     if (d->recorder && rt_recorder_is_recording(d->recorder) == 1) return recorder_capture(d->recorder);
     return RT_OK;
@@ -762,7 +821,7 @@ int rt_device_synchronize(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
     HIP_TRY(hipStreamSynchronize(d->stream));
-    return RT_OK;
+    return host_flag_check(d);
 }
 
 int rt_device_readback(rt_device d, void* dst, size_t row_pitch)
@@ -773,7 +832,7 @@ int rt_device_readback(rt_device d, void* dst, size_t row_pitch)
     HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->fb8, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
                              hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
-    return RT_OK;
+    return host_flag_check(d);
 }
 
 // GPU swizzle into the device BGRX buffer (rt_launch_bgrx), on the device stream
@@ -794,7 +853,7 @@ int rt_device_readback_bgrx(rt_device d, void* dst, size_t row_pitch)
     HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->bgrx, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
                              hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
-    return RT_OK;
+    return host_flag_check(d);
 }
 
 int rt_device_readback_float(rt_device d, float* dst)
@@ -803,7 +862,7 @@ int rt_device_readback_float(rt_device d, float* dst)
     if (!d->fb32) return fail(RT_ERR_STATE, "device created without RT_DEVICE_FLOAT_OUTPUT");
     HIP_TRY(hipMemcpyAsync(dst, d->fb32, (size_t)d->width * d->height * 16, hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
-    return RT_OK;
+    return host_flag_check(d);
 }
 
 int rt_device_size(rt_device d, int* w, int* h)
@@ -872,6 +931,16 @@ int rt_device_kernel_time(rt_device d, double* total_ms, int* launches)
     return RT_OK;
 }
 
+int rt_device_info(rt_device d, int key, unsigned long long* out)
+{
+    if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
+    switch (key) {
+    case RT_INFO_GATED_LAUNCHES: *out = d->gated_launches; return RT_OK;
+    case RT_INFO_PREPASS_LAUNCHES: *out = d->prepass_launches; return RT_OK;
+    default: return fail(RT_ERR_INVALID, "unknown rt_device_info key %d", key);
+    }
+}
+
 int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned long long* launches)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
@@ -904,6 +973,7 @@ int rt_device_check(rt_device d)
     HIP_TRY(hipStreamSynchronize(d->stream));
     uint32_t flags = 0;
     HIP_TRY(hipMemcpy(&flags, reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 4, hipMemcpyDeviceToHost));
+    flags |= host_flag_read(d->ordinal, true); // the GPU's fail-safe word (a timeout on another device's batch)
     if (!flags) return RT_OK;
     HIP_TRY(hipMemset(reinterpret_cast<char*>(d->queue) + RT_CTR_BYTES, 0, 4));
     return fail(RT_ERR_STATE, "device flags 0x%x:%s%s%s", flags,
@@ -1094,7 +1164,9 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     Shader* s = c->shader;
     if (!s) return RT_OK; // ComputeDirect3D.cpp:532
     rt_device dev = c->dev;
-    int rc = check_texture(s);
+    int rc = host_flag_check(dev);
+    if (rc) return rc;
+    rc = check_texture(s);
     if (rc) return rc;
     rc = sync_shader(dev, s);
     if (rc) return rc;
@@ -1186,6 +1258,7 @@ void* rt_array_map(rt_array a)
         fail(RT_ERR_HIP, "map readback failed");
         return nullptr;
     }
+    if (host_flag_check(a->dev)) return nullptr;
     return a->host.data();
 }
 
@@ -1216,13 +1289,15 @@ enum { PH_PRE = 1, PH_TRACE = 2, PH_STAGE = 4 };
 // the wait of its k_order for this batch's prepass that the previous k_trace ran
 struct TraceFuse {
     FusedPrepass next{nullptr, nullptr, 0u};
+    hipEvent_t next_after_order = nullptr; // recorded after this launch's k_order (it zeroes next.ctl)
     const uint32_t* wait_ctl = nullptr;
     uint32_t wait_total = 0;
 };
 static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
                                 int shard_count, bool feed, int phases = PH_PRE | PH_TRACE, int first = 0,
                                 int count = -1, float4* camera_out = nullptr, const float4* camera_in = nullptr,
-                                const TraceFuse* fuse = nullptr);
+                                const TraceFuse* fuse = nullptr, uint8_t* packed_dst = nullptr,
+                                size_t packed_stride = 0);
 
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
@@ -1256,7 +1331,9 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)(uintptr_t)a.spill_long, (uint64_t)a.hit_cap, (uint64_t)a.long_spill_cap,
                           (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)a.fit, (uint64_t)a.fitm, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool, (uint64_t)(uintptr_t)a.cpool,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
-                          (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames};
+                          (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames,
+                          (uint64_t)(uintptr_t)a.gated.gate, (uint64_t)(uintptr_t)a.gated.defer, (uint64_t)a.gated.tasks,
+                          (uint64_t)a.packed};
     k.insert(k.end(), std::begin(v), std::end(v));
 }
 
@@ -1394,10 +1471,13 @@ int batch_end(const rt_compute* scrs, int n, Batch& b)
 // (n x 1024 float4) for the split prepass of rt_terrain_prepass_batch / rt_terrain_trace_batch.
 static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
                                 int shard_count, bool feed, int phases, int first, int count, float4* camera_out,
-                                const float4* camera_in, const TraceFuse* fuse)
+                                const float4* camera_in, const TraceFuse* fuse, uint8_t* packed_dst,
+                                size_t packed_stride)
 {
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
     if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
+    if (scrs && n >= 1 && scrs[0] && scrs[0]->dev)
+        if (int rc0 = host_flag_check(scrs[0]->dev)) return rc0;
     if (cams && scrs && n >= 1 && n <= RT_MAX_BATCH && scrs[0] && scrs[0]->dev) {
         // a pending ahead prepass writes these frames' CameraResults: it comes before anything this
         // call queues, the constant uploads of batch_begin included (they rewrite the block the
@@ -1456,18 +1536,41 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     }
     if ((rc = ensure_split_buffers(dev, b.s0->aa, b.s0->ao, n))) return rc;
     RtLaunch la_cam = make_launch(dev, cams[0]->shader), la_scr = make_launch(dev, scrs[0]->shader);
-    if (!graphs && dev->ev_order) {
-        la_scr.after_order = dev->ev_order; // rt_terrain_prepass_ahead: the frames' CameraResults are read
+    if (packed_dst) { // rt_terrain_render_batch_packed: frame f's shard pixels straight into its packed buffer
+        for (int f = 0; f < n; ++f) {
+            if (ft.out32[f]) return fail(RT_ERR_UNSUPPORTED, "packed output: RGBA8-only devices (no RT_DEVICE_FLOAT_OUTPUT)");
+            ft.out8[f] = reinterpret_cast<uint32_t*>(packed_dst + (size_t)f * packed_stride);
+        }
+        la_scr.packed = 1;
+    }
+    // The gated launch (GatedPrepass): a full nomadplains render runs its prepass
+    // inside its own k_trace, and each unit starts once the prepass rays its cells read are in, instead of
+    // a latency-bound prepass launch the whole trace waits for.  Not for the instrumented kernels (their
+    // prepass counts stay separate), the camera feed (it wants the CameraResults before the trace), a
+    // trace from gathered CameraResults, a fused prepass, or RT_DEVICE_PREPASS_INLINE.
+    const bool gated = phases == (PH_PRE | PH_TRACE) && !feed && !camera_in &&
+                       (!fuse || (fuse->wait_ctl == nullptr && fuse->next.ctl == nullptr)) &&
+                       b.s0->landscape == RT_NOMADPLAINS &&
+                       !(dev->flags & (RT_DEVICE_STATS | RT_DEVICE_PREPASS_INLINE));
+    if (gated) la_scr.gated = GatedPrepass{dev->gate, dev->defer, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+    // rt_terrain_prepass_ahead: ev_order follows the last read of the frames' CameraResults -- k_order's,
+    // or with the gated launch k_trace's (recorded after the trace below)
+    if (!graphs && dev->ev_order && !gated) {
+        la_scr.after_order = dev->ev_order;
         dev->order_recorded = true;
     }
     if ((rc = upload_frames(dev, dev->table, ft))) return rc;
     la_cam.frames = la_scr.frames = dev->table.d;
     la_cam.frames_host = la_scr.frames_host = ft;
     la_cam.n_frames = la_scr.n_frames = (uint32_t)n;
-    // setTargetDepths runs at the start of the tracescreen launch (k_order), from the CameraResults
-    la_scr.cells_from_cam = 1;
+    // setTargetDepths runs at the start of the tracescreen launch (k_order), from the CameraResults; the
+    // gated launch's k_order orders the units by the frames' previous CellDistance instead (scheduling
+    // only: each unit derives its cells' brackets from this frame's rays, and the frame's last prepass
+    // task writes its CellDistance)
+    la_scr.cells_from_cam = gated ? 0 : 1;
     if (fuse) {
         la_scr.fuse_next = fuse->next;
+        la_scr.after_order_fuse = fuse->next_after_order;
         la_scr.wait_ctl = fuse->wait_ctl;
         la_scr.wait_total = fuse->wait_total;
     }
@@ -1481,9 +1584,11 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
         la_scr.fitm = la_scr.fitm && ft.out32[f] == nullptr;
     }
     auto pre = [&] {
-        if (phases & PH_PRE) rt_launch_camerarays_batch(la_cam);
+        if ((phases & PH_PRE) && !gated) rt_launch_camerarays_batch(la_cam);
     };
-    if (graphs) {
+    if (gated) ++dev->gated_launches;
+    else if (phases & PH_PRE) ++dev->prepass_launches;
+    if (graphs && !gated) {
         // the constant / table uploads stay outside: they precede the replay on this stream
         std::vector<uint64_t> kp;
         key_launch(kp, la_cam);
@@ -1519,6 +1624,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             trace();
         }
     }
+    if (gated && !graphs && dev->ev_order) { // k_trace read (and wrote) the frames' CameraResults
+        HIP_TRY(hipEventRecord(dev->ev_order, dev->stream));
+        dev->order_recorded = true;
+    }
     for (int f = 0; f < n; ++f)
         if (cam_copy[f])
             HIP_TRY(hipMemcpyAsync(cam_copy[f], camera_in + (size_t)f * 1024, 1024 * sizeof(float4),
@@ -1529,6 +1638,24 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
 int rt_terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank, int shard_count)
 {
     return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false);
+}
+
+int rt_terrain_render_batch_packed(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
+                                   int shard_count, void* dst_device, size_t frame_stride)
+{
+    if (!dst_device || shard_count < 2) return fail(RT_ERR_INVALID, "packed output: a device buffer and shard_count >= 2");
+    if (cams && scrs && n >= 1 && scrs[0] && scrs[0]->dev) {
+        const rt_device d = scrs[0]->dev;
+        size_t need = 0;
+        for (int f = 0; f < n; ++f) { // frame f traces shard (rank + f) % count (rotation, n > 1)
+            const int sh = n > 1 ? (shard_rank + f) % shard_count : shard_rank;
+            need = std::max(need, rt_shard_tiles(d->width, d->height, sh, shard_count) * RT_TILE * RT_TILE * 4);
+        }
+        if (frame_stride < need || frame_stride % 16) return fail(RT_ERR_INVALID, "packed output: frame_stride %zu < %zu bytes "
+                                                                   "or not 16-byte aligned", frame_stride, need);
+    }
+    return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, PH_PRE | PH_TRACE, 0, -1, nullptr,
+                                nullptr, nullptr, (uint8_t*)dst_device, frame_stride);
 }
 
 int rt_terrain_prepass_batch(const rt_compute* cams, const rt_compute* scrs, int n, int first, int count,
@@ -1559,6 +1686,7 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
     for (int f = 0; f < n; ++f)
         if (!cams[f] || !scrs[f] || cams[f]->dev != scrs[f]->dev) return fail(RT_ERR_INVALID, "computes must share a device");
     rt_device lead = scrs[0]->dev;
+    if (int rc0 = host_flag_check(lead)) return rc0;
     if (lead->flags & RT_DEVICE_GRAPH) return fail(RT_ERR_STATE, "the ahead prepass runs on a side stream: not with RT_DEVICE_GRAPH");
     if (lead->ahead_pending) return fail(RT_ERR_STATE, "a prepass is already ahead for this device's batch: trace it first");
     if (lead->fuse_state == rt_device_s::FUSE_FUSED && lead->ev_fuser_done) {
@@ -1623,6 +1751,7 @@ int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n
 {
     if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH || !scrs[0] || !scrs[0]->shader) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
     rt_device lead = scrs[0]->dev;
+    if (int rc0 = host_flag_check(lead)) return rc0;
     HIP_TRY(hipSetDevice(lead->ordinal));
     bool ahead = lead->ahead_pending && (size_t)n <= lead->ahead_cams.size();
     for (int f = 0; ahead && f < n; ++f)
@@ -1632,7 +1761,10 @@ int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n
     const int state = lead->fuse_state;
     if (ahead && state == rt_device_s::FUSE_FUSED) {
         // the previous k_trace ran this batch's prepass: k_order polls its ray counter, so the frames'
-        // devices need not wait for that whole kernel (their ahead_in event follows it)
+        // devices need not wait for that whole kernel (their ahead_in event follows it).  The poll comes
+        // after the fusing launch's k_order, which zeroed the counter (otherwise a k_order on
+        // this stream could run first and pass on the previous fused round's count)
+        HIP_TRY(hipStreamWaitEvent(lead->stream, lead->ev_fuse_order, 0));
         tf.wait_ctl = lead->fctl;
         tf.wait_total = (uint32_t)lead->fuse_n * (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES);
         for (rt_device d : lead->fuse_devs) d->ahead_in_pending = false;
@@ -1650,7 +1782,12 @@ int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n
     // landscape, noise tables and frame size)
     rt_device z = nullptr;
     const Shader* s0 = scrs[0]->shader;
-    if (s0->landscape == RT_NOMADPLAINS && !(lead->flags & (RT_DEVICE_STATS | RT_DEVICE_GRAPH))) {
+    // only a launch that runs k_trace can take it: a single-frame (or unrotated) shard past the last tile
+    // launches nothing (launch_split_l), and a batch fused there would wait for tasks no kernel runs
+    // 
+    const size_t frame_tiles = rt_shard_tiles(lead->width, lead->height, 0, 1);
+    const bool runs_trace = (n > 1 && shard_count > 1) || (size_t)shard_rank < frame_tiles;
+    if (runs_trace && s0->landscape == RT_NOMADPLAINS && !(lead->flags & (RT_DEVICE_STATS | RT_DEVICE_GRAPH))) {
         std::lock_guard<std::mutex> lk(g_stream_mu);
         auto& v = g_fuse_staged[lead->ordinal];
         for (auto it = v.begin(); it != v.end(); ++it) {
@@ -1668,7 +1805,13 @@ int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n
         // its staged constants and table are up, and its previous k_order (the last poll of its counters,
         // which this launch's k_order zeroes) is done
         HIP_TRY(hipStreamWaitEvent(lead->stream, z->ev_ahead, 0));
-        tf.next = FusedPrepass{z->fuse_table.d, z->fctl, (uint32_t)z->fuse_n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+        // (diagnostic RT_DEVICE_DEBUG_WITHHOLD_FUSE on the fusing device: no task runs, the counters are still
+        // zeroed, so z's k_order times out -- the fail-safe's test)
+        const uint32_t tasks = (lead->flags & RT_DEVICE_DEBUG_WITHHOLD_FUSE)
+                                   ? 0u : (uint32_t)z->fuse_n * (uint32_t)RT_FUSE_TASKS_PER_FRAME;
+        tf.next = FusedPrepass{z->fuse_table.d, z->fctl, tasks};
+        if (!z->ev_fuse_order) HIP_TRY(hipEventCreateWithFlags(&z->ev_fuse_order, hipEventDisableTiming));
+        tf.next_after_order = z->ev_fuse_order;
     }
     int rc = terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false, phases, 0, -1, nullptr, nullptr, &tf);
     if (z) {
@@ -1702,6 +1845,7 @@ static int shard_copy(const rt_device* devs, const int* shards, int count, void*
     if (!devs || !shards || !bufs || n < 0 || count < 1) return fail(RT_ERR_INVALID, "bad arguments");
     if (n == 0) return RT_OK;
     rt_device d0 = devs[0];
+    if (d0 && host_flag_check(d0)) return RT_ERR_STATE;
     for (int i = 0; i < n; ++i) {
         if (!devs[i] || !bufs[i] || shards[i] < 0 || shards[i] >= count) return fail(RT_ERR_INVALID, "bad arguments");
         if (devs[i]->width != d0->width || devs[i]->height != d0->height)

@@ -159,14 +159,21 @@ class Compute:
 class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
-    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False):
+    def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False,
+                 debug_withhold_fuse=False, prepass_inline=False):
         """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
         entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
-        shadows the fin[t] fallback; same bits)."""
+        shadows the fin[t] fallback; same bits).  debug_withhold_fuse: diagnostic
+        RT_DEVICE_DEBUG_WITHHOLD_FUSE (a trace this device leads runs none of the next batch's fused
+        prepass tasks, so that batch's wait times out: the fail-safe's test).  prepass_inline:
+        RT_DEVICE_PREPASS_INLINE (the prepass as its own launch before the trace, instead of the gated
+        launch that runs it inside the trace kernel; same bits)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
                       | (_native.RT_DEVICE_GRAPH if graph else 0)
-                      | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0))
+                      | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0)
+                      | (_native.RT_DEVICE_DEBUG_WITHHOLD_FUSE if debug_withhold_fuse else 0)
+                      | (_native.RT_DEVICE_PREPASS_INLINE if prepass_inline else 0))
         self._h = None
 
     def create(self):
@@ -213,6 +220,16 @@ class Device:
         s = _native.RtStats()
         check(lib().rt_device_stats_sized(self._h, C.byref(s), C.sizeof(s), 1 if reset else 0), "stats")
         return {n: int(getattr(s, n)) for n, _ in s._fields_}
+
+    def launch_info(self):
+        """(gated launches, prepass launches) of the renders this device led (rt_device_info, ABI 7): the
+        gated launch runs the prepass inside the trace kernel, a prepass launch is the ABI <= 6 sequence."""
+        out = []
+        for key in (0, 1):
+            v = C.c_ulonglong()
+            check(lib().rt_device_info(self._h, key, C.byref(v)), "device info")
+            out.append(int(v.value))
+        return tuple(out)
 
     def graph_info(self):
         """RT_DEVICE_GRAPH: (graphs captured, graph launches) since creation."""
@@ -536,6 +553,15 @@ def render_batch(terrains, shard_rank=0, shard_count=1):
     check(lib().rt_terrain_render_batch(cams, scrs, n, shard_rank, shard_count), "terrain_render_batch")
 
 
+def render_batch_packed(terrains, shard_rank, shard_count, dst_ptr, frame_stride):
+    """rt_terrain_render_batch_packed (ABI 7): the batch's shard (frame f traces shard (rank + f) % count)
+    with its pixels stored straight into the packed device buffer dst_ptr + f * frame_stride (rt_shard_pack's
+    layout) instead of the framebuffers: no pack launch before the gather (RGBA8-only devices)."""
+    n, cams, scrs = _batch_handles(terrains)
+    check(lib().rt_terrain_render_batch_packed(cams, scrs, n, shard_rank, shard_count, dst_ptr, frame_stride),
+          "terrain_render_batch_packed")
+
+
 def _batch_handles(terrains):
     n = len(terrains)
     for t in terrains:
@@ -629,7 +655,7 @@ class FrameRing:
     that call (a camera written after it makes the next batch prepass again, in line)."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 graph=False, batch=1, float_output=False, lookahead=False, **terrain_kw):
+                 graph=False, batch=1, float_output=False, lookahead=False, prepass_inline=False, **terrain_kw):
         self.depth, self.frame, self.batch = int(depth), 0, int(batch)
         if lookahead and graph:
             raise ValueError("lookahead runs the prepass on a side stream: not with graph=True")
@@ -647,7 +673,7 @@ class FrameRing:
         self.slots = []
         for _ in range(self.depth * self.batch):
             dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph,
-                                          float_output=float_output)
+                                          float_output=float_output, prepass_inline=prepass_inline)
             if dev is None:
                 raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
             ter = Terrain(dev, theme, **terrain_kw)

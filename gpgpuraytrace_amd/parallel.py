@@ -23,6 +23,11 @@ tests/test_dist.py with host ops (numpy, gloo), so the CPU tests exercise the sa
   2. trace: each rank traces its shard of every frame (setTargetDepths + tracescreen).
   3. pack: frame f's shard (r + f) % N goes to packed[f * max_bytes : ...] (k_shard_copy;
      1024 RGBA8 pixels per tile, tiles in ascending order), the batch's frames in one launch.
+     With direct_pack (bench.py's default, the unsplit in-line path) there is no pack step: ranks
+     r > 0 render their shards straight into that buffer (rt_terrain_render_batch_packed: the trace
+     kernels store each pixel at its packed offset), and rank 0, whose own shards are never sent,
+     renders into its framebuffers.  The pack launch used to queue behind the other batch's
+     persistent trace kernel before the gather could start.
   4. ONE gather of the packed buffers to rank 0, which unpacks rank src's frame f as shard
      (src + f) % N from gathered[src][f * max_bytes : ...], all (N-1) x B in one launch.
 
@@ -99,13 +104,15 @@ class BatchPlan:
 
     CAMERA_FLOATS = 1024 * 4  # CameraResults of one frame: float4[1024]
 
-    def __init__(self, width, height, batch, world, split_prepass=False, lookahead=False):
+    def __init__(self, width, height, batch, world, split_prepass=False, lookahead=False, direct_pack=False):
         if not 1 <= batch <= 24:
             raise ValueError("batch must be 1..24 frames (RT_MAX_BATCH)")
         self.width, self.height, self.batch, self.world = int(width), int(height), int(batch), int(world)
         self.split_prepass = bool(split_prepass) and self.world > 1
         # the ahead prepass is the unsplit one's (the split one is gathered before its trace)
         self.lookahead = bool(lookahead) and not self.split_prepass
+        # shards rendered straight into the packed buffer (the in-line render path only)
+        self.direct_pack = bool(direct_pack) and self.world > 1 and not self.split_prepass and not self.lookahead
         self.chunk = -(-self.batch // self.world)
         self.max_bytes = max(shard_bytes(self.width, self.height, r, self.world) for r in range(self.world))
 
@@ -149,7 +156,9 @@ def run_batch(plan, rank, ops, frames=None, mark=None, ahead_next=True):
     the side stream, unless the previous batch queued it), prepass_ahead_next() (the next
     batch's, before this trace; skipped with ahead_next=False: the last batch of a run) and
     trace_ahead(), pack_batch([(f, shard, offset)]) (this rank's frames; one
-    rt_shard_pack_batch launch on the GPU), gather(), unpack_batch([(src, f, shard, offset)])
+    rt_shard_pack_batch launch on the GPU), with plan.direct_pack render_packed([(f, shard, offset)])
+    in place of render() + pack_batch() on ranks > 0 (rank 0 renders and packs nothing: its own
+    shards are never sent), gather(), unpack_batch([(src, f, shard, offset)])
     (rank 0: every other rank's frames in one rt_shard_unpack_batch launch), present().
     `frames` < plan.batch renders a partial batch (its first frames).
     mark(name), if given, is called at the start ("start") and after each phase ("prepass",
@@ -171,12 +180,15 @@ def run_batch(plan, rank, ops, frames=None, mark=None, ahead_next=True):
         if ahead_next:
             ops.prepass_ahead_next()
         ops.trace_ahead()
+    elif plan.direct_pack and rank > 0:
+        ops.render_packed(plan.packs(rank, n))
     else:
         ops.render()
     mark("trace")
     if plan.world > 1:
-        ops.pack_batch(plan.packs(rank, n))
-        mark("pack")
+        if not plan.direct_pack:
+            ops.pack_batch(plan.packs(rank, n))
+            mark("pack")
         ops.gather()
         mark("gather")
         if rank == 0:

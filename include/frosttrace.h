@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 enum {
     RT_OK = 0,
@@ -47,7 +47,9 @@ enum {
     RT_DEVICE_GRAPH = 4u,
     /* 8u, 16u: retired in ABI 6 (ABI <= 5 RT_DEVICE_SEG_TAIL_OFF / _ON, no effect since ABI 4);
      * rt_device_create rejects them, as every unknown flag */
-    RT_DEVICE_DEBUG_SMALL_RINGS = 32u
+    RT_DEVICE_DEBUG_SMALL_RINGS = 32u,
+    RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64u,
+    RT_DEVICE_PREPASS_INLINE = 128u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
@@ -56,7 +58,17 @@ enum {
  * RT_DEVICE_DEBUG_SMALL_RINGS (ABI 4, diagnostic): the trace kernel's per-CU LDS long-ray ring holds
  * 64 entries instead of 570 and its fin pool 8 slots instead of 1536, so queued long rays take the
  * per-block spill rings in HBM and most long shadows the fin[t] fallback (the parity tests run
- * frames through those paths); same bits, slower. */
+ * frames through those paths); same bits, slower.
+ * RT_DEVICE_PREPASS_INLINE (ABI 7): renders this device leads run the camerarays prepass as its own launch,
+ * followed by setTargetDepths (k_order) and the trace -- the sequence of ABI <= 6.  By default (ABI 7) a
+ * full nomadplains render (rt_terrain_render / _batch, not the camera feed, not the instrumented
+ * RT_DEVICE_STATS kernels) is ONE gated launch: the trace kernel runs the batch's prepass rays first and
+ * starts each 8x8 unit as soon as the prepass rays its cells' setTargetDepths reads are in, so units no
+ * longer wait for the slowest prepass ray; the frame's last prepass task writes its CellDistance.  Same
+ * bits either way (frames, CameraResults, CellDistance).
+ * RT_DEVICE_DEBUG_WITHHOLD_FUSE (ABI 7, diagnostic): a trace this device leads that would run the next
+ * batch's fused prepass (rt_terrain_trace_ahead) runs none of its tasks, so that batch's bounded wait
+ * times out: the fail-safe's test (rt_device_check below). */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };
@@ -130,6 +142,11 @@ int rt_device_set_profiling(rt_device dev, int enable);
 int rt_device_kernel_time(rt_device dev, double* total_ms, int* launches);
 /* RT_DEVICE_GRAPH bookkeeping: graphs captured and graph launches since device creation. */
 int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned long long* launches);
+/* (ABI 7) Counters of the renders a device led: RT_INFO_GATED_LAUNCHES = renders whose prepass ran inside
+ * their trace kernel (the gated launch), RT_INFO_PREPASS_LAUNCHES = renders with a prepass launch of
+ * their own.  No reference counterpart (the tests check which sequence ran). */
+enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1 };
+int rt_device_info(rt_device dev, int key, unsigned long long* out);
 /* (ABI 6) Stream handoff without a host synchronisation.  `hip_event` is a hipEvent_t the caller
  * owns (a C++ host's, or torch.cuda.Event.cuda_event).  rt_device_wait_event: the work the device
  * queues from now on waits for the event -- e.g. buffers the caller filled on its own stream, then
@@ -145,7 +162,14 @@ int rt_device_record_event(rt_device dev, void* hip_event);
  * bounded by its work priorities (rt_spill_caps); a push that would exceed a bound is not stored and
  * raises a sticky flag on the device instead of overwriting queued work.  rt_device_check
  * synchronises the device stream and returns RT_ERR_STATE (the message names the queue) if any
- * flag was raised since the last check, clearing it; RT_OK otherwise. */
+ * flag was raised since the last check, clearing it; RT_OK otherwise.
+ * (ABI 7) Fail-safe of the fused prepass (rt_terrain_trace_ahead): when a batch's bounded wait for
+ * its prepass rays times out (0.5 s; never expected), its frames may be wrong.  The kernel then also
+ * sets a host-mapped word of its GPU, and from then on every call that launches on, synchronises or
+ * reads a device of that GPU (rt_terrain_*, rt_compute_run, rt_device_present / synchronize /
+ * readback*, rt_array_map, rt_shard_*) returns RT_ERR_STATE, until rt_device_check on a device of
+ * that GPU reports and clears it.  A host that follows the reference's call sequence and never calls
+ * rt_device_check therefore cannot read such a frame silently. */
 int rt_device_check(rt_device dev);
 
 /* ---- ITexture (IDevice::createTexture + ITexture::create(dims, fmt, w, h, data, binding, cpu)) ---- */
@@ -223,6 +247,14 @@ int rt_terrain_feed_wait(rt_compute camera_cs, float* camera_results);
  * shard index. */
 int rt_terrain_render_batch(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
                             int shard_count);
+/* (ABI 7) rt_terrain_render_batch of a shard (shard_count >= 2) whose pixels go straight to a packed
+ * device buffer instead of the framebuffers: frame i's shard at dst_device + i * frame_stride, in
+ * rt_shard_pack's layout (its k-th tile at k * 4 KiB, rows of 32 pixels).  The trace kernels store there
+ * directly, so a rank's batch needs no rt_shard_pack_batch launch before its gather (the pack queued
+ * behind the other batch in flight; parallel.run_batch's direct pack).  RGBA8-only devices
+ * (RT_ERR_UNSUPPORTED with RT_DEVICE_FLOAT_OUTPUT); the framebuffers are not written. */
+int rt_terrain_render_batch_packed(const rt_compute* camera_cs, const rt_compute* screen_cs, int n, int shard_rank,
+                                   int shard_count, void* dst_device, size_t frame_stride);
 /* The same batch in two phases, for a prepass split across ranks (one process per GPU):
  * rt_terrain_prepass_batch runs the camerarays prepass of frames [first, first + count) only
  * and writes frame f's 1024 CameraResults to camera_out + f * 1024 float4 (a device buffer of

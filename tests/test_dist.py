@@ -129,6 +129,18 @@ class HostOps:
         for f in range(self.n):
             self._render(f, synthetic_cameras(f))
 
+    def render_packed(self, items):
+        """plan.direct_pack: this rank's shards straight into the packed buffer (the framebuffers stay
+        untouched, as on the GPU)."""
+        import torch
+
+        from gpgpuraytrace_amd import parallel as P
+        self.log.append(("render_packed", len(items)))
+        for f, shard, off in items:
+            pk = P.pack_host(synthetic_batch_frame(self.w, self.h, f, synthetic_cameras(f)), shard,
+                             self.p.world).view(np.int32)
+            self.packed[off // 4:off // 4 + pk.size] = torch.from_numpy(pk.copy())
+
     def prepass_ahead(self):
         self.log.append(("prepass_ahead",))
 
@@ -178,7 +190,8 @@ def _batch_worker(rank, world, port, w, h, batch, frames, split, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead")
+        plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead",
+                           direct_pack=split == "direct")
         coll = P.Collectives(dist, "gloo", rank, world)
         group = dist.new_group(backend="gloo") if plan.split_prepass else None
         ops = HostOps(plan, rank, coll, w, h, frames, group)
@@ -208,6 +221,8 @@ def _batch_worker(rank, world, port, w, h, batch, frames, split, q):
     (3, 50, 36, 12, 7, False),       # unsplit prepass, partial batch
     (2, 1920, 1080, 12, 12, "ahead"),  # bench default: unsplit, the next batch's prepass queued ahead
     (3, 50, 36, 12, 7, "ahead"),     # the same, partial batch
+    (2, 1920, 1080, 12, 12, "direct"),  # bench default (ABI 7): shards rendered straight into the packed buffer
+    (3, 50, 36, 12, 7, "direct"),    # the same, ragged shards, partial batch
 ])
 def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
     """bench.py's N>1 batch sequence, driven through parallel.run_batch with host ops: split
@@ -227,19 +242,22 @@ def test_gloo_batch_plan_assembles_frames(world, w, h, batch, frames, split):
     ok, log, per_rank, skew = q.get(timeout=10)
     assert ok
     from gpgpuraytrace_amd import parallel as P
-    plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead")
+    plan = P.BatchPlan(w, h, batch, world, split_prepass=split is True, lookahead=split == "ahead",
+                       direct_pack=split == "direct")
     if plan.split_prepass:
         assert log[0] == ("prepass", 0, min(plan.chunk, frames)) and ("trace",) in log
     elif plan.lookahead:
         # this batch's prepass, then the next one's, both queued before this trace
         assert log[:3] == [("prepass_ahead",), ("prepass_ahead_next",), ("trace_ahead",)]
     else:
-        assert log[0] == ("render",)
-    # rank 0: one pack of its frames, one unpack of every other rank's (one launch each on the GPU)
-    assert ("pack_batch", frames) in log and ("unpack_batch", (world - 1) * frames) in log
+        assert log[0] == ("render",)  # (rank 0 renders into its framebuffers also with direct_pack)
+    # rank 0: one pack of its frames (none with direct_pack: its own shards are never sent), one unpack of
+    # every other rank's (one launch each on the GPU)
+    assert (("pack_batch", frames) in log) != plan.direct_pack and ("unpack_batch", (world - 1) * frames) in log
     # bench.py's config.per_rank / trace_start_skew_ms (make the first 8-GPU run diagnosable)
     assert [r["rank"] for r in per_rank] == list(range(world))
-    want = (["prepass", "all_gather"] if plan.split_prepass else []) + ["trace", "pack", "gather"]
+    want = (["prepass", "all_gather"] if plan.split_prepass else []) + ["trace"] + \
+        ([] if plan.direct_pack else ["pack"]) + ["gather"]
     for r in per_rank:
         keys = want + (["unpack"] if r["rank"] == 0 else [])
         assert sorted(r["phase_ms"]) == sorted(keys) and sorted(r["phase_ms_max"]) == sorted(keys)

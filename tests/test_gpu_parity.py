@@ -543,6 +543,45 @@ def test_shard_batch_pack_unpack_roundtrip(w, h, world, frames):
         d.destroy()
 
 
+@pytest.mark.parametrize("w,h,world,frames,pose,ao,land", [
+    (1920, 1080, 8, 3, "reset", 1, "nomadplains"),    # the bench's C3 shard: fit + k_finish, gated launch
+    (64, 48, 3, 4, "lookdown", 4, "nomadplains"),     # fitm (AO slots + colour pool), ragged shards
+    (64, 48, 2, 2, "reset", 0, "nomadplains"),        # fit with no k_finish
+    (48, 32, 3, 3, "reset", 2, "greenrocks"),         # fog live, the separate prepass launch
+])
+def test_render_batch_packed_equals_render_then_pack(w, h, world, frames, pose, ao, land):
+    """rt_terrain_render_batch_packed (ABI 7, parallel.run_batch's direct pack): every rank's shards
+    rendered straight into the packed buffer are byte-identical to render_batch + rt_shard_pack_batch of
+    the same rank (padding of partial tiles untouched), and the framebuffers are not written."""
+    import torch
+
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    consts = _consts_1080p_like(w, h, pose) if w >= 1280 else GI.consts(w, h, pose)
+    plan = P.BatchPlan(w, h, frames, world)
+    ms = 512 if w >= 1280 else 0
+    direct = [make(consts, land, max_steps=ms, ao=ao, float_output=False) for _ in range(frames)]
+    ref = [make(consts, land, max_steps=ms, ao=ao, float_output=False) for _ in range(frames)]
+    for rank in range(world):
+        a = torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0")
+        b = torch.zeros_like(a)
+        torch.cuda.synchronize()
+        E.render_batch_packed([t for _, t in direct], rank, world, a.data_ptr(), plan.max_bytes)
+        E.render_batch([t for _, t in ref], rank, world)
+        items = plan.packs(rank)
+        E.shard_pack_batch([ref[f][0] for f, _, _ in items], [s for _, s, _ in items], world,
+                           [b.data_ptr() + off for _, _, off in items])
+        for d, _ in direct + ref:
+            d.synchronize()
+        assert torch.equal(a, b), rank
+        for d, _ in direct:  # never written: still the cleared framebuffer
+            assert not d.readback().any()
+        for d, _ in direct + ref:
+            d.check()
+    for d, _ in direct + ref:
+        d.destroy()
+
+
 @pytest.mark.parametrize("land", ["nomadplains", "greenrocks"])
 def test_recording_macro_bitexact(land):
     consts = GI.consts(48, 32, "reset")
@@ -1306,7 +1345,7 @@ def test_device_flags_retired_and_check():
     rejected; rt_device_check is RT_OK after frames through the spill rings (no dropped push)."""
     import gpgpuraytrace_amd as G
     h = C.c_void_p()
-    for bad in (8, 16, 64, 1 << 20):
+    for bad in (8, 16, 256, 1 << 20):
         assert G.lib().rt_device_create(0, 64, 48, bad, C.byref(h)) == -1  # RT_ERR_INVALID
     dev, ter = make(GI.consts(64, 48, "lookdown"), small_rings=True, ao=4)
     for _ in range(3):
@@ -1418,6 +1457,202 @@ def test_fused_prepass_frame_ring_bitexact():
     for dev, _ in ring.slots:
         dev.check()
     ring.destroy()
+
+
+# --- the gated launch (ABI 7): the prepass inside the trace kernel, units gated on their cells' rays ----------
+GATED_SPECS = [GI.FRAMES[0], GI.FRAMES[1], GI.FRAMES[2], GI.FRAMES[3], GI.FRAMES[8], GI.FRAMES[9]]
+
+
+@pytest.mark.parametrize("float_output", [True, False], ids=["f32", "rgba8"])
+@pytest.mark.parametrize("spec", GATED_SPECS, ids=[GI.frame_key(*s) for s in GATED_SPECS])
+def test_gated_launch_golden(spec, float_output):
+    """The default render of a nomadplains frame is ONE gated launch (rt_device_info): k_trace runs the
+    1024 prepass rays as 8-ray tasks, each unit starts once its cells' 5x5 prepass rays have flagged and
+    derives its cells' setTargetDepths bracket from them, the frame's last task writes CellDistance.
+    The unit order comes from the PREVIOUS CellDistance, poisoned here with NaN / inf / garbage: frames,
+    CameraResults and CellDistance still equal the golden ones; a second frame (a real previous order)
+    too; and the RT_DEVICE_PREPASS_INLINE device (ABI <= 6 sequence) gives the same bits."""
+    import gpgpuraytrace_amd as G
+    gold = GI.load()
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    key = GI.frame_key(*spec)
+    consts = GI.consts(w, h, pose)
+    dev, ter = make(consts, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output)
+    rng = np.random.default_rng(7)
+    junk = rng.uniform(-1e3, 1e3, (1024, 2)).astype(np.float32)
+    junk[::7] = np.nan
+    junk[3::11, 1] = np.inf
+    junk[5::13, 0] = 0.0
+    ter.var_cell_distance.write(junk)
+    for rep in range(2):
+        ter.render_device()
+        assert dev.launch_info() == (rep + 1, 0)
+        assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), rep
+        if float_output:
+            assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"]), rep
+        assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"]), rep
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, gold[key + "_camera_results"]), rep
+    dev.check()
+    dev.destroy()
+    idev = G.DeviceFactory.construct(G.DeviceAPI.HIP, w, h, float_output=float_output, prepass_inline=True)
+    iter_ = G.Terrain(idev, land, aa_samples=aa, max_steps=ms, ao_samples=ao)
+    iter_.create()
+    assert iter_.reload()
+    iter_.set_camera(FixedCamera(consts))
+    iter_.set_time_of_day_vec(consts["sun"])
+    iter_.render_device()
+    assert idev.launch_info() == (0, 1)
+    assert np.array_equal(idev.readback(), gold[key + "_rgba8"])
+    idev.destroy()
+
+
+def test_gated_launch_c3_batch_rows():
+    """The gated launch at full size: a batch of 3 C3 frames (1920x1080, 512-step cap, AO 1; both poses
+    and the reset pose moved), the units of 3 x 2040 tiles deferred while 384 prepass tasks march, against
+    the oracle on row samples; then as an 8-way rotated shard of one rank (most of the batch's units wait
+    for rays of cells it does not trace)."""
+    from gpgpuraytrace_amd import engine as E
+    W, H = 1920, 1080
+    cams = [_consts_1080p_like(W, H, "reset"), _consts_1080p_like(W, H, "lookdown")]
+    cams.append(_moved_consts(cams[0], (60.0, -20.0, 35.0)))
+    rows = (0, H, 67)
+    nz = O.noise_tables()
+    refs = []
+    for c in cams:
+        rgba, rgba8, cr, cd, _ = O.render_rows(nz, O.make_frame(c, max_steps=512, ao=1, rows=rows, threads=0))
+        refs.append((rgba8, cr, cd))
+    pairs = [make(c, max_steps=512, ao=1, float_output=False) for c in cams]
+    E.render_batch([t for _, t in pairs])
+    for (dev, ter), (rgba8, cr, cd) in zip(pairs, refs):
+        img = dev.readback()
+        assert np.array_equal(img[0:H:67], rgba8[0:H:67])
+        assert np.array_equal(_device_cells(ter), cd)
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, cr)
+    assert pairs[0][0].launch_info() == (1, 0)
+    for dev, _ in pairs:
+        dev.check()
+    # one rank of an 8-way shard: its tiles of every frame against the whole-frame rows
+    E.render_batch([t for _, t in pairs], 3, 8)
+    tiles_x = (W + 31) // 32
+    for f, ((dev, _), (rgba8, _, _)) in enumerate(zip(pairs, refs)):
+        img = dev.readback()
+        shard = (3 + f) % 8
+        for y in range(0, H, 67):
+            for tx in range(tiles_x):
+                if ((y // 32) * tiles_x + tx) % 8 == shard:
+                    x0, x1 = tx * 32, min(W, tx * 32 + 32)
+                    assert np.array_equal(img[y, x0:x1], rgba8[y, x0:x1]), (f, y, tx)
+    for dev, _ in pairs:
+        dev.check()
+        dev.destroy()
+
+
+def _moved_consts(consts, d):
+    """The fixture's camera moved by d (eye and ViewInverse's translation row): a third pose whose
+    oracle frame the test renders itself."""
+    c = dict(consts)
+    c["eye"] = np.asarray(consts["eye"], np.float32).copy()
+    c["eye"][:3] += np.asarray(d, np.float32)
+    vi = np.asarray(consts["view_inverse"], np.float32).copy().reshape(4, 4)
+    vi[3, :3] += np.asarray(d, np.float32)
+    c["view_inverse"] = vi
+    return c
+
+
+def test_fused_prepass_cameras_change_every_batch():
+    """a batch must never trace from its group's PREVIOUS fused CameraResults.  Three cameras
+    cycle over two slot groups (group g renders cameras g, g + 2, g + 4, ... mod 3), so every group's
+    camera changes from one fused batch to its next; every frame, its CameraResults and CellDistance
+    equal the oracle's for that batch's own camera.  (With a fixed camera per group, a k_order that
+    passed on the previous round's count would still have matched.)"""
+    import gpgpuraytrace_amd as G
+    gold = GI.load()
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]
+    base = [GI.consts(*GI.unpack(s)[2:4], GI.unpack(s)[1]) for s in specs]
+    consts = base + [_moved_consts(base[0], (40.0, -30.0, 25.0))]
+    refs = [{"rgba8": gold[GI.frame_key(*specs[0]) + "_rgba8"],
+             "camera_results": gold[GI.frame_key(*specs[0]) + "_camera_results"],
+             "cell_distance": gold[GI.frame_key(*specs[0]) + "_cell_distance"]},
+            {"rgba8": gold[GI.frame_key(*specs[1]) + "_rgba8"],
+             "camera_results": gold[GI.frame_key(*specs[1]) + "_camera_results"],
+             "cell_distance": gold[GI.frame_key(*specs[1]) + "_cell_distance"]}]
+    refs.append(O.render(O.noise_tables(), O.make_frame(consts[2])))
+    assert not np.array_equal(refs[2]["camera_results"], refs[0]["camera_results"])
+    cams = [FixedCamera(c) for c in consts]
+    w, h = cams[0].width, cams[0].height
+    ring = G.FrameRing(w, h, depth=2, batch=2, camera=cams[0], lookahead=True)
+    for _, ter in ring.slots:
+        ter.set_time_of_day_vec(cams[0].c["sun"])
+
+    def set_group(g, c):
+        for _, ter in ring.slots[g * 2:(g + 1) * 2]:
+            ter.set_camera(cams[c])
+            ter.update_terrain()
+
+    def check_group(g, c, b, arrays):
+        for dev, ter in ring.slots[g * 2:(g + 1) * 2]:
+            assert np.array_equal(dev.readback(), refs[c]["rgba8"]), (b, g, c)
+            assert np.array_equal(_device_cells(ter), refs[c]["cell_distance"]), (b, g, c)
+            if arrays:  # (mid-run, the group's NEXT prepass is already fused into the running trace)
+                ter.get_camera_results()
+                assert np.array_equal(ter.camera_view, refs[c]["camera_results"]), (b, g, c)
+
+    n = 9
+    set_group(0, 0)
+    for b in range(n):
+        if b + 1 < n:
+            set_group((b + 1) % 2, (b + 1) % 3)  # the next batch's camera, before its prepass is staged
+        ring.render_batch(ahead=b + 1 < n)
+        if b >= 1:  # the previous batch (the other group), while this one runs
+            check_group((b - 1) % 2, (b - 1) % 3, b - 1, False)
+    ring.synchronize()
+    check_group((n - 1) % 2, (n - 1) % 3, n - 1, True)
+    check_group((n - 2) % 2, (n - 2) % 3, n - 2, True)
+    for dev, _ in ring.slots:
+        dev.check()
+    ring.destroy()
+
+
+def test_fused_prepass_timeout_fails_safe():
+    """a batch whose fused prepass never runs (RT_DEVICE_DEBUG_WITHHOLD_FUSE on the
+    fusing device) times out in k_order; from then on every call that launches on or reads a device of
+    the GPU fails with RT_ERR_STATE (a reference-shaped host that never calls rt_device_check cannot
+    read the frame), rt_device_check reports and clears it, and the next frames are bit-exact again."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import engine as E
+    gold = GI.load()
+    spec = GI.FRAMES[0]
+    consts = GI.consts(*GI.unpack(spec)[2:4], GI.unpack(spec)[1])
+    key = GI.frame_key(*spec)
+    pairs = [make(consts, float_output=False)]
+    a_dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], debug_withhold_fuse=True)
+    assert a_dev is not None
+    a_ter = G.Terrain(a_dev, "nomadplains")
+    a_ter.create()
+    assert a_ter.reload()
+    a_ter.set_camera(FixedCamera(consts))
+    a_ter.set_time_of_day_vec(consts["sun"])
+    a_ter.update_shaders()
+    b_dev, b_ter = pairs[0]
+    E.prepass_ahead([a_ter])   # staged; traced before any other trace: in line
+    E.prepass_ahead([b_ter])   # staged, then "fused" into a's trace, which withholds its tasks
+    E.trace_ahead([a_ter])
+    E.trace_ahead([b_ter])     # k_order waits 0.5 s for rays no kernel computes, then flags
+    with pytest.raises(G.NativeError):
+        b_dev.synchronize()
+    with pytest.raises(G.NativeError):
+        b_dev.readback()
+    with pytest.raises(G.NativeError):
+        a_ter.render_device()  # every device of the GPU refuses until the check
+    with pytest.raises(G.NativeError, match="timed out"):
+        b_dev.check()
+    b_dev.check()              # cleared
+    b_ter.render_device()
+    assert np.array_equal(b_dev.readback(), gold[key + "_rgba8"])
+    a_dev.destroy()
+    b_dev.destroy()
 
 
 def test_fused_prepass_camera_change_and_partial_batch():
