@@ -152,3 +152,5 @@ void rt_launch_shard_copy(hipStream_t s, const ShardJobs& jobs, int n, int w, in
 void rt_launch_debug_math(hipStream_t s, int op, const float* a, const float* b, float* y, int n);
 void rt_launch_debug_noise(const RtLaunch& a, const float* xyz, float* out, int n, int density);
 void rt_launch_debug_sky(const RtLaunch& a, const float* dirs, float* out, int n);
+void rt_launch_debug_spin(hipStream_t s, const unsigned long long* base, unsigned long long until_ticks,
+                          unsigned long long ticks, unsigned long long* stamp);

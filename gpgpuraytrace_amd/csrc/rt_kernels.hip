@@ -2239,7 +2239,27 @@ __global__ void __launch_bounds__(256) k_debug_sky(const RtConsts* __restrict__ 
     o[6] = space;
 }
 
+// scripts/batch_shard_sim.py's coupled transport model (diagnostics): one wave that stores the 100 MHz
+// clock when it starts (stamp, if set), waits until base[0] + until_ticks (base set: a stamp of an earlier
+// launch; a peer's side of a transfer becoming ready), then spins `ticks` more (the transfer), holding a CU
+// like a collective's kernel.  Vector stores only.
+__global__ void __launch_bounds__(64) k_debug_spin(const unsigned long long* base, unsigned long long until_ticks,
+                                                  unsigned long long ticks, unsigned long long* stamp)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (stamp && threadIdx.x == 0) *stamp = t0;
+    const unsigned long long ready = base ? base[0] + until_ticks : t0;
+    const unsigned long long end = (ready > t0 ? ready : t0) + ticks;
+    while (__builtin_amdgcn_s_memrealtime() < end) __builtin_amdgcn_s_sleep(16);
+}
+
 } // namespace
+
+void rt_launch_debug_spin(hipStream_t s, const unsigned long long* base, unsigned long long until_ticks,
+                          unsigned long long ticks, unsigned long long* stamp)
+{
+    hipLaunchKernelGGL(k_debug_spin, dim3(1), dim3(64), 0, s, base, until_ticks, ticks, stamp);
+}
 
 void rt_launch_debug_sky(const RtLaunch& a, const float* dirs, float* out, int n)
 {

@@ -931,6 +931,14 @@ int rt_device_kernel_time(rt_device d, double* total_ms, int* launches)
     return RT_OK;
 }
 
+int rt_debug_spin(void* hip_stream, const unsigned long long* base_device, unsigned long long until_ticks,
+                  unsigned long long ticks, unsigned long long* stamp_device)
+{
+    rt_launch_debug_spin((hipStream_t)hip_stream, base_device, until_ticks, ticks, stamp_device);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
 int rt_device_info(rt_device d, int key, unsigned long long* out)
 {
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");

@@ -321,6 +321,12 @@ int rt_debug_noise(rt_compute cs, const float* xyz, float* out, int n, int densi
  *   constants (Eye, SunDirection) and tables: 7 floats per direction, getRayleighMieColor's
  *   (mie.rgb, rayleigh.rgb) (sky.hlsl:83-137) and getSpaceColor (sky.hlsl:26-36). */
 int rt_debug_sky(rt_compute cs, const float* dirs, float* out, int n);
+/* rt_debug_spin (ABI 7, scripts/batch_shard_sim.py's coupled transport model): one 64-thread workgroup
+ *   on `hip_stream` that stores the GPU's 100 MHz clock at its start to *stamp_device (if not NULL), waits
+ *   until *base_device + until_ticks (base_device a stamp an earlier spin stored; NULL: no wait), then
+ *   spins `ticks` more -- the CU a collective's kernel holds while it waits for its peer and transfers. */
+int rt_debug_spin(void* hip_stream, const unsigned long long* base_device, unsigned long long until_ticks,
+                  unsigned long long ticks, unsigned long long* stamp_device);
 
 /* ---- IRecorder (Factories/IRecorder.h; RecorderWinAPI.cpp; RecorderFactory.cpp) ----
  * rt_recorder_create   <- RecorderFactory::construct(device, frameRate, fixedSpeed) + create():

@@ -58,6 +58,17 @@ def main():
                          "rt_shard_pack_batch, a one-block spin kernel of this many us for the RCCL gather (it "
                          "needs a CU like RCCL's kernels do; 200 us ~ rank 0 receiving 7 x 10 frames' shards "
                          "over xGMI), and rank 0's rt_shard_unpack_batch of the other ranks' (N-1) x B shards")
+    ap.add_argument("--transport-model", choices=["local", "coupled"], default="local",
+                    help="with --transport-us: local = every rank's stand-in spins --transport-us on its own; coupled "
+                         "= rank 0's receive stand-in (after its batch's trace, on the batch stream) spins "
+                         "--transport-us and stores when it started, and rank r > 0's send stand-in holds its CU "
+                         "until rank 0's receive of that batch started plus --transport-us (rank 0 runs first; the "
+                         "ranks' timed regions are aligned at their start): a peer's send waits for rank 0's "
+                         "receive, which queues behind rank 0's other-batch trace kernel")
+    ap.add_argument("--direct-pack", type=int, default=1,
+                    help="N > 1: ranks > 0 render their shards straight into the packed buffer "
+                         "(rt_terrain_render_batch_packed, bench.py's default) and nobody packs; 0: render + "
+                         "rt_shard_pack_batch on every rank (round 4)")
     ap.add_argument("--gate", type=int, default=0,
                     help="with --transport-us: each batch's prepass (rt_terrain_prepass_batch) is queued at once, its "
                          "trace (rt_terrain_trace_batch) after an event recorded behind the previous batch's pack, "
@@ -90,36 +101,52 @@ def main():
 
         plan_n = {}
 
-        def transport(r, n):
+        def plan_for(n):
             from gpgpuraytrace_amd import parallel as P
-            if n == 1 or a.transport_us <= 0:
-                return
             if n not in plan_n:
                 plan = P.BatchPlan(W, H, B, n)
                 plan_n[n] = (plan, [torch.zeros(plan.packed_bytes(), dtype=torch.uint8, device="cuda:0")
                                     for _ in range(a.depth)])
                 torch.cuda.synchronize()
-            plan, packed = plan_n[n]
+            return plan_n[n]
+
+        # coupled model: rank 0's receive starts (100 MHz GPU clock, per timed batch) and each pass's t0
+        clock = torch.zeros(64, dtype=torch.int64, device="cuda:0")  # [0] t0 of the pass, [1 + i] rank 0's recv i
+        recv_off = {}  # n -> [rank 0's receive start of timed batch i - its t0] (ticks)
+        xfer_ticks = int(a.transport_us * 100)  # 100 MHz
+
+        def transport(r, n, i):
+            """i: the timed batch's index (-1: warm-up)"""
+            if n == 1 or a.transport_us <= 0:
+                return
+            plan, packed = plan_for(n)
             g = ((ring.frame - B) // B) % ring.depth  # the batch just queued
             grp = ring.slots[g * B:(g + 1) * B]
             devs = [d for d, _ in grp]
             base = packed[g].data_ptr()
-            items = plan.packs(r)
-            G.engine.shard_pack_batch([devs[f] for f, _, _ in items], [s for _, s, _ in items], n,
-                                      [base + off for _, _, off in items])
-            with torch.cuda.stream(torch.cuda.ExternalStream(devs[0].stream(), device="cuda:0")):
+            if not a.direct_pack:
+                items = plan.packs(r)
+                G.engine.shard_pack_batch([devs[f] for f, _, _ in items], [s for _, s, _ in items], n,
+                                          [base + off for _, _, off in items])
+            stream = devs[0].stream()
+            with torch.cuda.stream(torch.cuda.ExternalStream(stream, device="cuda:0")):
                 if a.gate:
                     gate[0] = torch.cuda.Event()
                     gate[0].record()
-                torch.cuda._sleep(int(a.transport_us * 2400))  # clock64 ticks ~2.4 per ns (tests: 50e6 ~ 20 ms)
+                if a.transport_model == "local" or i < 0:
+                    torch.cuda._sleep(int(a.transport_us * 2400))  # clock64 ticks ~2.4 per ns (tests: 50e6 ~ 20 ms)
+                elif r == 0:  # the receive: stamped, then the transfer time
+                    G.lib().rt_debug_spin(stream, None, 0, xfer_ticks, clock.data_ptr() + 8 * (1 + i))
+                else:  # the send: holds its CU until rank 0's receive of this batch started, plus the transfer
+                    G.lib().rt_debug_spin(stream, clock.data_ptr(), recv_off[n][i], xfer_ticks, None)
             if r == 0:
                 ups = plan.unpacks()
                 G.engine.shard_unpack_batch([devs[f] for _, f, _, _ in ups], [s for _, _, s, _ in ups], n,
                                             [base + off for _, _, _, off in ups])
 
-        def step(r, n, ahead=True):
+        def step(r, n, ahead=True, i=-1):
             step_(r, n, ahead)
-            transport(r, n)
+            transport(r, n, i)
 
         gate = [None]
 
@@ -139,6 +166,13 @@ def main():
                 G.engine.trace_batch([t for _, t in ring.slots[g * B:(g + 1) * B]], r, n, bufs[g].data_ptr())
                 ring.frame += B
                 return
+            if a.direct_pack and n > 1 and r > 0 and not a.split_prepass and not ring.lookahead:
+                plan, packed = plan_for(n)
+                g = (ring.frame // B) % ring.depth
+                G.engine.render_batch_packed([t for _, t in ring.slots[g * B:(g + 1) * B]], r, n,
+                                             packed[g].data_ptr(), plan.max_bytes)
+                ring.frame += B
+                return
             if not a.split_prepass or n == 1:
                 ring.render_batch(r, n, present=False, ahead=ahead)
                 return
@@ -155,17 +189,23 @@ def main():
                     step(r, n, ahead=i + 1 < 2 * a.depth)
                 torch.cuda.synchronize()
                 nb = max(1, a.frames // B)
+                G.lib().rt_debug_spin(None, None, 0, 0, clock.data_ptr())  # the pass's t0 (GPU clock)
                 t0 = time.perf_counter()
                 for i in range(nb):
-                    step(r, n, ahead=i + 1 < nb)
+                    step(r, n, ahead=i + 1 < nb, i=i)
                 torch.cuda.synchronize()
                 ms = (time.perf_counter() - t0) / (nb * B) * 1e3
+                if r == 0 and n > 1 and a.transport_model == "coupled" and a.transport_us > 0:
+                    c = clock.cpu().tolist()
+                    recv_off[n] = [max(0, c[1 + i] - c[0]) for i in range(nb)]
                 per.append(round(ms, 4))
                 worst = max(worst, ms)
             if base is None:
                 base = worst
             print(json.dumps({"batch": B, "depth": a.depth, "split_prepass": a.split_prepass, "no_prepass": a.no_prepass,
-                              "transport_us": a.transport_us, "gate": a.gate,
+                              "transport_us": a.transport_us, "transport_model": a.transport_model,
+                              "direct_pack": a.direct_pack, "gate": a.gate,
+                              **({"rank0_recv_start_ms": [round(x / 1e5, 4) for x in recv_off[n]]} if n in recv_off else {}),
                               "lookahead": int(ring.lookahead), "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()
