@@ -3,7 +3,7 @@
 #   gpurun -- bash scripts/gpu_run.sh <name> <step> [<step> ...]
 # Output goes to gpurun_out/<name>/; the call stops at the first failing step (each step has its own
 # time limit; a GPU step that fails, faults or times out ends the call).
-#   tests[=<pytest -k expr>]     python -m pytest tests -m gpu (optionally -k)
+#   tests[=<pytest -k expr>]     python -m pytest tests -m gpu -x (optionally -k); testsall: without -x
 #   bench[=<bench.py args>]      one bench.py line -> bench<i>.json (default args: the driver's default)
 #   r4bench[=<args>]             the same command on the round-4 snapshot in _ab/r4 (same-box A/B)
 #   ab=<args>                    bench.py --no-cpu-baseline --traffic off --no-companions <args>: one line
@@ -11,6 +11,7 @@
 #   sim=<batch_shard_sim args>   scripts/batch_shard_sim.py
 #   prof=<bench.py args>         rocprofv3 --kernel-trace --stats over bench.py -> prof<i>/
 #   py=<script and args>         any python script of the repo (diagnostics)
+#   vpy=<variant>:<script args>  the same against an A/B build _build/librt_hip_<variant>.so
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 name=$1; shift
@@ -31,9 +32,10 @@ for step in "$@"; do
   i=$((i+1)); kind=${step%%=*}; arg=""; [ "$kind" != "$step" ] && arg=${step#*=}
   echo "[$i] $step"
   case $kind in
-    tests)
+    tests|testsall)  # testsall: no -x (every failure of the suite in one call)
       k=(); [ -n "$arg" ] && k=(-k "$arg")
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${k[@]}" \
+      x=-x; [ $kind = testsall ] && x=
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu $x -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$out/tests$i.log" 2>&1 || { tail -40 "$out/tests$i.log"; exit 1; }
       tail -1 "$out/tests$i.log";;
     bench|r4bench|ab|r4ab)
@@ -52,6 +54,11 @@ for step in "$@"; do
       tail -1 "$out/prof$i.log";;
     py)
       timeout -k 10 600 python3 $arg > "$out/py$i.log" 2>&1 || { tail -20 "$out/py$i.log"; exit 1; }
+      tail -5 "$out/py$i.log";;
+    vpy)  # vpy=<variant>:<script and args>: the script against _build/librt_hip_<variant>.so (with_variant.py)
+      v=${arg%%:*}; rest=${arg#*:}
+      RT_LIB_VARIANT=$v timeout -k 10 600 python3 scripts/with_variant.py $rest > "$out/py$i.log" 2>&1 \
+        || { tail -20 "$out/py$i.log"; exit 1; }
       tail -5 "$out/py$i.log";;
     *) echo "unknown step $step"; exit 2;;
   esac
