@@ -978,6 +978,7 @@ struct TraceQueues {
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
     uint32_t d_head, d_tail;   // the gated launch: the block's deferred units, defer[d_head, d_tail) in HBM
+    uint32_t gq_done;          // the global unit queue is exhausted (drained: and no unit is deferred either)
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
     uint32_t ao_ctr[kAoSlots / 2]; // AO slot s: bits 16 (s & 1) + 0..4 rays finished, + 5..9 occluded
@@ -1061,6 +1062,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.f_top = fin_slots;
         q.overflow = 0;
         q.d_head = q.d_tail = 0;
+        q.gq_done = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
@@ -1822,13 +1824,22 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 else if (!defer_push(qi)) run = wait = true;
             };
             if (deferred && defer_pop(&qi)) try_unit(); // the oldest deferred unit first, if its rays are in
-            if (!run && (!drained || first_unit)) {
+            // `drained` (the tail behaviours: small shading and long-ray batches, segments) only once no unit
+            // is left anywhere: the global queue is exhausted AND nothing waits in the deferred list
+            auto nothing_deferred = [&]() { return gp.tasks == 0u || vload(q.d_tail) == vload(q.d_head); };
+            if (!run && (vload(q.gq_done) == 0u || first_unit)) {
                 qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
                 first_unit = false;
-                if (qi < n_total) try_unit();
-                else if (lane == 0) q.drained = 1u;
+                if (qi < n_total) {
+                    try_unit();
+                } else if (lane == 0) {
+                    q.gq_done = 1u;
+                    if (nothing_deferred()) q.drained = 1u;
+                }
             } else if (!run) {
-                __builtin_amdgcn_s_sleep(4); // drained: only deferred units whose rays are still marching
+                // the queue is exhausted: only deferred units, whose rays are still marching
+                if (lane == 0 && nothing_deferred()) q.drained = 1u;
+                __builtin_amdgcn_s_sleep(32);
             }
             if (run) {
                 if (wait)
