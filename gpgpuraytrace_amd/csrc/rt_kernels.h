@@ -9,7 +9,8 @@
 // first-unit counter per wave slot of a k_trace block), then the device's sticky flags (zeroed at
 // device creation and by rt_device_check only): a k_trace queue push that would exceed its bound
 // raises a flag instead of storing (rt_spill_caps)
-enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1, RT_CTR_GATE = 24 }; // RT_CTR_GATE: the in-launch prepass's task counter
+// RT_CTR_GATE / RT_CTR_SCAN: the gated launch's prepass task counter and its tile scan's start (GatedPrepass)
+enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1, RT_CTR_GATE = 24, RT_CTR_SCAN = 25 };
 #define RT_CTR_BYTES 128
 #define RT_QUEUE_BYTES 192
 enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_TIMEOUT = 4u };
@@ -44,18 +45,18 @@ struct FusedPrepass {
 // The batch's OWN camerarays prepass inside its k_trace (the gated launch, nomadplains; DESIGN.md
 // section 7): `tasks` = frames x RT_FUSE_TASKS_PER_FRAME tasks of 8 rays, taken first by the waves
 // (top priority), each storing its 8 CameraResults as one whole 128-B line (sc1) and then, per frame
-// (RT_GATE_WORDS words at gate + f * RT_GATE_WORDS, zeroed by k_order), its task flag (sc1 store) and
-// the frame's ray counter (agent add; the task that completes the frame derives its CellDistance).  A
-// primary unit starts only once the tasks of every CameraResults ray its cells' setTargetDepths reads
-// (the 5x5 neighbourhood) have flagged, so units start while the prepass's long rays still march
-// instead of after the whole prepass.  Not-yet-ready units wait in their block's deferred list
-// (defer_cap entries per block in HBM).  tasks == 0: off (the prepass ran before; cells from k_order).
-#define RT_GATE_WORDS 160 // per frame: 128 task flags, the ray counter on its own 128-B line
-#define RT_GATE_CTR 128
-#define RT_DEFER_CAP 1024 // deferred units per k_trace block
+// (RT_GATE_WORDS words at gate + f * RT_GATE_WORDS, zeroed by k_order), setting its bit in the frame's
+// task mask (words 0-3; task = ray row * 4 + ray column / 8) and adding 8 to the frame's ray counter
+// (word RT_GATE_CTR; the task that completes the frame derives the frame's CellDistance and flags it in
+// word RT_GATE_CTR + 1).  Units are claimed by tile (claims[i]: units of order entry i taken) in k_order's
+// longest-first order from the tiles whose cells' prepass rays (the 5x5 neighbourhoods setTargetDepths
+// reads) are in, so units start while the prepass's long rays still march.  tasks == 0: off (the prepass
+// ran before; cells from k_order).
+#define RT_GATE_WORDS 64 // per frame: the task mask (words 0-3), the ray counter and the cells flag on a line of their own
+#define RT_GATE_CTR 32
 struct GatedPrepass {
-    uint32_t* gate;  // RT_MAX_BATCH x RT_GATE_WORDS
-    uint32_t* defer; // num_cus x RT_DEFER_CAP unit indices
+    uint32_t* gate;   // RT_MAX_BATCH x RT_GATE_WORDS
+    uint32_t* claims; // per order entry (tile of the batch): its units claimed so far
     uint32_t tasks;
 };
 

@@ -419,7 +419,7 @@ constexpr uint32_t kOrderBatchUnitsPerWave = 4u;
 __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ ft, UnitMap m,
                                                 uint32_t* __restrict__ order, uint32_t* __restrict__ counters,
                                                 const uint32_t* wait_ctl, uint32_t wait_total, uint32_t* zero_ctl,
-                                                uint32_t* host_flag, uint32_t* gate)
+                                                uint32_t* host_flag, uint32_t* gate, uint32_t* claims)
 {
     __shared__ float s_key[RT_CAMERA_RES * RT_CAMERA_RES];
     __shared__ uint32_t s_hist[64];
@@ -428,9 +428,11 @@ __global__ void __launch_bounds__(1024) k_order(const FrameTable* __restrict__ f
     // of the next batch's prepass that k_trace runs (FusedPrepass)
     if (blockIdx.x == 0 && threadIdx.x < RT_CTR_BYTES / 4) counters[threadIdx.x] = 0u;
     if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 2) zero_ctl[threadIdx.x] = 0u;
-    if (gate) { // the gated launch: this workgroup's frames' task flags and ray counters start at zero
+    if (gate) { // the gated launch: this workgroup's frames' task masks, ray counters and tile claims start at zero
         const uint32_t g0 = m.order_batch ? 0u : blockIdx.x, g1 = m.order_batch ? m.n_frames : blockIdx.x + 1u;
         for (uint32_t i = g0 * RT_GATE_WORDS + threadIdx.x; i < g1 * RT_GATE_WORDS; i += blockDim.x) gate[i] = 0u;
+        const uint32_t nt = m.n_units >> 4; // order entries per frame (this workgroup writes entries [g0 nt, g1 nt))
+        for (uint32_t i = g0 * nt + threadIdx.x; i < g1 * nt; i += blockDim.x) claims[i] = 0u;
     }
     if (wait_ctl) {
         // this batch's prepass runs inside the previous batch's k_trace (FusedPrepass): wait until its
@@ -592,11 +594,14 @@ __device__ __forceinline__ float4 ld_rec(const float4* base, uint32_t i)
     const v4f_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(i * 16u), 0, 16 /* sc1 */);
     return make_float4(v.x, v.y, v.z, v.w);
 }
-__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i)
+// word i of a buffer with a uniform base (one offset register per lane): sc1 (another wave or workgroup
+// wrote it in this launch) or plain
+__device__ __forceinline__ uint32_t ld_u32(const uint32_t* base, uint32_t i, bool sc1 = true)
 {
     const __amdgpu_buffer_rsrc_t r =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(base), (short)0, 0x7fffffff, 0x00020000);
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 16 /* sc1 */);
+    return sc1 ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 16 /* sc1 */)
+               : __builtin_amdgcn_raw_buffer_load_b32(r, (int)(i * 4u), 0, 0);
 }
 __device__ __forceinline__ float4 ld_fresh(const float4* p)
 {
@@ -977,8 +982,9 @@ struct TraceQueues {
     uint32_t pad1;
     uint32_t f_top;            // free slots of the block's fin pool: fin_free[0, f_top)
     uint32_t overflow;         // RT_FLAG_*: a queue push past its bound was dropped (published at exit)
-    uint32_t d_head, d_tail;   // the gated launch: the block's deferred units, defer[d_head, d_tail) in HBM
-    uint32_t gq_done;          // the global unit queue is exhausted (drained: and no unit is deferred either)
+    // the gated launch (GatedPrepass), per block so that no wave holds them in registers: the block's tile
+    // scan position, every frame's prepass seen done, the frames whose CellDistance is seen flagged
+    uint32_t gscan, gate_all, gate_cells;
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
     uint32_t ao_ctr[kAoSlots / 2]; // AO slot s: bits 16 (s & 1) + 0..4 rays finished, + 5..9 occluded
@@ -1061,8 +1067,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.ls_top = 0;
         q.f_top = fin_slots;
         q.overflow = 0;
-        q.d_head = q.d_tail = 0;
-        q.gq_done = 0;
+        q.gscan = q.gate_all = q.gate_cells = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
@@ -1077,6 +1082,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     if constexpr (STATS) c.nz.lds_calls = (__attribute__((address_space(3))) unsigned long long*)&s_st.v[BlockStats::NOISE];
     const uint32_t W = (uint32_t)k->width, H = (uint32_t)k->height, aa = (uint32_t)k->aa_samples;
     const int max_steps = k->max_steps;
+    const uint32_t n_total = (uint32_t)__builtin_amdgcn_readfirstlane(m.n_units * m.n_frames); // units (an SGPR)
     // this block's hit stack and long-ray spill stack (hit_cap / long_spill_cap records per block)
     constexpr uint32_t HR = HitRec<L>::N;
     float4* const hq = hitq + (size_t)blockIdx.x * hit_cap * HR;
@@ -1560,91 +1566,127 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             guint* gf = (guint*)(gp.gate + f * RT_GATE_WORDS);
             uint32_t old = 0;
             if (lane == 0) {
-                __hip_atomic_store(gf + (qt - f * RT_FUSE_TASKS_PER_FRAME), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t task = qt - f * RT_FUSE_TASKS_PER_FRAME; // = ray row * 4 + ray column / 8
+                __hip_atomic_fetch_or(gf + (task >> 5), 1u << (task & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 old = __hip_atomic_fetch_add(gf + RT_GATE_CTR, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
             }
             if ((uint32_t)__builtin_amdgcn_readfirstlane(old) == RT_CAMERA_RES * RT_CAMERA_RES - RT_FUSE_RAYS_PER_TASK) {
-                // the frame's last task (its add returned last): every ray is in
+                // the frame's last task (its add returned last): every ray is in.  Its CellDistance (8-B sc1
+                // stores), waited, then the cells flag: later units read their brackets from it (gate_cells)
                 const float4* cam = pft->cam[f];
-                float2* cells = pft->cells[f];
-                for (uint32_t c = late(lane); c < RT_CAMERA_RES * RT_CAMERA_RES; c += 64u)
-                    cells[c] = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); },
+                typedef unsigned long long __attribute__((address_space(1))) gu64;
+                gu64* cells = (gu64*)pft->cells[f];
+                for (uint32_t c = late(lane); c < RT_CAMERA_RES * RT_CAMERA_RES; c += 64u) {
+                    const float2 b = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); },
                                                   (int)(c % RT_CAMERA_RES), (int)(c / RT_CAMERA_RES));
+                    __hip_atomic_store(cells + c, (unsigned long long)__float_as_uint(b.x) |
+                                                      ((unsigned long long)__float_as_uint(b.y) << 32),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+                if (lane == 0) __hip_atomic_store(gf + RT_GATE_CTR + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     };
 
-    // ---- the gated launch (GatedPrepass): may unit (f, u) start? ----
-    // Its lanes' cells (the corner pixels' cells bound them: the cell index grows with the pixel) read
-    // CameraResults rays of rows cy0 - 2 .. cy1 + 2 and columns cx0 - 2 .. cx1 + 2 (setTargetDepths'
-    // 5 x 5 taps, clamped; its edge extrapolation reads inside that range).  Ready when the frame's ray
-    // counter is complete, or every task (8 rays of a row) covering that range has flagged.  sc1 polls
-    // (the hand-off: each task wave stored its line sc1 and waited before its flag store / counter add).
+    // ---- the gated launch (GatedPrepass): which unit next? ----
+    // Units are claimed by tile, in k_order's longest-first order, from the tiles whose prepass rays are in:
+    // the scan starts at the first tile with units left (counters[RT_CTR_SCAN]), reads 64 order entries
+    // and their claim counters (claims[i]: units of order entry i taken, atomic adds) per step, and takes the
+    // first unit of the first READY tile with units left.  A tile is ready when every task (8 rays of a row)
+    // holding a CameraResults ray its cells' setTargetDepths reads has set its bit in the frame's task mask
+    // (rows cy0 - 2 .. cy1 + 2, columns cx0 - 2 .. cx1 + 2 of its pixels' cells; the cell index grows with
+    // the pixel, so the corner pixels bound them).  So units run in the longest-first order among the ready
+    // ones, on any block (no unit waits in a block that took it).  sc1 loads throughout (the hand-off: a
+    // task wave stored its line sc1 and waited before its mask bit).
     typedef const uint32_t __attribute__((address_space(1))) gcuint;
-    uint32_t gate_done = 0u; // frames whose ray counter this wave has seen complete (wave-uniform)
-    auto gate_ready = [&](uint32_t f, uint32_t u) -> bool {
-        if ((gate_done >> f) & 1u) return true;
-        const uint32_t* gf = gp.gate + f * RT_GATE_WORDS;
-        if (__hip_atomic_load((gcuint*)(gf + RT_GATE_CTR), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-            (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES)) {
-            gate_done |= 1u << f;
-            return true;
-        }
-        uint32_t px0, py0;
-        unit_pixel(m, f, u, 0u, W, H, &px0, &py0);
-        if (px0 >= W || py0 >= H) return true; // no lane of the unit is in the frame
-        const uint32_t px1 = px0 + 7u < W ? px0 + 7u : W - 1u, py1 = py0 + 7u < H ? py0 + 7u : H - 1u;
-        auto cell_of = [&](uint32_t p, float r) {
-            return __builtin_amdgcn_readfirstlane((int)rtm::floor(((float)p * r) * 32.0f));
-        };
-        const int cx0 = cell_of(px0, k->rcp_w), cx1 = cell_of(px1, k->rcp_w);
-        const int cy0 = cell_of(py0, k->rcp_h), cy1 = cell_of(py1, k->rcp_h);
-        const int xlo = cx0 - 2 < 0 ? 0 : cx0 - 2, xhi = cx1 + 2 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cx1 + 2;
-        const int ylo = cy0 - 2 < 0 ? 0 : cy0 - 2, yhi = cy1 + 2 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cy1 + 2;
-        constexpr int kTaskRow = RT_CAMERA_RES / RT_FUSE_RAYS_PER_TASK; // 4 tasks per prepass row
-        const int tlo = xlo / RT_FUSE_RAYS_PER_TASK, thi = xhi / RT_FUSE_RAYS_PER_TASK;
-        // lane p: row ylo + p / 4, task p % 4 of that row (rows <= 32: two rounds at most)
-        const uint32_t gbase = f * RT_GATE_WORDS + (uint32_t)ylo * kTaskRow;
-        const uint32_t nflags = (uint32_t)(yhi - ylo + 1) * kTaskRow;
-        bool ok = true;
-        for (uint32_t p = lane; p < nflags; p += 64u) {
-            const int t = (int)(p & (kTaskRow - 1));
-            if (t >= tlo && t <= thi)
-                ok = ok && __hip_atomic_load((gcuint*)(gp.gate + gbase + p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        }
-        return __ballot(!ok) == 0ull;
+    auto ld_sc1 = [&](const uint32_t* p) {
+        return __hip_atomic_load((gcuint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // the block's deferred units (not ready when taken): a FIFO in HBM under the block's lock, retried
-    // before new units are taken.  A full list (never expected: 1024 per block) makes the wave wait instead.
-    uint32_t* const dq = gp.defer + (size_t)blockIdx.x * RT_DEFER_CAP;
-    auto defer_push = [&](uint32_t qi) -> bool {
-        q_lock(&q.lock, lane);
-        const uint32_t t = vload(q.d_tail), h = vload(q.d_head);
-        const bool ok = t - h < (uint32_t)RT_DEFER_CAP;
-        if (ok && lane == 0) dq[t % RT_DEFER_CAP] = qi;
-        __builtin_amdgcn_s_waitcnt(0);
-        if (ok && lane == 0) q.d_tail = t + 1u;
-        q_unlock(&q.lock, lane);
+    // tile order entry e (frame << 24 | shard tile) against its frame's task mask w0..w3
+    auto tile_ready = [&](uint32_t e, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) -> bool {
+        const uint32_t f = e >> 24, first = m.frame_rot ? (m.tile_first + f) % m.tile_stride : m.tile_first;
+        const uint32_t T = (e & 0xffffffu) * m.tile_stride + first;
+        const uint32_t gx = (T % m.tiles32_x) * 32u, gy = (T / m.tiles32_x) * 32u;
+        const uint32_t px0 = gx + m.off_x, py0 = gy + m.off_y;
+        if (gx >= m.ext_x || gy >= m.ext_y || px0 >= W || py0 >= H) return true; // no pixel: nothing to wait for
+        const uint32_t xe = m.off_x + m.ext_x < W ? m.off_x + m.ext_x : W, ye = m.off_y + m.ext_y < H ? m.off_y + m.ext_y : H;
+        const uint32_t px1 = px0 + 31u < xe ? px0 + 31u : xe - 1u, py1 = py0 + 31u < ye ? py0 + 31u : ye - 1u;
+        auto cell_of = [&](uint32_t p, float r) { return (int)rtm::floor(((float)p * r) * 32.0f); };
+        const int cx0 = cell_of(px0, k->rcp_w) - 2, cx1 = cell_of(px1, k->rcp_w) + 2;
+        const int cy0 = cell_of(py0, k->rcp_h) - 2, cy1 = cell_of(py1, k->rcp_h) + 2;
+        const int xlo = cx0 < 0 ? 0 : cx0, xhi = cx1 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cx1;
+        const int ylo = cy0 < 0 ? 0 : cy0, yhi = cy1 > RT_CAMERA_RES - 1 ? RT_CAMERA_RES - 1 : cy1;
+        // the row's tasks tlo .. thi as a 4-bit group (task = row * 4 + x / 8: bits 4 (row % 8) .. of word row / 8)
+        const uint32_t g = ((2u << (xhi / RT_FUSE_RAYS_PER_TASK)) - 1u) & ~((1u << (xlo / RT_FUSE_RAYS_PER_TASK)) - 1u);
+        bool ok = true;
+        for (int r = ylo; r <= yhi; ++r) {
+            const uint32_t w = (r >> 3) == 0 ? w0 : (r >> 3) == 1 ? w1 : (r >> 3) == 2 ? w2 : w3;
+            ok = ok && ((w >> ((r & 7) * 4)) & g) == g;
+        }
         return ok;
     };
-    auto defer_pop = [&](uint32_t* qi) -> bool {
-        if (vload(q.d_tail) == vload(q.d_head)) return false;
-        q_lock(&q.lock, lane);
-        const uint32_t t = vload(q.d_tail), h = vload(q.d_head);
-        uint32_t v = 0;
-        if (t != h) {
-            v = ld_u32(dq, h % RT_DEFER_CAP); // another wave of this block stored it: L1-bypassing
-            __builtin_amdgcn_s_waitcnt(0);
-            if (lane == 0) q.d_head = h + 1u;
+    // one scan step per call: 64 order entries from the block's scan position q.gscan (the global head when
+    // it is behind it); 1: a unit (f, u) claimed; 0: none ready in this step (the next call looks further, and
+    // starts over at the head once past the end); -1: no unit left anywhere
+    auto gated_fetch = [&](uint32_t* pf, uint32_t* pu) -> int {
+        const uint32_t nt = n_total >> 4; // order entries (tiles) of the batch
+        const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(ld_sc1(counters + RT_CTR_SCAN));
+        if (h >= nt) return -1;
+        const bool gate_all = vload(q.gate_all) != 0u;
+        const uint32_t gs = vload(q.gscan);
+        const uint32_t base = gs > h && gs < nt ? gs : h;
+        const uint32_t i = late(base + lane); // (late: no per-lane scan address hoisted into the prologue)
+        uint32_t e = 0u, c = 16u;
+        if (i < nt) { // buffer loads: uniform bases, one offset register
+            e = ld_u32(order, i, false);
+            c = ld_u32(gp.claims, i);
         }
-        q_unlock(&q.lock, lane);
-        *qi = (uint32_t)__builtin_amdgcn_readfirstlane(v);
-        return t != h;
+        const bool left = c < 16u;
+        const uint64_t lb = __ballot(left);
+        if (base == h) { // the head moves past the tiles with no unit left
+            const uint32_t nh = lb ? base + (uint32_t)__builtin_ctzll(lb) : base + 64u;
+            if (nh > h && lane == 0) atomicMax(counters + RT_CTR_SCAN, nh);
+        }
+        if (lane == 0) q.gscan = base + 64u; // the block's next step (a hint: racing waves may repeat one)
+        bool ready = left;
+        if (!gate_all && left) { // the tile's frame's task mask (sc1 loads of its four words)
+            const uint32_t gw = (e >> 24) * RT_GATE_WORDS;
+            ready = tile_ready(e, ld_u32(gp.gate, gw), ld_u32(gp.gate, gw + 1u), ld_u32(gp.gate, gw + 2u),
+                               ld_u32(gp.gate, gw + 3u));
+        }
+        for (uint64_t rb = __ballot(ready); rb; rb &= rb - 1ull) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(rb);
+            uint32_t kk = 0u;
+            if (lane == 0) kk = atomicAdd(gp.claims + late(base + l), 1u);
+            kk = (uint32_t)__builtin_amdgcn_readfirstlane(kk);
+            if (kk < 16u) {
+                const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)l);
+                *pf = el >> 24;
+                *pu = (el & 0xffffffu) * 16u + kk;
+                if (lane == 0) q.gscan = base; // (this step again next time: its tile may have units left)
+                return 1;
+            }
+        }
+        if (!gate_all && base + 64u >= nt) { // a pass over the order done: every frame's prepass done yet?
+            const uint32_t gw = lane < m.n_frames ? ld_u32(gp.gate, late(lane * RT_GATE_WORDS + RT_GATE_CTR))
+                                                  : (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES);
+            if (__ballot(gw < (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES)) == 0ull && lane == 0) q.gate_all = 1u;
+        }
+        return 0;
     };
 
     // ---- one 8x8 primary unit ----
     auto do_unit = [&](uint32_t f, uint32_t u) {
+        bool cells_in = true; // (the gated launch: the frame's CellDistance is stored, flagged by its last task)
+        if (gp.tasks) {
+            cells_in = (vload(q.gate_cells) >> f) & 1u;
+            if (!cells_in && ld_sc1(gp.gate + f * RT_GATE_WORDS + RT_GATE_CTR + 1) != 0u) {
+                cells_in = true;
+                if (lane == 0) atomicOr(&q.gate_cells, 1u << f);
+            }
+        }
         Ctx cf = frame_ctx(c, ft, f);
         cf.nz.phase = RT_PHASE_PRIMARY;
         uint32_t px, py;
@@ -1654,10 +1696,15 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
             const uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
-            if (gp.tasks) { // the gated launch: the cell's setTargetDepths from its CameraResults (gate_ready passed)
+            if (!cells_in) {
+                // the gated launch before the frame's CellDistance is flagged: the cell's setTargetDepths from
+                // its CameraResults (gate_ready passed)
                 const float4* cam = ft->cam[f];
                 plane_x = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); }, (int)(cell % RT_CAMERA_RES),
                                        (int)(cell / RT_CAMERA_RES)).x;
+            } else if (gp.tasks) { // flagged in this launch: an sc1 load of the bracket the frame's last task stored
+                typedef const float __attribute__((address_space(1))) gcfloat;
+                plane_x = __hip_atomic_load((gcfloat*)(ft->cells[f] + cell), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
                 plane_x = gptr(ft->cells[f])[cell].x;
             }
@@ -1754,7 +1801,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     bool first_unit = true;
     bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
     bool gp_open = gp.tasks != 0u; // this batch's own prepass tasks may remain (GatedPrepass)
-    const uint32_t n_total = m.n_units * m.n_frames;
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
         if constexpr (L == RT_NOMADPLAINS) {
@@ -1803,57 +1849,39 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }
-        // the gated launch: units that were not ready when taken wait in the block's deferred list
-        const bool deferred = gp.tasks != 0u && vload(q.d_tail) != vload(q.d_head);
-        if (!drained || first_unit || deferred) { // a wave's static first unit is taken even after the queue drained
+        if (gp.tasks != 0u ? !drained : (!drained || first_unit)) {
+            // (without the gated launch a wave's static first unit is taken even after the queue drained)
             if (lane == 0) atomicAdd(&q.active, 1u);
-            // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
-            auto unit_of = [&](uint32_t qi, uint32_t* f, uint32_t* u) {
-                const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);
-                *f = e >> 24;
-                *u = (e & 0xffffffu) * 16u + (qi & 15u);
-            };
-            // one unit to run, from the deferred list or the queue (do_unit is inlined once)
             bool run = false;
-            uint32_t qi = 0, f = 0, u = 0;
-            // try: unit qi may run now, or goes (back) to the deferred list, or (the list is full) is waited for
-            bool wait = false;
-            auto try_unit = [&]() {
-                unit_of(qi, &f, &u);
-                if (gp.tasks == 0u || gate_ready(f, u)) run = true;
-                else if (!defer_push(qi)) run = wait = true;
-            };
-            if (deferred && defer_pop(&qi)) try_unit(); // the oldest deferred unit first, if its rays are in
-            // `drained` (the tail behaviours: small shading and long-ray batches, segments) only once no unit
-            // is left anywhere: the global queue is exhausted AND nothing waits in the deferred list
-            auto nothing_deferred = [&]() { return gp.tasks == 0u || vload(q.d_tail) == vload(q.d_head); };
-            if (!run && (vload(q.gq_done) == 0u || first_unit)) {
-                qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+            uint32_t f = 0, u = 0;
+            if (gp.tasks != 0u) { // the gated launch: the first unit of a ready tile, longest-first
+                const int got = __builtin_amdgcn_readfirstlane(gated_fetch(&f, &u)); // (wave-uniform)
+                run = got > 0;
+                if (got < 0) {
+                    if (lane == 0) q.drained = 1u;
+                } // (0: no ready tile in this step; the next call looks further)
+            } else {
+                const uint32_t qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
                 first_unit = false;
                 if (qi < n_total) {
-                    try_unit();
+                    // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
+                    const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);
+                    f = e >> 24;
+                    u = (e & 0xffffffu) * 16u + (qi & 15u);
+                    run = true;
                 } else if (lane == 0) {
-                    q.gq_done = 1u;
-                    if (nothing_deferred()) q.drained = 1u;
+                    q.drained = 1u;
                 }
-            } else if (!run) {
-                // the queue is exhausted: only deferred units, whose rays are still marching
-                if (lane == 0 && nothing_deferred()) q.drained = 1u;
-                __builtin_amdgcn_s_sleep(32);
             }
-            if (run) {
-                if (wait)
-                    while (!gate_ready(f, u)) __builtin_amdgcn_s_sleep(8);
-                do_unit(f, u);
+            if (run) { // (do_unit inlined once; f and u are wave-uniform: say so, for the divergence analysis)
+                do_unit((uint32_t)__builtin_amdgcn_readfirstlane(f), (uint32_t)__builtin_amdgcn_readfirstlane(u));
                 WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
             }
             if (lane == 0) atomicSub(&q.active, 1u);
             continue;
         }
         // drained and nothing queued: leave once no wave of the block can still push
-        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u &&
-            (gp.tasks == 0u || vload(q.d_tail) == vload(q.d_head)))
-            break;
+        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) break;
         __builtin_amdgcn_s_sleep(2);
         WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
     }
@@ -2093,7 +2121,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     // k_order: setTargetDepths (cells_from_cam), the work counters' reset, the tile order
     // (fuse_next.ctl is zeroed even with no tasks: RT_DEVICE_DEBUG_WITHHOLD_FUSE's timeout test)
     hipLaunchKernelGGL(k_order, dim3(m.order_batch ? 1u : m.n_frames), blk, 0, a.stream, a.frames, m, a.order, a.queue,
-                       a.wait_ctl, a.wait_total, a.fuse_next.ctl, a.host_flag, a.gated.tasks ? a.gated.gate : nullptr);
+                       a.wait_ctl, a.wait_total, a.fuse_next.ctl, a.host_flag, a.gated.tasks ? a.gated.gate : nullptr,
+                       a.gated.claims);
     if (a.after_order) (void)hipEventRecord(a.after_order, a.stream);
     if (a.after_order_fuse) (void)hipEventRecord(a.after_order_fuse, a.stream);
     // primary + shading + long rays; what does not fit a CU's LDS rings goes to its spill stacks

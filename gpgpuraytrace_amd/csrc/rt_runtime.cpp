@@ -126,7 +126,7 @@ struct rt_device_s {
     float4* finpool = nullptr; // k_trace's per-block fin pools (RT_FIN_SLOTS slots of 3 float4 per block)
     float4* cpool = nullptr;   // k_trace's per-block AO colour pools (RT_AO_POOL_SLOTS float4 per block)
     uint32_t* gate = nullptr;  // the gated launch (GatedPrepass): per frame task flags + ray counter
-    uint32_t* defer = nullptr; //   and k_trace's per-block deferred units (RT_DEFER_CAP per block)
+    uint32_t* claims = nullptr; //   and the units claimed per tile of the batch's order
     uint32_t* aocc = nullptr;
     size_t samples_cap = 0;
     // dominant-kernel timing (rt_device_set_profiling)
@@ -605,7 +605,6 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         HIP_TRY(hipMalloc(&dev->finpool, (size_t)dev->num_cus * RT_FIN_SLOTS * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->cpool, (size_t)dev->num_cus * RT_AO_POOL_SLOTS * sizeof(float4)));
         if (!dev->gate) HIP_TRY(hipMalloc(&dev->gate, (size_t)RT_MAX_BATCH * RT_GATE_WORDS * sizeof(uint32_t)));
-        if (!dev->defer) HIP_TRY(hipMalloc(&dev->defer, (size_t)dev->num_cus * RT_DEFER_CAP * sizeof(uint32_t)));
         dev->hitq_n = hq_need;
         dev->spill_long_n = ls_need;
     }
@@ -630,6 +629,8 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
     HIP_TRY(hipMemsetAsync(dev->aocc, 0, (need + 3) / 4 * sizeof(uint32_t), dev->stream));
     HIP_TRY(hipMalloc(&dev->order, rt_split_samples(dev->width, dev->height, 1) / 64 * RT_MAX_BATCH * sizeof(uint32_t)));
     HIP_TRY(hipMalloc(&dev->hitmask, need / 64 * sizeof(uint64_t)));
+    if (dev->claims) HIP_TRY(hipFree(dev->claims));
+    HIP_TRY(hipMalloc(&dev->claims, rt_split_samples(dev->width, dev->height, 1) / 1024 * RT_MAX_BATCH * sizeof(uint32_t)));
     dev->samples_cap = need;
     return RT_OK;
 }
@@ -733,7 +734,7 @@ rt_device_s::~rt_device_s()
         delete t;
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
-                    (void*)hitq, (void*)finpool, (void*)cpool, (void*)gate, (void*)defer, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
+                    (void*)hitq, (void*)finpool, (void*)cpool, (void*)gate, (void*)claims, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
                     (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
@@ -1340,7 +1341,7 @@ void key_launch(std::vector<uint64_t>& k, const RtLaunch& a)
                           (uint64_t)a.cells_from_cam, (uint64_t)a.small_rings, (uint64_t)a.fit, (uint64_t)a.fitm, (uint64_t)(uintptr_t)a.fin, (uint64_t)(uintptr_t)a.finpool, (uint64_t)(uintptr_t)a.cpool,
                           (uint64_t)(uintptr_t)a.aocc, (uint64_t)a.ao_samples, (uint64_t)a.aa,
                           (uint64_t)(uintptr_t)a.order, (uint64_t)(uintptr_t)a.frames, (uint64_t)a.n_frames,
-                          (uint64_t)(uintptr_t)a.gated.gate, (uint64_t)(uintptr_t)a.gated.defer, (uint64_t)a.gated.tasks,
+                          (uint64_t)(uintptr_t)a.gated.gate, (uint64_t)(uintptr_t)a.gated.claims, (uint64_t)a.gated.tasks,
                           (uint64_t)a.packed};
     k.insert(k.end(), std::begin(v), std::end(v));
 }
@@ -1560,7 +1561,7 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
                        (!fuse || (fuse->wait_ctl == nullptr && fuse->next.ctl == nullptr)) &&
                        b.s0->landscape == RT_NOMADPLAINS &&
                        !(dev->flags & (RT_DEVICE_STATS | RT_DEVICE_PREPASS_INLINE));
-    if (gated) la_scr.gated = GatedPrepass{dev->gate, dev->defer, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+    if (gated) la_scr.gated = GatedPrepass{dev->gate, dev->claims, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
     // rt_terrain_prepass_ahead: ev_order follows the last read of the frames' CameraResults -- k_order's,
     // or with the gated launch k_trace's (recorded after the trace below)
     if (!graphs && dev->ev_order && !gated) {
