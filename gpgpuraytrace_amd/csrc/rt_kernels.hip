@@ -1656,7 +1656,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             ready = tile_ready(e, ld_u32(gp.gate, gw), ld_u32(gp.gate, gw + 1u), ld_u32(gp.gate, gw + 2u),
                                ld_u32(gp.gate, gw + 3u));
         }
-        for (uint64_t rb = __ballot(ready); rb; rb &= rb - 1ull) {
+        // the wave's first try is the ready tile at or after its own lane slot in the step (rotated ballot), so
+        // the waves scanning one step spread their claims over its ready tiles instead of all contending for
+        // the first one (within a step of 64 the order is longest-first only roughly anyway)
+        const uint64_t rdy = __ballot(ready);
+        // (the spread: the wave's hardware id -- wave, SIMD, CU -- read when needed, no register held for it)
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        const uint64_t from = rdy & (~0ull << ((hw ^ (hw >> 6) ^ (hw >> 12)) & 63u));
+        for (uint64_t rb = from ? from : rdy; rb; rb &= rb - 1ull) {
             const uint32_t l = (uint32_t)__builtin_ctzll(rb);
             uint32_t kk = 0u;
             if (lane == 0) kk = atomicAdd(gp.claims + late(base + l), 1u);
@@ -1809,7 +1816,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (gp_open) {
                 const uint32_t qt = wave_fetch(&counters[RT_CTR_GATE], lane);
                 if (qt < gp.tasks) {
+                    WT(const unsigned long long tp = __builtin_amdgcn_s_memrealtime();)
                     do_prepass(ft, qt, true);
+                    WT(const unsigned long long tq = __builtin_amdgcn_s_memrealtime(); wt[21] += tq - tp; wt[22] = tq;)
                     continue;
                 }
                 gp_open = false;

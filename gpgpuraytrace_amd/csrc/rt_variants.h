@@ -93,7 +93,7 @@
 #define RT_DIAG_HITPAD 0
 #endif
 #ifdef RT_WAVE_TRACE
-#define RT_WT_FIELDS 21
+#define RT_WT_FIELDS 23
 #define RT_WT_MAX_WAVES 8192
 #define WT(...) __VA_ARGS__
 #else

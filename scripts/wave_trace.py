@@ -17,7 +17,7 @@ import with_variant  # noqa: E402
 
 with_variant.apply()
 
-F = 21
+F = 23
 
 
 def main():
@@ -75,6 +75,11 @@ def main():
         print(f"  {end[i]:8.1f}  {us(r[2]):8.1f},{r[5]:3d}  {us(r[3]):8.1f},{r[6]:3d}  {us(r[4]):8.1f},{r[7]:3d}  "
               f"{us(r[8] - t0) if r[8] else 0:8.1f}  {us(r[9]):7.1f}  {r[10]:#010x}  {r[11]}  {r[12]}  {r[13]}  "
               f"{r[14]}  {r[16]}")
+    # the gated launch's prepass tasks (fields 21, 22: task time, last task end)
+    tw = t[:, 21] > 0
+    if tw.any():
+        print(f"prepass tasks: {tw.sum()} waves, task time mean {tot(21)[tw].mean():.1f} max {tot(21)[tw].max():.1f} us; "
+              f"last task end p50 {np.percentile(us(t[tw, 22] - t0), 50):.1f} max {us(t[tw, 22] - t0).max():.1f} us")
     # per SIMD busy (unit+shade+long) from hw_id: simd [5:4], cu [11:8], sh [12], se [15:13], + xcc
     hw = t[:, 10]
     simd = (hw >> 4) & 3
