@@ -1543,7 +1543,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             while (march_live<L, false, true>(cp, st, RT_CAMERA_FAR, 0)) {
                 auto dens = [&](f3 q0) {
                     uint32_t used;
-                    return density_nomadplains_seg<LPR, true>(cp, g, q0, j, base, &used);
+                    return density_nomadplains_seg<LPR, false>(cp, g, q0, j, base, &used);
                 };
                 march_step_with<L, false, true, decltype(dens), true>(cp, st, dens);
             }
@@ -1632,9 +1632,28 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // starts over at the head once past the end); -1: no unit left anywhere
     auto gated_fetch = [&](uint32_t* pf, uint32_t* pu) -> int {
         const uint32_t nt = n_total >> 4; // order entries (tiles) of the batch
+        const bool gate_all = vload(q.gate_all) != 0u;
+        if (gate_all) {
+            // every prepass ray is in: the first tile with units left, by its claim counter (a ticket per tile:
+            // one atomic per unit, as the queue counter of a launch without the gate)
+            for (int tries = 0; tries < 4; ++tries) {
+                const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(ld_u32(counters, RT_CTR_SCAN));
+                if (h >= nt) return -1;
+                uint32_t kk = 0u;
+                if (lane == 0) kk = atomicAdd(gp.claims + late(h), 1u);
+                kk = (uint32_t)__builtin_amdgcn_readfirstlane(kk);
+                if (kk < 16u) {
+                    const uint32_t e = __builtin_amdgcn_readfirstlane(order[h]);
+                    *pf = e >> 24;
+                    *pu = (e & 0xffffffu) * 16u + kk;
+                    return 1;
+                }
+                if (lane == 0) atomicMax(counters + RT_CTR_SCAN, h + 1u);
+            }
+            return 0;
+        }
         const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(ld_sc1(counters + RT_CTR_SCAN));
         if (h >= nt) return -1;
-        const bool gate_all = vload(q.gate_all) != 0u;
         const uint32_t gs = vload(q.gscan);
         const uint32_t base = gs > h && gs < nt ? gs : h;
         const uint32_t i = late(base + lane); // (late: no per-lane scan address hoisted into the prologue)
@@ -1882,6 +1901,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     q.drained = 1u;
                 }
             }
+            WT(if (!run) wt[9] += __builtin_amdgcn_s_memrealtime() - t0;) // (a fetch that found no unit: idle)
             if (run) { // (do_unit inlined once; f and u are wave-uniform: say so, for the divergence analysis)
                 do_unit((uint32_t)__builtin_amdgcn_readfirstlane(f), (uint32_t)__builtin_amdgcn_readfirstlane(u));
                 WT(const unsigned long long t1 = __builtin_amdgcn_s_memrealtime(); wt[2] += t1 - t0; wt[5]++; wt[8] = t1;)
