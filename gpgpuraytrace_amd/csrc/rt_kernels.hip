@@ -1632,37 +1632,43 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // starts over at the head once past the end); -1: no unit left anywhere
     auto gated_fetch = [&](uint32_t* pf, uint32_t* pu) -> int {
         const uint32_t nt = n_total >> 4; // order entries (tiles) of the batch
-        const bool gate_all = vload(q.gate_all) != 0u;
+        bool gate_all = vload(q.gate_all) != 0u;
+        if (!gate_all) { // every frame's prepass done? (its ray counter; lanes < n_frames)
+            const uint32_t gw = lane < m.n_frames ? ld_u32(gp.gate, late(lane * RT_GATE_WORDS + RT_GATE_CTR))
+                                                  : (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES);
+            gate_all = __ballot(gw < (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES)) == 0ull;
+            if (gate_all && lane == 0) q.gate_all = 1u;
+        }
         if (gate_all) {
-            // every prepass ray is in: the first tile with units left, by its claim counter (a ticket per tile:
-            // one atomic per unit, as the queue counter of a launch without the gate)
-            for (int tries = 0; tries < 4; ++tries) {
-                const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(ld_u32(counters, RT_CTR_SCAN));
-                if (h >= nt) return -1;
-                uint32_t kk = 0u;
-                if (lane == 0) kk = atomicAdd(gp.claims + late(h), 1u);
-                kk = (uint32_t)__builtin_amdgcn_readfirstlane(kk);
-                if (kk < 16u) {
-                    const uint32_t e = __builtin_amdgcn_readfirstlane(order[h]);
+            // every prepass ray is in: the units in order by the queue counter (one atomic per unit, as without
+            // the gate), each claimed by its bit in its tile's word (claims[i], 16 units); a unit the scan took
+            // while the prepass ran (its bit set) is skipped
+            for (int tries = 0; tries < 16; ++tries) {
+                const uint32_t qi = wave_fetch(&counters[RT_CTR_PRIMARY], lane);
+                if (qi >= n_total) return -1;
+                uint32_t old = 0u;
+                if (lane == 0) old = atomicOr(gp.claims + late(qi >> 4), 1u << (qi & 15u));
+                if (!((__builtin_amdgcn_readfirstlane(old) >> (qi & 15u)) & 1u)) {
+                    const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);
                     *pf = e >> 24;
-                    *pu = (e & 0xffffffu) * 16u + kk;
+                    *pu = (e & 0xffffffu) * 16u + (qi & 15u);
                     return 1;
                 }
-                if (lane == 0) atomicMax(counters + RT_CTR_SCAN, h + 1u);
             }
             return 0;
         }
+        // while the prepass runs: a scan step of 64 tiles from the block's position (the head when behind it)
         const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane(ld_sc1(counters + RT_CTR_SCAN));
         if (h >= nt) return -1;
         const uint32_t gs = vload(q.gscan);
         const uint32_t base = gs > h && gs < nt ? gs : h;
         const uint32_t i = late(base + lane); // (late: no per-lane scan address hoisted into the prologue)
-        uint32_t e = 0u, c = 16u;
+        uint32_t e = 0u, c = 0xffffu;
         if (i < nt) { // buffer loads: uniform bases, one offset register
             e = ld_u32(order, i, false);
             c = ld_u32(gp.claims, i);
         }
-        const bool left = c < 16u;
+        const bool left = (c & 0xffffu) != 0xffffu;
         const uint64_t lb = __ballot(left);
         if (base == h) { // the head moves past the tiles with no unit left
             const uint32_t nh = lb ? base + (uint32_t)__builtin_ctzll(lb) : base + 64u;
@@ -1670,35 +1676,34 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
         if (lane == 0) q.gscan = base + 64u; // the block's next step (a hint: racing waves may repeat one)
         bool ready = left;
-        if (!gate_all && left) { // the tile's frame's task mask (sc1 loads of its four words)
+        if (left) { // the tile's frame's task mask (sc1 loads of its four words)
             const uint32_t gw = (e >> 24) * RT_GATE_WORDS;
             ready = tile_ready(e, ld_u32(gp.gate, gw), ld_u32(gp.gate, gw + 1u), ld_u32(gp.gate, gw + 2u),
                                ld_u32(gp.gate, gw + 3u));
         }
-        // the wave's first try is the ready tile at or after its own lane slot in the step (rotated ballot), so
-        // the waves scanning one step spread their claims over its ready tiles instead of all contending for
-        // the first one (within a step of 64 the order is longest-first only roughly anyway)
+        // the wave's first try is the ready tile at or after its own slot in the step, so the waves scanning one
+        // step spread their claims over its ready tiles (within a step the order is longest-first only roughly
+        // anyway); the slot from the wave's hardware id, read when needed (no register held for it)
         const uint64_t rdy = __ballot(ready);
-        // (the spread: the wave's hardware id -- wave, SIMD, CU -- read when needed, no register held for it)
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
         const uint64_t from = rdy & (~0ull << ((hw ^ (hw >> 6) ^ (hw >> 12)) & 63u));
         for (uint64_t rb = from ? from : rdy; rb; rb &= rb - 1ull) {
             const uint32_t l = (uint32_t)__builtin_ctzll(rb);
-            uint32_t kk = 0u;
-            if (lane == 0) kk = atomicAdd(gp.claims + late(base + l), 1u);
-            kk = (uint32_t)__builtin_amdgcn_readfirstlane(kk);
-            if (kk < 16u) {
-                const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)l);
-                *pf = el >> 24;
-                *pu = (el & 0xffffffu) * 16u + kk;
-                if (lane == 0) q.gscan = base; // (this step again next time: its tile may have units left)
-                return 1;
+            uint32_t cl = (uint32_t)__builtin_amdgcn_readlane((int)c, (int)l) | 0xffff0000u;
+            while (cl != 0xffffffffu) { // the tile's first unclaimed unit, by its bit
+                const uint32_t kk = (uint32_t)__builtin_ctz(~cl);
+                uint32_t old = 0u;
+                if (lane == 0) old = atomicOr(gp.claims + late(base + l), 1u << kk);
+                old = (uint32_t)__builtin_amdgcn_readfirstlane(old);
+                if (!((old >> kk) & 1u)) {
+                    const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)e, (int)l);
+                    *pf = el >> 24;
+                    *pu = (el & 0xffffffu) * 16u + kk;
+                    if (lane == 0) q.gscan = base; // (this step again next time: its tile may have units left)
+                    return 1;
+                }
+                cl |= old;
             }
-        }
-        if (!gate_all && base + 64u >= nt) { // a pass over the order done: every frame's prepass done yet?
-            const uint32_t gw = lane < m.n_frames ? ld_u32(gp.gate, late(lane * RT_GATE_WORDS + RT_GATE_CTR))
-                                                  : (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES);
-            if (__ballot(gw < (uint32_t)(RT_CAMERA_RES * RT_CAMERA_RES)) == 0ull && lane == 0) q.gate_all = 1u;
         }
         return 0;
     };
