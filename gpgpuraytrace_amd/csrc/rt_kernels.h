@@ -52,8 +52,14 @@ struct FusedPrepass {
 // longest-first order from the tiles whose cells' prepass rays (the 5x5 neighbourhoods setTargetDepths
 // reads) are in, so units start while the prepass's long rays still march.  tasks == 0: off (the prepass
 // ran before; cells from k_order).
-#define RT_GATE_WORDS 64 // per frame: the task mask (words 0-3), the ray counter and the cells flag on a line of their own
-#define RT_GATE_CTR 32
+#define RT_GATE_WORDS 256 // per frame: the task mask (words 0-3), the ray counter and the cells flag on a line of
+#define RT_GATE_CTR 32    // their own, the per-task wave counters (words 128-255)
+#define RT_GATE_TASKS 128
+// lanes per prepass ray in k_trace's prepass tasks (a task's 8 rays are marched by 8 / (64 / LPR) waves):
+// 32 lanes = one round of the 18 octave values per step (the standalone camerarays' shape)
+#ifndef RT_PREPASS_LPR
+#define RT_PREPASS_LPR 32
+#endif
 struct GatedPrepass {
     uint32_t* gate;   // RT_MAX_BATCH x RT_GATE_WORDS
     uint32_t* claims; // per order entry (tile of the batch): its units claimed so far

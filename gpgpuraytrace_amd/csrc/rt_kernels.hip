@@ -48,7 +48,11 @@ __device__ __forceinline__ void load_noise_lds(uint32_t* lds, const uint32_t* __
         const int i = threadIdx.x;
         if (i < kNpOct) {
             const int n = i <= RT_NP_OCTAVES ? i : RT_NP_OCTAVES;
-            oct[i] = make_float4(k->np_scale[n], k->np_scale_y[n], k->np_rcp[n], 0.0f);
+            float pre = 0.0f; // RT_FBM_EXIT: sum of the octave weights 1 .. n (the suffix bound's prefix)
+#if RT_FBM_EXIT
+            for (int m = 1; m <= n; ++m) pre += k->np_rcp[m];
+#endif
+            oct[i] = make_float4(k->np_scale[n], k->np_scale_y[n], k->np_rcp[n], pre);
         }
     }
     float4* gxy = reinterpret_cast<float4*>(lds + kLdsGxy / 4);
@@ -834,6 +838,37 @@ __device__ __forceinline__ void ao_begin(const Ctx& c, const ShadeHit& h, uint32
     march_begin(c, st, h.hp, 0.4f, h.prec, ao_dir(h.n, h.px, h.py, h.a, kk), false);
 }
 
+// AO generator record (RT_AO_GEN, AO_SAMPLES >= 2): a shaded hit's AO rays as ONE ring record, expanded
+// into its AO_SAMPLES rays at refill, one lane each (gen_begin), instead of AO_SAMPLES long-ray records
+// pushed by the shading (64 hits x (1 + AO_SAMPLES) records per batch overflowed the LDS ring into the
+// spill stack: C5's long-ray spills).  (hit position, stepmod), (n.x, aux, kGenMark, t),
+// (n.y, n.z, px | py << 16, a): kGenMark in a long record's iters slot (a march has far fewer steps).
+constexpr uint32_t kGenMark = 0xfffffff0u;
+// generator records carry 2 .. 8 AO rays: a post-drain segment wave (8 rays) must be able to take one whole
+__device__ __forceinline__ bool gen_on(const RtConsts* k)
+{
+    return RT_AO_GEN && k->ao_samples >= 2 && k->ao_samples <= 8 && 64u / (RT_SEG_LANES ? RT_SEG_LANES : 8u) >= 8u;
+}
+__device__ __forceinline__ bool rec_is_gen(float4 r1) { return __float_as_uint(r1.z) == kGenMark; }
+__device__ __forceinline__ void gen_pack(const ShadeHit& h, uint32_t t, uint32_t aux, float4* r)
+{
+    r[0] = make_float4(h.hp.x, h.hp.y, h.hp.z, h.prec);
+    r[1] = make_float4(h.n.x, __uint_as_float(aux), __uint_as_float(kGenMark), __uint_as_float(t));
+    r[2] = make_float4(h.n.y, h.n.z, __uint_as_float(h.px | (h.py << 16)), __uint_as_float(h.a));
+}
+// AO ray kk of a generator record: ao_begin's march state (the state long_pack + long_unpack would
+// carry: lastStep, d, f and sd are not read before the first step overwrites them)
+template <int L>
+__device__ __forceinline__ uint32_t gen_begin(const Ctx& c, float4 r0, float4 r1, float4 r2, uint32_t kk,
+                                              March<L, true>& st, uint32_t* aux)
+{
+    *aux = __float_as_uint(r1.y);
+    const uint32_t pp = __float_as_uint(r2.z);
+    march_begin(c, st, rtm::mk(r0.x, r0.y, r0.z), 0.4f, r0.w,
+                ao_dir(rtm::mk(r1.x, r2.x, r2.y), pp & 0xffffu, pp >> 16, __float_as_uint(r2.w), kk), false);
+    return __float_as_uint(r1.w);
+}
+
 // The inputs a long shadow ray needs to finish its sample: (albedo + specular, brightness), fcolord
 // (fog-live landscapes only; 0 otherwise) and (rayleigh, skyAmount): FinRec<L>::N float4 at f, a
 // slot of the block's fin pool or fin[t].
@@ -954,6 +989,9 @@ constexpr uint32_t kCompactLive = RT_COMPACT_LIVE; // live lanes below which a d
 // as segments of kSegLanes lanes per ray (density_nomadplains_seg: the octaves spread over the
 // segment), cutting the per-step latency that sets a launch's last few hundred microseconds.
 constexpr uint32_t kSegLanes = RT_SEG_LANES, kSegHandBack = RT_SEG_HANDBACK, kSegQueue = RT_SEG_QUEUE;
+// a prepass task (FusedPrepass / GatedPrepass: 8 rays) is marched by kPrepassSplit waves of 64 / RT_PREPASS_LPR rays
+constexpr uint32_t kPrepassSplit = RT_FUSE_RAYS_PER_TASK / (64u / RT_PREPASS_LPR);
+static_assert(kPrepassSplit >= 1u && RT_PREPASS_LPR >= RT_FUSE_RAYS_PER_TASK && RT_PREPASS_LPR <= 32, "prepass lanes per ray");
 // A primary unit's last few rays (nomadplains): once at most kPrimarySeg rays of an 8x8 unit are
 // still marching, they continue as segments of 64 / kPrimarySeg lanes per ray (primary_seg in
 // k_trace) instead of keeping 64 lanes on a few rays' octave loops.  0: off.
@@ -1103,21 +1141,21 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
        wt[11] = __builtin_amdgcn_s_getreg((31 << 11) | 20); uint32_t wl_rays = 0, wl_maxit = 0, wp_maxit = 0;)
     // push the lanes' long rays (shadow continuations or AO starts) to the ring, or to the
     // block's spill stack when the LDS ring is full (stored before the tail publishes them)
-    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
+    auto push_recs = [&](bool want, auto pack) {
         const uint64_t lb = __ballot(want);
         if (!lb) return;
         const uint32_t n = (uint32_t)__popcll(lb), rank = lane_rank(lb);
         q_lock(&q.lock, lane);
         const uint32_t lh = vload(q.l_head), lt = vload(q.l_tail);
         if (lt - lh + n <= long_ring_cap) {
-            if (want) long_pack(st, t, aux, &q.longs[((lt + rank) % kLongRing) * kShadowRec]);
+            if (want) pack(&q.longs[((lt + rank) % kLongRing) * kShadowRec]);
             if (lane == 0) q.l_tail = lt + n;
         } else {
             // the spill stack's bound (rt_spill_caps) holds by the work priorities; a push past it is
             // dropped and flagged (rt_device_check), never written over queued rays
             const uint32_t stl = (uint32_t)__builtin_amdgcn_readfirstlane(vload(q.ls_top));
             const bool fits = stl + n <= long_spill_cap;
-            if (want && fits) long_pack(st, t, aux, lspill + (size_t)(stl + rank) * kShadowRec);
+            if (want && fits) pack(lspill + (size_t)(stl + rank) * kShadowRec);
             __builtin_amdgcn_s_waitcnt(0);
             if (lane == 0) {
                 q.ls_top = fits ? stl + n : stl;
@@ -1126,6 +1164,63 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
         q_unlock(&q.lock, lane);
     };
+    auto push_long = [&](bool want, const March<L, true>& st, uint32_t t, uint32_t aux) {
+        push_recs(want, [&](float4* r) { long_pack(st, t, aux, r); });
+    };
+
+#if RT_AO_GEN
+    // Refill (the lock held; RT_AO_GEN with AO generator records): fill up to nslots ray slots from the
+    // ring (from its head) and then the spill stack (from its top), whole records only, a generator
+    // record filling AO_SAMPLES consecutive slots.  Candidate record i is lane i's; slot `slot` (want)
+    // finds its record by a binary search over the records' first slots.  Sets the slot's ray; returns
+    // the records taken from the ring (take) and the spill stack (more).
+    auto refill_gen = [&](uint32_t head, uint32_t tail, uint32_t sl, uint32_t nslots, uint32_t slot, bool want,
+                          March<L, true>& st, uint32_t& t, uint32_t& aux, bool& live, Ctx& cl, uint32_t* more_out) {
+        const uint32_t A = (uint32_t)k->ao_samples, avail = tail - head;
+        const uint32_t ci = late(lane);
+        const bool cand = ci < avail + sl && ci < nslots; // (a record takes at least one slot)
+        float4 r1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (cand) r1 = ci < avail ? q.longs[((head + ci) % kLongRing) * kShadowRec + 1u]
+                                  : ld_rec(lspill, (sl - 1u - (ci - avail)) * kShadowRec + 1u);
+        const uint64_t gb = __ballot(cand && rec_is_gen(r1));
+        const uint32_t gens_before = lane_rank(gb);
+        const uint32_t start = ci + (A - 1u) * gens_before; // first slot of candidate ci
+        const uint32_t cnt = ((gb >> ci) & 1ull) ? A : 1u;
+        const uint64_t tb = __ballot(cand && start + cnt <= nslots);
+        const uint32_t ncand = (uint32_t)__popcll(tb); // whole records that fit (a prefix of the candidates)
+        const uint32_t take = ncand < avail ? ncand : avail;
+        *more_out = ncand - take;
+        uint32_t cc = 0;
+        for (uint32_t step = 32u; step != 0u; step >>= 1u) {
+            const uint32_t nx = cc + step;
+            const uint32_t s2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((nx & 63u) << 2), (int)start);
+            if (nx < ncand && s2 <= slot) cc = nx;
+        }
+        const uint32_t kk = slot - (uint32_t)__builtin_amdgcn_ds_bpermute((int)(cc << 2), (int)start);
+        const uint32_t ncc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(cc << 2), (int)cnt); // slots of record cc
+        if (want && cc < ncand && kk < ncc) { // (slots past the last whole record stay empty)
+            float4 q0, q1, q2;
+            if (cc < avail) {
+                const float4* r = &q.longs[((head + cc) % kLongRing) * kShadowRec];
+                q0 = r[0];
+                q1 = r[1];
+                q2 = r[2];
+            } else {
+                const uint32_t ri = (sl - 1u - (cc - avail)) * kShadowRec;
+                q0 = ld_rec(lspill, ri);
+                q1 = ld_rec(lspill, ri + 1u);
+                q2 = ld_rec(lspill, ri + 2u);
+            }
+            if (rec_is_gen(q1)) t = gen_begin<L>(c, q0, q1, q2, kk, st, &aux);
+            else t = long_unpack(q0, q1, q2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
+            const float* fr = s_fr.v[frame_of(m, t)];
+            cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
+            if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
+            live = true;
+        }
+        return take;
+    };
+#endif
 
     // the fin pool slots of finished shadow rays (idle lanes whose aux is a slot) go back to the free
     // list; the lock is held
@@ -1198,6 +1293,22 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q_lock(&q.lock, lane);
                 free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
+#if RT_AO_GEN
+                if (gen_on(k)) { // AO generator records: whole records into the idle lanes
+                    const uint32_t sl = vload(q.ls_top);
+                    uint32_t more;
+                    const bool idl = (idle >> lane) & 1ull;
+                    const uint32_t take = refill_gen(head, tail, sl, nidle, lane_rank(idle), idl, st, t, aux, live, cl, &more);
+                    if (more) __builtin_amdgcn_s_waitcnt(0);
+                    if (lane == 0) {
+                        q.l_head = head + take;
+                        q.ls_top = sl - more;
+                    }
+                    q_unlock(&q.lock, lane);
+                    goto refilled;
+                }
+#endif
+                {
                 const uint32_t take = (tail - head) < nidle ? (tail - head) : nidle;
                 // the block's spill stack tops up what the LDS ring cannot give (from its top)
                 const uint32_t sl = vload(q.ls_top);
@@ -1224,7 +1335,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     q.ls_top = sl - more;
                 }
                 q_unlock(&q.lock, lane);
+                }
             }
+#if RT_AO_GEN
+            refilled:
+#endif
             const uint64_t lv = __ballot(live);
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
@@ -1259,8 +1374,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             constexpr uint32_t LPR = kSegLanes ? kSegLanes : 8u, RPW = 64u / LPR; // (8 only to compile the discarded branch when off)
             // late(): the segment's lane values (and the octave scales derived from them) are formed
             // here, not hoisted into the kernel's prologue where they would stay live throughout
-            const uint32_t lid = late(lane);
-            const uint32_t j = lid & (LPR - 1u), grp = lid / LPR, base = lid & ~(LPR - 1u);
             March<L, true> st;
             st.d = 0.0f;
             st.iters = 0;
@@ -1270,10 +1383,15 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             cl.nz.phase = RT_PHASE_LONG;
             q_lock(&q.lock, lane);
             const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
-            const uint32_t take = (tail - head) < RPW ? (tail - head) : RPW;
+            uint32_t take = (tail - head) < RPW ? (tail - head) : RPW;
             const uint32_t sl = vload(q.ls_top);
-            const uint32_t more = sl < RPW - take ? sl : RPW - take;
-            if (grp < take + more) { // every lane of the segment unpacks the same record
+            uint32_t more = sl < RPW - take ? sl : RPW - take;
+#if RT_AO_GEN
+            if (gen_on(k)) { // AO generator records: whole records into the segments
+                take = refill_gen(head, tail, sl, RPW, late(lane) / LPR, true, st, t, aux, live, cl, &more);
+            } else
+#endif
+            if (const uint32_t grp = late(lane) / LPR; grp < take + more) { // every lane of the segment unpacks the same record
                 float4 r0, r1, r2;
                 if (grp < take) {
                     const float4* r = &q.longs[((head + grp) % kLongRing) * kShadowRec];
@@ -1298,6 +1416,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
+            const uint32_t lid = late(lane);
+            const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
             for (;;) {
                 if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
@@ -1502,6 +1622,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         // AO extension: the hit's AO rays start as long rays (fit: after its unoccluded pixel is stored,
         // which an occluded AO ray overwrites)
         if (m.fit || m.fitm) __builtin_amdgcn_s_waitcnt(0);
+#if RT_AO_GEN
+        if (gen_on(k)) { // one generator record per hit (expanded at refill)
+            push_recs(valid, [&](float4* r) { gen_pack(h, t, ao_aux, r); });
+        } else
+#endif
         for (int kk = 0; kk < k->ao_samples; ++kk) {
             March<L, true> ao;
             if (valid) ao_begin(c, h, (uint32_t)kk, ao);
@@ -1520,9 +1645,11 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // frame's CellDistance (the API's array: units compute their own cells' brackets, gate_ready)
     auto do_prepass = [&](const FrameTable* __restrict__ pft, uint32_t qt, bool own) {
         if constexpr (L == RT_NOMADPLAINS) {
-            constexpr uint32_t LPR = RT_FUSE_RAYS_PER_TASK;
-            const uint32_t f = qt / RT_FUSE_TASKS_PER_FRAME;
-            const uint32_t ray = (qt - f * RT_FUSE_TASKS_PER_FRAME) * RT_FUSE_RAYS_PER_TASK + late(lane) / LPR;
+            constexpr uint32_t LPR = RT_PREPASS_LPR, RPW = 64u / LPR; // lanes per ray, rays per wave
+            constexpr uint32_t WPF = RT_CAMERA_RES * RT_CAMERA_RES / RPW;   // waves per frame
+            const uint32_t f = qt / WPF;
+            const uint32_t ray0 = (qt - f * WPF) * RPW;
+            const uint32_t ray = ray0 + late(lane) / LPR;
             const uint32_t lid = late(lane);
             const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
             Ctx cp = c;
@@ -1558,18 +1685,25 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             }
             asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
             if (!own) {
-                if (lane == 0) __hip_atomic_fetch_add(np.ctl + 1, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) __hip_atomic_fetch_add(np.ctl + 1, RPW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 return;
             }
             typedef uint32_t __attribute__((address_space(1))) guint;
             guint* gf = (guint*)(gp.gate + f * RT_GATE_WORDS);
             uint32_t old = 0;
             if (lane == 0) {
-                const uint32_t task = qt - f * RT_FUSE_TASKS_PER_FRAME; // = ray row * 4 + ray column / 8
-                __hip_atomic_fetch_or(gf + (task >> 5), 1u << (task & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                old = __hip_atomic_fetch_add(gf + RT_GATE_CTR, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t task = ray0 / RT_FUSE_RAYS_PER_TASK; // = ray row * 4 + ray column / 8
+                // a task's last wave (its add to the task's counter returned the other waves' rays) flags it;
+                // the earlier waves' lines were acknowledged before their adds
+                bool whole = true;
+                if constexpr (RPW < RT_FUSE_RAYS_PER_TASK)
+                    whole = __hip_atomic_fetch_add(gf + RT_GATE_TASKS + task, RPW, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) == RT_FUSE_RAYS_PER_TASK - RPW;
+                if (whole) {
+                    __hip_atomic_fetch_or(gf + (task >> 5), 1u << (task & 31u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    old = __hip_atomic_fetch_add(gf + RT_GATE_CTR, (uint32_t)RT_FUSE_RAYS_PER_TASK, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             if ((uint32_t)__builtin_amdgcn_readfirstlane(old) == RT_CAMERA_RES * RT_CAMERA_RES - RT_FUSE_RAYS_PER_TASK) {
                 // the frame's last task (its add returned last): every ray is in.  Its CellDistance (8-B sc1
@@ -1768,6 +1902,16 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                         break;
                     }
                 }
+#if RT_FBM_EXIT
+                if constexpr (L == RT_NOMADPLAINS) {
+                    if (lv) { // exact unless the march provably continues after this sample (RT_FBM_EXIT)
+                        const float ns = st.step * k->step_factor;
+                        const bool allow = st.dist + ns < RT_CAMERA_FAR && ns > k->min_limit &&
+                                           !(max_steps > 0 && st.iters + 1 >= max_steps);
+                        march_step_with<L, true, false>(cf, st, [&](f3 q) { return density_nomadplains_x(cf, q, allow); });
+                    }
+                } else
+#endif
                 if (lv) march_step<L, true, false>(cf, st);
                 if (it == 96u) __builtin_amdgcn_s_setprio(1);
                 else if (it == 224u) __builtin_amdgcn_s_setprio(2);
@@ -1832,14 +1976,25 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     bool first_unit = true;
     bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
     bool gp_open = gp.tasks != 0u; // this batch's own prepass tasks may remain (GatedPrepass)
+#if RT_GATE_STATIC
+    uint32_t gp_next = first_qi;
+#endif
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
         if constexpr (L == RT_NOMADPLAINS) {
             // the gated launch: this batch's own prepass before anything else (every unit waits for some
             // of its rays).  Tasks are taken by resident waves, so every taken task finishes.
             if (gp_open) {
+#if RT_GATE_STATIC
+                // static: the wave's tasks are its first-unit index and every n_static-th after it, so the
+                // first ones go to wave 0 of each block in the order the blocks start, then wave 1, ...: one
+                // task wave per SIMD (the standalone prepass's shape) instead of the first blocks' 16 waves
+                const uint32_t qt = gp_next;
+                gp_next += n_static;
+#else
                 const uint32_t qt = wave_fetch(&counters[RT_CTR_GATE], lane);
-                if (qt < gp.tasks) {
+#endif
+                if (qt < gp.tasks * kPrepassSplit) {
                     WT(const unsigned long long tp = __builtin_amdgcn_s_memrealtime();)
                     do_prepass(ft, qt, true);
                     WT(const unsigned long long tq = __builtin_amdgcn_s_memrealtime(); wt[21] += tq - tp; wt[22] = tq;)
@@ -1851,7 +2006,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             // A wave leaves only after it found no task left, so every task is taken by a resident wave.
             if (np_open && !first_unit) {
                 const uint32_t qt = wave_fetch(np.ctl, lane);
-                if (qt < np.tasks) {
+                if (qt < np.tasks * kPrepassSplit) {
                     do_prepass(np.ft, qt, false);
                     continue;
                 }

@@ -392,6 +392,82 @@ __device__ __forceinline__ float density_nomadplains(const Ctx& c, f3 p)
     return d + s;
 }
 
+#if RT_FBM_EXIT
+// (A/B build, rt_variants.h RT_FBM_EXIT) density_nomadplains with an exact early exit.  d = -y + F(s) + G
+// with F(s) = pow(|30 s + 1| 35, expo) and G (terraces + floor lift) independent of the FBM sum s.  After
+// K octaves the rest add at most B (P[n] - P[K]) in magnitude (P: the octave weights' prefix sums, the
+// LDS octave table's w column; B = kNoiseBound >= max |noise3d| for the {-1,0,1} edge gradients).  If
+// every s in that interval gives d in [-5 + m, -m] (m: rounding margin), the march takes the no-hit
+// unit step whatever the exact d is (stepmult = 1 + pow(0, df) = 1), so the sample returns -2.5 in
+// place of d.  `allow` false (the march could exit after this sample) keeps the sample exact; the
+// exact path is density_nomadplains's operation sequence, bit for bit.
+constexpr float kNoiseBound = 1.05f; // grid maximum 1.0364 of sum_c w_c (two largest |f - c|), + slack
+// octaves from LDS table address op up to (not including) oe, as np_fbm's loop
+template <bool FAST>
+__device__ __forceinline__ float fbm_range(const Ctx& c, f3 q0, uint32_t op, uint32_t oe, float s)
+{
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const volatile v4f lds_f4;
+    #pragma unroll 1
+    do {
+        const v4f oc = *(lds_f4*)(uintptr_t)op;
+        count_noise(c.nz);
+        s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * oc.x, q0.y * oc.y, q0.z * oc.x)), oc.z, s);
+        op += 16u;
+        asm("" : "+v"(op));
+    } while (op != oe);
+    return s;
+}
+__device__ __forceinline__ float density_nomadplains_x(const Ctx& c, f3 p, bool allow)
+{
+    constexpr int K = RT_FBM_EXIT;
+    float d = -p.y;
+    f3 p1 = rtm::scale(p, 0.4f);
+    f3 q0 = rtm::scale(p1, 0.006f);
+    const int n_oct = np_octaves(c, p);
+    const float qm = rtm::max(rtm::max(rtm::abs(q0.x), rtm::abs(q0.y)), rtm::abs(q0.z));
+    const bool fast = !__ballot(!(qm * c.nz.oct[n_oct].x < kFastCellRange));
+    count_noise(c.nz);
+    const float sn = fast ? noise3d_z0<true>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f)
+                          : noise3d_z0<false>(c.nz, p1.x * 0.007138f, p1.z * 0.007138f);
+    const float steep = rtm::sat((sn - 0.2f) * 6.0f) * 7.5f;
+    const float lb = rtm::sat((-p1.y + 10.0f) * 1.6f);
+    const float lift = __ballot(lb != 0.0f) ? rtm::pow_nonneg(lb, 1.5f) : 0.0f;
+    uint32_t op = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float4*)(c.nz.oct + 1);
+    asm volatile("" : "+v"(op));
+    const int k1 = n_oct < K ? n_oct : K;
+    const uint32_t o1 = op + (uint32_t)k1 * 16u, oe = op + (uint32_t)n_oct * 16u;
+    float s = 0.0f;
+    s = fast ? fbm_range<true>(c, q0, op, o1, s) : fbm_range<false>(c, q0, op, o1, s);
+    op = o1;
+    bool skip = false;
+    const bool cand = allow && n_oct > K;
+    if (__ballot(cand)) {
+        const float G = fma(lift, 19.0f, terraces(0.0f, p1.y, steep));
+        if (cand) {
+            const float m = 0.01f + 1e-5f * rtm::abs(p.y);
+            const float f_hi_ok = p.y - G - m, f_lo_ok = p.y - G - 5.0f + m; // d <= -m, d >= -5 + m
+            const float P = c.nz.oct[n_oct].w - c.nz.oct[K].w;
+            const float R = kNoiseBound * P * 1.0001f + 1e-6f * (rtm::abs(s) + 1.0f);
+            const float u_lo = fma(s - R, 30.0f, 1.0f), u_hi = fma(s + R, 30.0f, 1.0f);
+            const float a_lo = u_lo >= 0.0f ? u_lo : (u_hi <= 0.0f ? -u_hi : 0.0f);
+            const float a_hi = rtm::max(-u_lo, u_hi);
+            const float F_lo = rtm::pow_nonneg(a_lo * 35.0f, c.k->np_expo) * (1.0f - 1e-5f);
+            const float F_hi = rtm::pow_nonneg(a_hi * 35.0f, c.k->np_expo) * (1.0f + 1e-5f);
+            skip = F_lo >= f_lo_ok && F_hi <= f_hi_ok;
+        }
+    }
+    if (!skip && n_oct > k1) {
+        s = fast ? fbm_range<true>(c, q0, op, oe, s) : fbm_range<false>(c, q0, op, oe, s);
+    }
+    if (skip) return -2.5f;
+    s = rtm::pow_nonneg(rtm::abs(fma(s, 30.0f, 1.0f)) * 35.0f, c.k->np_expo);
+    s = terraces(s, p1.y, steep);
+    s = fma(lift, 19.0f, s);
+    return d + s;
+}
+#endif
+
 // density_nomadplains with the FBM spread over a segment of LPR lanes that march ONE
 // ray together (the camerarays prepass: 1024 latency-bound rays for 256 CUs).  The 18 noise values of a sample are numbered
 // v = 0 (the steep noise) and v = N (octave N = 1..17); lane j of the segment evaluates

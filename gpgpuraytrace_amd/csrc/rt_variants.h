@@ -12,6 +12,11 @@
 #ifndef RT_REFILL_IDLE
 #define RT_REFILL_IDLE 4
 #endif
+// the gated launch's prepass tasks: 1 = each wave's by its first-unit index (spread one wave per SIMD in
+// block start order), 0 = taken from a counter by whichever waves come first
+#ifndef RT_GATE_STATIC
+#define RT_GATE_STATIC 1
+#endif
 // queued long rays that make a wave switch to them
 #ifndef RT_LONG_BATCH
 #define RT_LONG_BATCH 128
@@ -73,6 +78,18 @@
 // (batch-wide below kOrderBatchUnitsPerWave units per wave slot)
 #ifndef RT_ORDER_BATCH
 #define RT_ORDER_BATCH -1
+#endif
+
+// AO generator records (AO_SAMPLES >= 2): a hit's AO rays as one ring record expanded at refill
+#ifndef RT_AO_GEN
+#define RT_AO_GEN 0
+#endif
+// RT_FBM_EXIT=K (A/B only, 0 in the product): the exact FBM early exit of the primary march.  After K
+// octaves a sample whose density provably stays in the unit-step no-hit band [-5, 0) (the remaining
+// octaves' amplitude bound from the LDS octave table's prefix column) skips the
+// rest; a sample after which the march could exit is always exact.  profiles/r05/fbm_exit_ab.md.
+#ifndef RT_FBM_EXIT
+#define RT_FBM_EXIT 0
 #endif
 
 // ---- diagnostic builds (never in the product) ------------------------------------------------

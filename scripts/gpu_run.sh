@@ -8,6 +8,9 @@
 #   r4bench[=<args>]             the same command on the round-4 snapshot in _ab/r4 (same-box A/B)
 #   ab=<args>                    bench.py --no-cpu-baseline --traffic off --no-companions <args>: one line
 #   r4ab=<args>                  the same on the round-4 snapshot
+#   vtests=<variant>:<-k expr>  the GPU tests (-k) against an A/B build
+#   vbench=<variant>:<args>      bench.py against the A/B build _build/librt_hip_<variant>.so
+#   ibench=<args>                bench.py with RT_BENCH_PREPASS_INLINE=1 (the prepass as its own launch)
 #   sim=<batch_shard_sim args>   scripts/batch_shard_sim.py
 #   prof=<bench.py args>         rocprofv3 --kernel-trace --stats over bench.py -> prof<i>/
 #   py=<script and args>         any python script of the repo (diagnostics)
@@ -38,11 +41,22 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u -m pytest tests -m gpu $x -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$out/tests$i.log" 2>&1 || { tail -40 "$out/tests$i.log"; exit 1; }
       tail -1 "$out/tests$i.log";;
+    vtests)  # vtests=<variant>:<pytest -k expr>: the GPU tests against an A/B build
+      v=${arg%%:*}; k=${arg#*:}
+      RT_LIB_VARIANT=$v timeout -k 10 900 python3 -u scripts/with_variant.py -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread -k "$k" > "$out/tests$i.log" 2>&1 || { tail -40 "$out/tests$i.log"; exit 1; }
+      tail -1 "$out/tests$i.log";;
     bench|r4bench|ab|r4ab)
       dir=.; [ "${kind:0:2}" = r4 ] && dir=_ab/r4
       extra=""; [ "${kind#r4}" = ab ] && extra="--no-cpu-baseline --traffic off --no-companions"
       (cd $dir && timeout -k 10 600 python3 bench.py $extra $arg) > "$out/bench$i.json" 2> "$out/bench$i.err" \
         || { tail -20 "$out/bench$i.err"; exit 1; }
+      summ "$step" "$out/bench$i.json";;
+    vbench|ibench)  # vbench=<variant>:<bench args> (an A/B build); ibench=<args>: RT_BENCH_PREPASS_INLINE=1
+      if [ $kind = vbench ]; then v=${arg%%:*}; rest=${arg#*:}; else v=; rest=$arg; fi
+      inl=0; [ $kind = ibench ] && inl=1
+      RT_BENCH_PREPASS_INLINE=$inl RT_LIB_VARIANT=$v timeout -k 10 600 python3 scripts/with_variant.py bench.py $rest \
+        > "$out/bench$i.json" 2> "$out/bench$i.err" || { tail -20 "$out/bench$i.err"; exit 1; }
       summ "$step" "$out/bench$i.json";;
     sim)
       timeout -k 10 600 python3 scripts/batch_shard_sim.py $arg > "$out/sim$i.log" 2>&1 || { tail -20 "$out/sim$i.log"; exit 1; }
