@@ -52,9 +52,9 @@ sys.path.insert(0, ROOT)
 # (RT_BENCH_HW_QUEUES overrides the count for A/B runs)
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_BENCH_HW_QUEUES", "8")
 
-# A/B runs only: RT_BENCH_PREPASS_INLINE=1 renders with RT_DEVICE_PREPASS_INLINE (the prepass as its own launch
-# before the trace, the ABI <= 6 sequence) instead of the default gated launch
-PREPASS_INLINE = os.environ.get("RT_BENCH_PREPASS_INLINE") == "1"
+# A/B runs only: RT_BENCH_GATED=1 renders with RT_DEVICE_GATED (the gated launch: the prepass inside the trace
+# kernel) instead of the default prepass launch before the trace
+GATED = os.environ.get("RT_BENCH_GATED") == "1"
 METRIC = "Mray/s + ms/frame at 1920×1080, 1/2/4/8 MI355X; % HBM roofline"
 FLOPS_PER_NOISE3D = 88          # algorithmic work unit
 PEAK_FP32_VECTOR_TFLOPS = 157.3 # MI355X_MICROARCH.md chip table (vector FP32, = FP32 MFMA dense)
@@ -72,7 +72,7 @@ CONFIGS = {
     "ref": {"width": 1920, "height": 1080, "max_steps": 0, "ao": 0, "cpu_rows": 1, "cpu_rows_1t": 16,
             "name": "1920x1080, reference semantics (uncapped march, shadow, no AO)"},
 }
-TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_finish (the gated launch: the prepass runs inside k_trace)"
+TRACESCREEN_KERNELS = "tracescreen = k_order + k_trace + k_finish"
 
 
 def parse():
@@ -229,7 +229,7 @@ def traffic_child(a):
     from gpgpuraytrace_amd import engine as E
     euler = G.camera.INITIAL_ROTATION_EULER if a.pose == "reset" else G.camera.LOOKDOWN_ROTATION_EULER
     B = max(1, min(24, a.batch))
-    ring = E.FrameRing(a.width, a.height, prepass_inline=PREPASS_INLINE, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
+    ring = E.FrameRing(a.width, a.height, gated=GATED, depth=1, theme=a.landscape, camera=G.Camera(a.width, a.height, euler=euler),
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     for _ in range(2):
         ring.render_batch()
@@ -367,7 +367,7 @@ def main():
 
     def make(stats, max_steps=a.max_steps, ao=a.ao, float_output=False):
         dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, gpu=local, stats=stats, float_output=float_output,
-                                        prepass_inline=PREPASS_INLINE)
+                                        gated=GATED)
         if dev is None:
             raise RuntimeError("device create failed: " + G.lib().rt_last_error().decode())
         ter = G.Terrain(dev, a.landscape, max_steps=max_steps, ao_samples=ao)
@@ -431,7 +431,7 @@ def main():
 
     # --- timed: batches of B frames, D batches in flight (FrameRing slot groups) ---
     camera = G.Camera(W, H, euler=euler)
-    ring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+    ring = E.FrameRing(W, H, gated=GATED, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                        time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, graph=bool(a.graph), batch=B)
     plan = P.BatchPlan(W, H, B, world, split_prepass=a.split_prepass, lookahead=a.lookahead,
                        direct_pack=bool(a.direct_pack))
@@ -652,7 +652,7 @@ def main():
         # B = 1 with three frames in flight (D3D11's default maximum frame latency, the reference
         # frame loop's own queue depth): each frame is its own prepass -> k_order -> k_trace ->
         # k_finish on its slot's stream, and the next frame's prepass overlaps this one's tail
-        sring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
+        sring = E.FrameRing(W, H, gated=GATED, depth=3, gpu=local, theme=a.landscape, camera=camera, time_of_day=0.3,
                             max_steps=a.max_steps, ao_samples=a.ao, batch=1, lookahead=True)
         for i in range(sring.depth + 1):
             sring.render_batch(ahead=i < sring.depth)
@@ -678,7 +678,7 @@ def main():
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)
-        rring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        rring = E.FrameRing(W, H, gated=GATED, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=0, ao_samples=0, batch=B, lookahead=bool(a.lookahead))
         for i in range(rring.depth + 1):
             rring.render_batch(ahead=i < rring.depth)
@@ -712,7 +712,7 @@ def main():
             if i + 1 == len(path):
                 want_last = cdev.readback()
         cdev.destroy()
-        mring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        mring = E.FrameRing(W, H, gated=GATED, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
 
         def path_batch(first, n):
@@ -742,7 +742,7 @@ def main():
         # sustained rate: the timed loop's batches back to back for ~--sustained-s seconds (clocks and
         # power under a long load), a HIP event after every batch on its stream, read once at the end
         n_sus = max(2, int(a.sustained_s * 1e3 / (elapsed / a.steps * 1e3 * B) + 0.5))
-        uring = E.FrameRing(W, H, prepass_inline=PREPASS_INLINE, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
+        uring = E.FrameRing(W, H, gated=GATED, depth=a.frames_in_flight, gpu=local, theme=a.landscape, camera=camera,
                             time_of_day=0.3, max_steps=a.max_steps, ao_samples=a.ao, batch=B)
         for _ in range(uring.depth + 1):
             uring.render_batch()
@@ -786,9 +786,9 @@ def main():
 
     ms_per_frame = elapsed / a.steps * 1e3
     value = rays_per_frame * a.steps / elapsed / 1e6
-    # the timed launch's noise3d: tracescreen's, plus (the gated launch, the default for nomadplains) the
-    # batch's prepass rays, which run inside the same trace kernel
-    gated = not PREPASS_INLINE and a.landscape == "nomadplains"
+    # the timed launch's noise3d: tracescreen's, plus (RT_BENCH_GATED=1: the gated launch, nomadplains) the
+    # batch's prepass rays, which then run inside the same trace kernel
+    gated = GATED and a.landscape == "nomadplains"
     batch_noise = counts["batch_noise"] + (counts["prepass_noise"] if gated else 0)
     achieved = batch_noise * FLOPS_PER_NOISE3D / (k_avg_ms * 1e-3) / 1e12
     traffic, traffic_how = None, "not measured (N>1: a rank's launch traces a shard; or --traffic off)"
@@ -850,7 +850,7 @@ def main():
                 "frac": round(achieved / PEAK_FP32_VECTOR_TFLOPS, 4), "traffic": traffic,
                 "traffic_how": traffic_how,
                 **({"traffic_per_frame_vs_rgba8": round(traffic / B / (W * H * 4), 2)} if traffic else {}),
-                "kernel": TRACESCREEN_KERNELS, "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
+                "kernel": TRACESCREEN_KERNELS + (" (the gated launch: the prepass runs inside k_trace)" if gated else ""), "kernel_avg_ms": round(k_avg_ms, 4), "kernel_launches": kn,
                 "timing": "HIP events per launch on its stream, one batch in flight (the last "
                           f"{kn} tracescreen launches of the run; one launch = {B} frames)",
                 "work_unit": f"{FLOPS_PER_NOISE3D} FP32 flop per noise3d x {batch_noise} noise3d per launch ({B} "

@@ -19,7 +19,7 @@ RT_DEVICE_STATS = 2
 RT_DEVICE_GRAPH = 4
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
 RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the next batch's prepass tasks (timeout test)
-RT_DEVICE_PREPASS_INLINE = 128  # ABI 7: the prepass as its own launch before the trace (the ABI <= 6 sequence)
+RT_DEVICE_GATED = 128  # ABI 7 (opt-in): the prepass inside the trace kernel, units gated on their cells' rays
 ABI_VERSION = 7  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3

@@ -30,9 +30,9 @@ struct FrameTable {
 };
 
 // The NEXT batch's camerarays prepass fused into this batch's k_trace (nomadplains):
-// `tasks` tasks of 8 rays (8 lanes per ray) of the frames of `ft` (their camerarays constant blocks
-// kcam, their CameraResults cam), taken from ctl[0]; a finished task stores its rays' CameraResults
-// (one whole 128-B line, sc1) and adds 8 to ctl[1]; that batch's k_order waits for ctl[1] to reach
+// `tasks` tasks of 8 rays (RT_PREPASS_LPR lanes per ray) of the frames of `ft` (their camerarays constant
+// blocks kcam, their CameraResults cam), taken from ctl[0]; a finished wave stores its rays' CameraResults
+// (sc1; one whole 128-B line per 8-ray wave) and adds its rays to ctl[1]; that batch's k_order waits for ctl[1] to reach
 // its rays (frames x 1024) before it reads them.  tasks == 0: none.
 #define RT_FUSE_RAYS_PER_TASK 8
 #define RT_FUSE_TASKS_PER_FRAME (RT_CAMERA_RES * RT_CAMERA_RES / RT_FUSE_RAYS_PER_TASK)
@@ -56,9 +56,11 @@ struct FusedPrepass {
 #define RT_GATE_CTR 32    // their own, the per-task wave counters (words 128-255)
 #define RT_GATE_TASKS 128
 // lanes per prepass ray in k_trace's prepass tasks (a task's 8 rays are marched by 8 / (64 / LPR) waves):
-// 32 lanes = one round of the 18 octave values per step (the standalone camerarays' shape)
+// 8 = one wave per task, 3 rounds of the 18 octave values per step.  32 (one round, 4 waves per task) was
+// measured slower inside k_trace: the rays' latency there is set by the units sharing their SIMDs
+// (profiles/r05/gated_ab.md)
 #ifndef RT_PREPASS_LPR
-#define RT_PREPASS_LPR 32
+#define RT_PREPASS_LPR 8
 #endif
 struct GatedPrepass {
     uint32_t* gate;   // RT_MAX_BATCH x RT_GATE_WORDS

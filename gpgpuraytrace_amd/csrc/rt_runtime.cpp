@@ -755,7 +755,7 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
     const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS |
-                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_PREPASS_INLINE;
+                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED;
     if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -1552,15 +1552,16 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
         }
         la_scr.packed = 1;
     }
-    // The gated launch (GatedPrepass): a full nomadplains render runs its prepass
-    // inside its own k_trace, and each unit starts once the prepass rays its cells read are in, instead of
-    // a latency-bound prepass launch the whole trace waits for.  Not for the instrumented kernels (their
-    // prepass counts stay separate), the camera feed (it wants the CameraResults before the trace), a
-    // trace from gathered CameraResults, a fused prepass, or RT_DEVICE_PREPASS_INLINE.
+    // The gated launch (GatedPrepass; opt-in, RT_DEVICE_GATED): a full nomadplains
+    // render runs its prepass inside its own k_trace, and each unit starts once the prepass rays its cells
+    // read are in, instead of a latency-bound prepass launch the whole trace waits for.  Measured slower
+    // (the prepass rays march 2-3x slower beside the units), so off by default.  Not for the instrumented
+    // kernels (their prepass counts stay separate), the camera feed (it wants the CameraResults before the
+    // trace), a trace from gathered CameraResults or a fused prepass.
     const bool gated = phases == (PH_PRE | PH_TRACE) && !feed && !camera_in &&
                        (!fuse || (fuse->wait_ctl == nullptr && fuse->next.ctl == nullptr)) &&
                        b.s0->landscape == RT_NOMADPLAINS &&
-                       !(dev->flags & (RT_DEVICE_STATS | RT_DEVICE_PREPASS_INLINE));
+                       (dev->flags & RT_DEVICE_GATED) && !(dev->flags & RT_DEVICE_STATS);
     if (gated) la_scr.gated = GatedPrepass{dev->gate, dev->claims, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
     // rt_terrain_prepass_ahead: ev_order follows the last read of the frames' CameraResults -- k_order's,
     // or with the gated launch k_trace's (recorded after the trace below)

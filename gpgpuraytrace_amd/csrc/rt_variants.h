@@ -12,10 +12,14 @@
 #ifndef RT_REFILL_IDLE
 #define RT_REFILL_IDLE 4
 #endif
-// the gated launch's prepass tasks: 1 = each wave's by its first-unit index (spread one wave per SIMD in
-// block start order), 0 = taken from a counter by whichever waves come first
+// the gated launch's prepass tasks: 0 = taken from a counter by whichever waves come first, 1 = each wave's by
+// its first-unit index (one task wave per SIMD in block start order; measured slower: profiles/r05/gated_ab.md)
 #ifndef RT_GATE_STATIC
-#define RT_GATE_STATIC 1
+#define RT_GATE_STATIC 0
+#endif
+// the gated launch: s_sleep argument (x 64 cycles) of a wave whose tile scan step found nothing ready
+#ifndef RT_GATE_SLEEP
+#define RT_GATE_SLEEP 0
 #endif
 // queued long rays that make a wave switch to them
 #ifndef RT_LONG_BATCH

@@ -160,20 +160,20 @@ class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
     def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False,
-                 debug_withhold_fuse=False, prepass_inline=False):
+                 debug_withhold_fuse=False, gated=False):
         """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
         entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
         shadows the fin[t] fallback; same bits).  debug_withhold_fuse: diagnostic
         RT_DEVICE_DEBUG_WITHHOLD_FUSE (a trace this device leads runs none of the next batch's fused
-        prepass tasks, so that batch's wait times out: the fail-safe's test).  prepass_inline:
-        RT_DEVICE_PREPASS_INLINE (the prepass as its own launch before the trace, instead of the gated
-        launch that runs it inside the trace kernel; same bits)."""
+        prepass tasks, so that batch's wait times out: the fail-safe's test).  gated:
+        RT_DEVICE_GATED (the gated launch: the prepass inside the trace kernel instead of its own launch
+        before it; same bits, measured slower)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
                       | (_native.RT_DEVICE_GRAPH if graph else 0)
                       | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0)
                       | (_native.RT_DEVICE_DEBUG_WITHHOLD_FUSE if debug_withhold_fuse else 0)
-                      | (_native.RT_DEVICE_PREPASS_INLINE if prepass_inline else 0))
+                      | (_native.RT_DEVICE_GATED if gated else 0))
         self._h = None
 
     def create(self):
@@ -655,7 +655,7 @@ class FrameRing:
     that call (a camera written after it makes the next batch prepass again, in line)."""
 
     def __init__(self, width, height, depth=3, gpu=0, theme="nomadplains", camera=None, time_of_day=0.3,
-                 graph=False, batch=1, float_output=False, lookahead=False, prepass_inline=False, **terrain_kw):
+                 graph=False, batch=1, float_output=False, lookahead=False, gated=False, **terrain_kw):
         self.depth, self.frame, self.batch = int(depth), 0, int(batch)
         if lookahead and graph:
             raise ValueError("lookahead runs the prepass on a side stream: not with graph=True")
@@ -673,7 +673,7 @@ class FrameRing:
         self.slots = []
         for _ in range(self.depth * self.batch):
             dev = DeviceFactory.construct(DeviceAPI.HIP, width, height, gpu=gpu, graph=graph,
-                                          float_output=float_output, prepass_inline=prepass_inline)
+                                          float_output=float_output, gated=gated)
             if dev is None:
                 raise RuntimeError("device create failed: " + lib().rt_last_error().decode())
             ter = Terrain(dev, theme, **terrain_kw)

@@ -49,7 +49,7 @@ enum {
      * rt_device_create rejects them, as every unknown flag */
     RT_DEVICE_DEBUG_SMALL_RINGS = 32u,
     RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64u,
-    RT_DEVICE_PREPASS_INLINE = 128u
+    RT_DEVICE_GATED = 128u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
@@ -59,13 +59,13 @@ enum {
  * 64 entries instead of 570 and its fin pool 8 slots instead of 1536, so queued long rays take the
  * per-block spill rings in HBM and most long shadows the fin[t] fallback (the parity tests run
  * frames through those paths); same bits, slower.
- * RT_DEVICE_PREPASS_INLINE (ABI 7): renders this device leads run the camerarays prepass as its own launch,
- * followed by setTargetDepths (k_order) and the trace -- the sequence of ABI <= 6.  By default (ABI 7) a
- * full nomadplains render (rt_terrain_render / _batch, not the camera feed, not the instrumented
- * RT_DEVICE_STATS kernels) is ONE gated launch: the trace kernel runs the batch's prepass rays first and
- * starts each 8x8 unit as soon as the prepass rays its cells' setTargetDepths reads are in, so units no
- * longer wait for the slowest prepass ray; the frame's last prepass task writes its CellDistance.  Same
- * bits either way (frames, CameraResults, CellDistance).
+ * RT_DEVICE_GATED (ABI 7, opt-in): a full nomadplains render this device leads (rt_terrain_render /
+ * _batch, not the camera feed, not the instrumented RT_DEVICE_STATS kernels) is ONE gated launch: the
+ * trace kernel runs the batch's prepass rays first and starts each 8x8 unit as soon as the prepass rays
+ * its cells' setTargetDepths reads are in; the frame's last prepass task writes its CellDistance.  Same
+ * bits as the default sequence (the camerarays prepass as its own launch, then setTargetDepths and the
+ * trace).  Measured slower on MI355X (prepass rays that share their SIMDs with
+ * units march 2-3x slower than alone), so it is not the default.
  * RT_DEVICE_DEBUG_WITHHOLD_FUSE (ABI 7, diagnostic): a trace this device leads that would run the next
  * batch's fused prepass (rt_terrain_trace_ahead) runs none of its tasks, so that batch's bounded wait
  * times out: the fail-safe's test (rt_device_check below). */

@@ -10,7 +10,7 @@
 #   r4ab=<args>                  the same on the round-4 snapshot
 #   vtests=<variant>:<-k expr>  the GPU tests (-k) against an A/B build
 #   vbench=<variant>:<args>      bench.py against the A/B build _build/librt_hip_<variant>.so
-#   ibench=<args>                bench.py with RT_BENCH_PREPASS_INLINE=1 (the prepass as its own launch)
+#   gbench=<args>                bench.py with RT_BENCH_GATED=1 (the gated launch: the prepass inside k_trace)
 #   sim=<batch_shard_sim args>   scripts/batch_shard_sim.py
 #   prof=<bench.py args>         rocprofv3 --kernel-trace --stats over bench.py -> prof<i>/
 #   py=<script and args>         any python script of the repo (diagnostics)
@@ -52,10 +52,10 @@ for step in "$@"; do
       (cd $dir && timeout -k 10 600 python3 bench.py $extra $arg) > "$out/bench$i.json" 2> "$out/bench$i.err" \
         || { tail -20 "$out/bench$i.err"; exit 1; }
       summ "$step" "$out/bench$i.json";;
-    vbench|ibench)  # vbench=<variant>:<bench args> (an A/B build); ibench=<args>: RT_BENCH_PREPASS_INLINE=1
+    vbench|gbench)  # vbench=<variant>:<bench args> (an A/B build); gbench=<args>: RT_BENCH_GATED=1
       if [ $kind = vbench ]; then v=${arg%%:*}; rest=${arg#*:}; else v=; rest=$arg; fi
-      inl=0; [ $kind = ibench ] && inl=1
-      RT_BENCH_PREPASS_INLINE=$inl RT_LIB_VARIANT=$v timeout -k 10 600 python3 scripts/with_variant.py bench.py $rest \
+      gt=0; [ $kind = gbench ] && gt=1
+      RT_BENCH_GATED=$gt RT_LIB_VARIANT=$v timeout -k 10 600 python3 scripts/with_variant.py bench.py $rest \
         > "$out/bench$i.json" 2> "$out/bench$i.err" || { tail -20 "$out/bench$i.err"; exit 1; }
       summ "$step" "$out/bench$i.json";;
     sim)

@@ -31,12 +31,12 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         ao=0, graph=False, small_rings=False, float_output=True):
+         ao=0, graph=False, small_rings=False, float_output=True, gated=False):
     """float_output=False: the product's device (RGBA8 only), where one sample per pixel with at most one
     AO ray finishes hit pixels in k_trace (UnitMap::fit) instead of through per-sample colours."""
     import gpgpuraytrace_amd as G
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=float_output,
-                                    stats=stats, graph=graph, small_rings=small_rings)
+                                    stats=stats, graph=graph, small_rings=small_rings, gated=gated)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -547,10 +547,10 @@ def test_shard_batch_pack_unpack_roundtrip(w, h, world, frames):
 
 
 @pytest.mark.parametrize("w,h,world,frames,pose,ao,land", [
-    (1920, 1080, 8, 3, "reset", 1, "nomadplains"),    # the bench's C3 shard: fit + k_finish, gated launch
+    (1920, 1080, 8, 3, "reset", 1, "nomadplains"),    # the bench's C3 shard: fit + k_finish
     (64, 48, 3, 4, "lookdown", 4, "nomadplains"),     # fitm (AO slots + colour pool), ragged shards
     (64, 48, 2, 2, "reset", 0, "nomadplains"),        # fit with no k_finish
-    (48, 32, 3, 3, "reset", 2, "greenrocks"),         # fog live, the separate prepass launch
+    (48, 32, 3, 3, "reset", 2, "greenrocks"),         # fog live
 ])
 def test_render_batch_packed_equals_render_then_pack(w, h, world, frames, pose, ao, land):
     """rt_terrain_render_batch_packed (ABI 7, parallel.run_batch's direct pack): every rank's shards
@@ -1479,18 +1479,18 @@ GATED_SPECS = [GI.FRAMES[0], GI.FRAMES[1], GI.FRAMES[2], GI.FRAMES[3], GI.FRAMES
 @pytest.mark.parametrize("float_output", [True, False], ids=["f32", "rgba8"])
 @pytest.mark.parametrize("spec", GATED_SPECS, ids=[GI.frame_key(*s) for s in GATED_SPECS])
 def test_gated_launch_golden(spec, float_output):
-    """The default render of a nomadplains frame is ONE gated launch (rt_device_info): k_trace runs the
+    """With RT_DEVICE_GATED a render of a nomadplains frame is ONE gated launch (rt_device_info): k_trace runs the
     1024 prepass rays as 8-ray tasks, each unit starts once its cells' 5x5 prepass rays have flagged and
     derives its cells' setTargetDepths bracket from them, the frame's last task writes CellDistance.
     The unit order comes from the PREVIOUS CellDistance, poisoned here with NaN / inf / garbage: frames,
     CameraResults and CellDistance still equal the golden ones; a second frame (a real previous order)
-    too; and the RT_DEVICE_PREPASS_INLINE device (ABI <= 6 sequence) gives the same bits."""
+    too; and the default device (the prepass as its own launch) gives the same bits."""
     import gpgpuraytrace_amd as G
     gold = GI.load()
     land, pose, w, h, aa, ms, ao = GI.unpack(spec)
     key = GI.frame_key(*spec)
     consts = GI.consts(w, h, pose)
-    dev, ter = make(consts, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output)
+    dev, ter = make(consts, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, gated=True)
     rng = np.random.default_rng(7)
     junk = rng.uniform(-1e3, 1e3, (1024, 2)).astype(np.float32)
     junk[::7] = np.nan
@@ -1508,7 +1508,7 @@ def test_gated_launch_golden(spec, float_output):
         assert np.array_equal(ter.camera_view, gold[key + "_camera_results"]), rep
     dev.check()
     dev.destroy()
-    idev = G.DeviceFactory.construct(G.DeviceAPI.HIP, w, h, float_output=float_output, prepass_inline=True)
+    idev = G.DeviceFactory.construct(G.DeviceAPI.HIP, w, h, float_output=float_output)
     iter_ = G.Terrain(idev, land, aa_samples=aa, max_steps=ms, ao_samples=ao)
     iter_.create()
     assert iter_.reload()
@@ -1535,7 +1535,7 @@ def test_gated_launch_c3_batch_rows():
     for c in cams:
         rgba, rgba8, cr, cd, _ = O.render_rows(nz, O.make_frame(c, max_steps=512, ao=1, rows=rows, threads=0))
         refs.append((rgba8, cr, cd))
-    pairs = [make(c, max_steps=512, ao=1, float_output=False) for c in cams]
+    pairs = [make(c, max_steps=512, ao=1, float_output=False, gated=True) for c in cams]
     E.render_batch([t for _, t in pairs])
     for (dev, ter), (rgba8, cr, cd) in zip(pairs, refs):
         img = dev.readback()
