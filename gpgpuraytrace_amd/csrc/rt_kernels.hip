@@ -1169,58 +1169,48 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     };
 
 #if RT_AO_GEN
-    // Refill with AO generator records (RT_AO_GEN): fill up to nslots ray slots from the ring (from its head)
-    // and then the spill stack (from its top), whole records only, a generator record filling AO_SAMPLES
-    // consecutive slots.  gen_claim (the lock held): candidate record i is lane i's, loaded whole; returns
-    // the records taken from the ring (take) and the spill stack (*more).  gen_take (after the unlock): slot
-    // `slot` finds its record by a binary search over the records' first slots, fetches it from its lane
-    // and starts the ray (an AO ray of a generator, or the stored march), so the lock is not held for it.
-    struct GenCand {
-        float4 r0, r1, r2;
-        uint32_t start, cnt, ncand;
-    };
-    auto gen_claim = [&](uint32_t head, uint32_t tail, uint32_t sl, uint32_t nslots, GenCand& g, uint32_t* more) {
+    // Refill (the lock held; RT_AO_GEN with AO generator records): fill up to nslots ray slots from the
+    // ring (from its head) and then the spill stack (from its top), whole records only, a generator
+    // record filling AO_SAMPLES consecutive slots.  Candidate record i is lane i's; slot `slot` (want)
+    // finds its record by a binary search over the records' first slots.  Sets the slot's ray; returns
+    // the records taken from the ring (take) and the spill stack (more).
+    auto refill_gen = [&](uint32_t head, uint32_t tail, uint32_t sl, uint32_t nslots, uint32_t slot, bool want,
+                          March<L, true>& st, uint32_t& t, uint32_t& aux, bool& live, Ctx& cl, uint32_t* more_out) {
         const uint32_t A = (uint32_t)k->ao_samples, avail = tail - head;
         const uint32_t ci = late(lane);
         const bool cand = ci < avail + sl && ci < nslots; // (a record takes at least one slot)
-        g.r0 = g.r1 = g.r2 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (cand) {
-            if (ci < avail) {
-                const float4* r = &q.longs[((head + ci) % kLongRing) * kShadowRec];
-                g.r0 = r[0];
-                g.r1 = r[1];
-                g.r2 = r[2];
-            } else {
-                const uint32_t ri = (sl - 1u - (ci - avail)) * kShadowRec;
-                g.r0 = ld_rec(lspill, ri);
-                g.r1 = ld_rec(lspill, ri + 1u);
-                g.r2 = ld_rec(lspill, ri + 2u);
-            }
-        }
-        const uint64_t gb = __ballot(cand && rec_is_gen(g.r1));
-        g.start = ci + (A - 1u) * lane_rank(gb); // first slot of candidate ci
-        g.cnt = ((gb >> ci) & 1ull) ? A : 1u;
-        g.ncand = (uint32_t)__popcll(__ballot(cand && g.start + g.cnt <= nslots)); // whole records that fit
-        const uint32_t take = g.ncand < avail ? g.ncand : avail;
-        *more = g.ncand - take;
-        return take;
-    };
-    auto gen_take = [&](const GenCand& g, uint32_t slot, bool want, March<L, true>& st, uint32_t& t, uint32_t& aux,
-                        bool& live, Ctx& cl) {
-        auto from = [&](uint32_t src, uint32_t v) { return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v); };
-        auto fromf = [&](uint32_t src, float v) { return __uint_as_float(from(src, __float_as_uint(v))); };
+        float4 r1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (cand) r1 = ci < avail ? q.longs[((head + ci) % kLongRing) * kShadowRec + 1u]
+                                  : ld_rec(lspill, (sl - 1u - (ci - avail)) * kShadowRec + 1u);
+        const uint64_t gb = __ballot(cand && rec_is_gen(r1));
+        const uint32_t gens_before = lane_rank(gb);
+        const uint32_t start = ci + (A - 1u) * gens_before; // first slot of candidate ci
+        const uint32_t cnt = ((gb >> ci) & 1ull) ? A : 1u;
+        const uint64_t tb = __ballot(cand && start + cnt <= nslots);
+        const uint32_t ncand = (uint32_t)__popcll(tb); // whole records that fit (a prefix of the candidates)
+        const uint32_t take = ncand < avail ? ncand : avail;
+        *more_out = ncand - take;
         uint32_t cc = 0;
         for (uint32_t step = 32u; step != 0u; step >>= 1u) {
             const uint32_t nx = cc + step;
-            const uint32_t s2 = from(nx & 63u, g.start);
-            if (nx < g.ncand && s2 <= slot) cc = nx;
+            const uint32_t s2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((nx & 63u) << 2), (int)start);
+            if (nx < ncand && s2 <= slot) cc = nx;
         }
-        const uint32_t kk = slot - from(cc, g.start);
-        const bool mine = want && cc < g.ncand && kk < from(cc, g.cnt); // (slots past the last record stay empty)
-        const float4 q0 = make_float4(fromf(cc, g.r0.x), fromf(cc, g.r0.y), fromf(cc, g.r0.z), fromf(cc, g.r0.w));
-        const float4 q1 = make_float4(fromf(cc, g.r1.x), fromf(cc, g.r1.y), fromf(cc, g.r1.z), fromf(cc, g.r1.w));
-        const float4 q2 = make_float4(fromf(cc, g.r2.x), fromf(cc, g.r2.y), fromf(cc, g.r2.z), fromf(cc, g.r2.w));
-        if (mine) {
+        const uint32_t kk = slot - (uint32_t)__builtin_amdgcn_ds_bpermute((int)(cc << 2), (int)start);
+        const uint32_t ncc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(cc << 2), (int)cnt); // slots of record cc
+        if (want && cc < ncand && kk < ncc) { // (slots past the last whole record stay empty)
+            float4 q0, q1, q2;
+            if (cc < avail) {
+                const float4* r = &q.longs[((head + cc) % kLongRing) * kShadowRec];
+                q0 = r[0];
+                q1 = r[1];
+                q2 = r[2];
+            } else {
+                const uint32_t ri = (sl - 1u - (cc - avail)) * kShadowRec;
+                q0 = ld_rec(lspill, ri);
+                q1 = ld_rec(lspill, ri + 1u);
+                q2 = ld_rec(lspill, ri + 2u);
+            }
             if (rec_is_gen(q1)) t = gen_begin<L>(c, q0, q1, q2, kk, st, &aux);
             else t = long_unpack(q0, q1, q2, rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
             const float* fr = s_fr.v[frame_of(m, t)];
@@ -1228,6 +1218,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
             live = true;
         }
+        return take;
     };
 #endif
 
@@ -1306,15 +1297,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (gen_on(k)) { // AO generator records: whole records into the idle lanes
                     const uint32_t sl = vload(q.ls_top);
                     uint32_t more;
-                    GenCand g;
-                    const uint32_t take = gen_claim(head, tail, sl, nidle, g, &more);
+                    const bool idl = (idle >> lane) & 1ull;
+                    const uint32_t take = refill_gen(head, tail, sl, nidle, lane_rank(idle), idl, st, t, aux, live, cl, &more);
                     if (more) __builtin_amdgcn_s_waitcnt(0);
                     if (lane == 0) {
                         q.l_head = head + take;
                         q.ls_top = sl - more;
                     }
                     q_unlock(&q.lock, lane);
-                    gen_take(g, lane_rank(idle), (idle >> lane) & 1ull, st, t, aux, live, cl);
                     goto refilled;
                 }
 #endif
@@ -1397,9 +1387,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             const uint32_t sl = vload(q.ls_top);
             uint32_t more = sl < RPW - take ? sl : RPW - take;
 #if RT_AO_GEN
-            GenCand gc;
-            if (gen_on(k)) { // AO generator records: whole records into the segments (started after the unlock)
-                take = gen_claim(head, tail, sl, RPW, gc, &more);
+            if (gen_on(k)) { // AO generator records: whole records into the segments
+                take = refill_gen(head, tail, sl, RPW, late(lane) / LPR, true, st, t, aux, live, cl, &more);
             } else
 #endif
             if (const uint32_t grp = late(lane) / LPR; grp < take + more) { // every lane of the segment unpacks the same record
@@ -1427,9 +1416,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
-#if RT_AO_GEN
-            if (gen_on(k)) gen_take(gc, late(lane) / LPR, true, st, t, aux, live, cl);
-#endif
             const uint32_t lid = late(lane);
             const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);

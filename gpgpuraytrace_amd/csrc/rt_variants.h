@@ -84,7 +84,8 @@
 #define RT_ORDER_BATCH -1
 #endif
 
-// AO generator records (AO_SAMPLES >= 2): a hit's AO rays as one ring record expanded at refill
+// AO generator records (AO_SAMPLES >= 2): a hit's AO rays as one ring record expanded at refill (A/B only:
+// bit-exact, C5 HBM 5.9x -> 5.0x but 24% slower; profiles/r05/ao_gen_ab.md)
 #ifndef RT_AO_GEN
 #define RT_AO_GEN 0
 #endif

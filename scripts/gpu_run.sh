@@ -41,11 +41,13 @@ for step in "$@"; do
       timeout -k 10 900 python3 -u -m pytest tests -m gpu $x -v --timeout 300 --timeout-method thread "${k[@]}" \
         > "$out/tests$i.log" 2>&1 || { tail -40 "$out/tests$i.log"; exit 1; }
       tail -1 "$out/tests$i.log";;
-    vtests)  # vtests=<variant>:<pytest -k expr>: the GPU tests against an A/B build
+    vtests|vtestsc)  # vtests=<variant>:<pytest -k expr>: the GPU tests against an A/B build (vtestsc: a test
+                     # failure does not end the call; a timeout or crash still does)
       v=${arg%%:*}; k=${arg#*:}
       RT_LIB_VARIANT=$v timeout -k 10 900 python3 -u scripts/with_variant.py -m pytest tests -m gpu -x -v --timeout 300 \
-        --timeout-method thread -k "$k" > "$out/tests$i.log" 2>&1 || { tail -40 "$out/tests$i.log"; exit 1; }
-      tail -1 "$out/tests$i.log";;
+        --timeout-method thread -k "$k" > "$out/tests$i.log" 2>&1; rc=$?
+      tail -1 "$out/tests$i.log"
+      if [ $rc -ne 0 ] && { [ $kind = vtests ] || [ $rc -ne 1 ]; }; then tail -40 "$out/tests$i.log"; exit 1; fi;;
     bench|r4bench|ab|r4ab)
       dir=.; [ "${kind:0:2}" = r4 ] && dir=_ab/r4
       extra=""; [ "${kind#r4}" = ab ] && extra="--no-cpu-baseline --traffic off --no-companions"
