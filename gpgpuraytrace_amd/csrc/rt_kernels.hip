@@ -1270,6 +1270,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
     };
 
+    // RT_SEG_DRAIN_ALL: after the drain every long ray goes to the segment waves (nomadplains only: the other
+    // landscapes have no segment march, so their waves keep refilling)
+    constexpr bool kSegDrainAll = RT_SEG_DRAIN_ALL && L == RT_NOMADPLAINS && kSegLanes > 0u;
     // ---- a batch of long rays, lane refill from the ring ----
     auto do_shadow = [&]() {
         March<L, true> st;
@@ -1289,7 +1292,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             }
             const uint64_t idle = __ballot(!live);
             const uint32_t nidle = (uint32_t)__popcll(idle);
-            if (nidle >= refill_idle && queued_long() != 0u) {
+            if (nidle >= refill_idle && queued_long() != 0u && !(kSegDrainAll && vload(q.drained) != 0u)) {
                 q_lock(&q.lock, lane);
                 free_fin_locked(live, aux);
                 const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
@@ -1347,8 +1350,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             const bool drained_now = vload(q.drained) != 0u;
             bool hand_back = lv != 0ull && (uint32_t)__popcll(lv) < compact_live && queued_long() == 0u && !drained_now;
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) // after the drain: few rays go to segment waves
-                hand_back = hand_back || (drained_now && lv != 0ull && (uint32_t)__popcll(lv) <= kSegHandBack &&
-                                          queued_long() == 0u);
+                hand_back = hand_back || (drained_now && lv != 0ull && (kSegDrainAll ||
+                                          ((uint32_t)__popcll(lv) <= kSegHandBack && queued_long() == 0u)));
             if (lv == 0ull || hand_back) {
                 if (__ballot(!live && (aux < kFinSlots || aux_slot_free(aux)))) {
                     q_lock(&q.lock, lane);
@@ -2020,7 +2023,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
            wt[15] = t0; if (drained && wt[18] == 0) { wt[18] = t0; wt[19] = lp; wt[20] = hp; })
         if (lp >= long_batch || (drained && lp > 0u)) {
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
-                if (drained && lp <= kSegQueue) {
+                if (drained && (kSegDrainAll || lp <= kSegQueue)) { // (drain-all: do_shadow refills nothing now)
                     do_shadow_seg();
                     WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
                     continue;

@@ -31,15 +31,22 @@
 #endif
 // after the unit queue drains (nomadplains): a long-ray wave with <= RT_SEG_HANDBACK live rays and an
 // empty ring hands them back; a wave that finds <= RT_SEG_QUEUE queued marches them as segments of
-// RT_SEG_LANES lanes per ray (0: off)
+// RT_SEG_LANES lanes per ray (0: off).  Round 5: 64 / 4096 (every post-drain wave with an empty ring
+// hands back, every post-drain long-ray job is a segment job): the blocks' median post-drain tail -10%,
+// the N = 8 shard simulation -0.3 to -1.6%, N = 1 within noise (profiles/r05/tail_ab.md; round 4: 16 / 64)
 #ifndef RT_SEG_LANES
 #define RT_SEG_LANES 8
 #endif
 #ifndef RT_SEG_HANDBACK
-#define RT_SEG_HANDBACK 16
+#define RT_SEG_HANDBACK 64
 #endif
 #ifndef RT_SEG_QUEUE
-#define RT_SEG_QUEUE 64
+#define RT_SEG_QUEUE 4096
+#endif
+// 1: after the drain a long-ray wave refills nothing and hands back all its rays, so every post-drain long
+// ray marches on a segment (with RT_SEG_QUEUE large enough that waves take them as segments)
+#ifndef RT_SEG_DRAIN_ALL
+#define RT_SEG_DRAIN_ALL 0
 #endif
 // a primary unit's last <= RT_PRIMARY_SEG rays march on 64 / RT_PRIMARY_SEG lanes each (0, 4, 8, 16)
 #ifndef RT_PRIMARY_SEG

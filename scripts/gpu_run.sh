@@ -13,6 +13,7 @@
 #   gbench=<args>                bench.py with RT_BENCH_GATED=1 (the gated launch: the prepass inside k_trace)
 #   sim=<batch_shard_sim args>   scripts/batch_shard_sim.py
 #   prof=<bench.py args>         rocprofv3 --kernel-trace --stats over bench.py -> prof<i>/
+#   smoke                        __graft_entry__.smoke()
 #   py=<script and args>         any python script of the repo (diagnostics)
 #   vpy=<variant>:<script args>  the same against an A/B build _build/librt_hip_<variant>.so
 set -o pipefail
@@ -76,6 +77,10 @@ for step in "$@"; do
       RT_LIB_VARIANT=$v timeout -k 10 600 python3 scripts/with_variant.py $rest > "$out/py$i.log" 2>&1 \
         || { tail -20 "$out/py$i.log"; exit 1; }
       tail -5 "$out/py$i.log";;
+    smoke)  # __graft_entry__.smoke() (the driver's round-end smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke$i.log" 2>&1 \
+        || { tail -20 "$out/smoke$i.log"; exit 1; }
+      tail -2 "$out/smoke$i.log";;
     *) echo "unknown step $step"; exit 2;;
   esac
 done
