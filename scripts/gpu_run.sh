@@ -65,7 +65,7 @@ for step in "$@"; do
       timeout -k 10 600 python3 scripts/batch_shard_sim.py $arg > "$out/sim$i.log" 2>&1 || { tail -20 "$out/sim$i.log"; exit 1; }
       tail -5 "$out/sim$i.log";;
     prof)
-      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof$i" \
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof$i" \
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --traffic off --no-companions $arg) \
         > "$out/prof$i.log" 2>&1 || { tail -20 "$out/prof$i.log"; exit 1; }
       tail -1 "$out/prof$i.log";;

@@ -16,6 +16,6 @@ export LD_LIBRARY_PATH="$(dirname "$RT"):/opt/rocm/lib/llvm/lib:${LD_LIBRARY_PAT
 # python itself is not instrumented: its allocations are not leaks of ours
 export ASAN_OPTIONS="detect_leaks=0:halt_on_error=1:abort_on_error=1:allocator_may_return_null=1"
 export UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"
-python3 scripts/sanitize_run.py -q -p no:cacheprovider -m "not gpu" \
+python3 tests/tools/sanitize_run.py -q -p no:cacheprovider -m "not gpu" \
   tests/test_oracle.py tests/test_sky_kat.py tests/test_host.py tests/test_varmgr.py tests/test_output.py \
   tests/test_flyby.py "$@"

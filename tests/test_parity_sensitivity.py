@@ -1,4 +1,4 @@
-"""The error bar on "parity unpinned" (profiles/r03/parity_sensitivity.md, scripts/parity_sensitivity.py).
+"""The error bar on "parity unpinned" (profiles/r03/parity_sensitivity.md, tests/tools/parity_sensitivity.py).
 
 The GPU equals oracle/rt_oracle.c bit for bit, but the oracle fixes one reading of the HLSL's
 arithmetic (mad fusion, div, transcendental precision) that fxc + a D3D driver may make otherwise.

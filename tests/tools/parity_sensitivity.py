@@ -16,7 +16,7 @@ against the default oracle (= the GPU):
 
 Cases: every committed golden frame (tests/golden, small) and row samples of BASELINE C2 and C3.
 Writes profiles/r03/parity_sensitivity.{json,md}.
-  python scripts/parity_sensitivity.py [--row-step 8] [--threads 0]
+  python tests/tools/parity_sensitivity.py [--row-step 8] [--threads 0]
 """
 import argparse
 import json
@@ -26,7 +26,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import golden_index as GI  # noqa: E402
@@ -110,7 +110,7 @@ def main():
 
 
 def report(r):
-    lines = ["# Parity sensitivity to the HLSL arithmetic conventions (generated by scripts/parity_sensitivity.py)",
+    lines = ["# Parity sensitivity to the HLSL arithmetic conventions (generated by tests/tools/parity_sensitivity.py)",
              "",
              "Each variant re-renders the case with oracle/rt_oracle.c built under another equally valid reading",
              "of the HLSL (RO_CONV_UNFUSED: every mad / lerp / dot / mul unfused, tracing.hlsl:54 included;",

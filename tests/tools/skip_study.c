@@ -9,10 +9,10 @@
  * bounded by NB * sum_{N>k} 1/S_N (|noise3d| <= NB); pushing that interval through
  * pow(|30 s + 1| * 35, 0.78), the terraces and the floor lift (terrain.hlsl:26-38) bounds d.
  * Per sample this records (n, k_need): the octaves evaluated now and the fewest that decide the
- * step.  Built by scripts/skip_study.py, which includes the oracle's own source.
+ * step.  Built by tests/tools/skip_study.py, which includes the oracle's own source.
  */
 #define RO_STUDY 1
-#include "../oracle/rt_oracle.c"
+#include "../../oracle/rt_oracle.c"
 
 #include <stdio.h>
 

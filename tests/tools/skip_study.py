@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
-"""Diagnostic: potential of an exact FBM early exit (scripts/skip_study.c) at a BASELINE config.
+"""Diagnostic: potential of an exact FBM early exit (tests/tools/skip_study.c) at a BASELINE config.
 
 Renders bands of 8 rows with the oracle instrumented per march sample, then emulates the GPU's
 wave64 lockstep: a primary unit (8x8 pixels) pays, per march iteration, the max over its live
 lanes of the octaves evaluated; long rays (shadow / AO) refill lanes, so they are modelled as
 random groups of 64 samples.  Prints octave-iteration totals now vs with the early exit.
 
-  python scripts/skip_study.py [--config c3] [--nb 1.0] [--band-every 64]
+  python tests/tools/skip_study.py [--config c3] [--nb 1.0] [--band-every 64]
 """
 import argparse
 import ctypes as C
@@ -16,17 +16,17 @@ import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle_lib as O  # noqa: E402
 
-SO = os.path.join(ROOT, "scripts", "_build", "libskip_study.so")
+SO = os.path.join(ROOT, "tests", "tools", "_build", "libskip_study.so")
 
 
 def build():
     os.makedirs(os.path.dirname(SO), exist_ok=True)
-    src = os.path.join(ROOT, "scripts", "skip_study.c")
+    src = os.path.join(ROOT, "tests", "tools", "skip_study.c")
     subprocess.run(["gcc", "-O2", "-std=c11", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fopenmp",
                     "-shared", "-o", SO, src, "-lm"], check=True)
 
