@@ -674,7 +674,9 @@ def main():
             "value": round(rays_per_frame * a.steps / dt_serial / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt_serial / a.steps * 1e3, 4),
             "primary_plus_shadow_mrays": round(ps * a.steps / dt_serial / 1e6, 3),
-            "how": f"rt_terrain_render, one frame at a time on one stream (B=1, no overlap), {a.steps} frames"}
+            "how": f"rt_terrain_render, one frame per call on one device and its stream (B=1; each frame's prepass "
+                   f"on the device's prepass stream behind the previous frame's k_order, overlapping that frame's "
+                   f"trace tail), {a.steps} frames"}
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)

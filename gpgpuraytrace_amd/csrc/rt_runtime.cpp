@@ -160,6 +160,13 @@ struct rt_device_s {
     // are not read -- by a render this device leads, or a map -- before ev_ahead_in
     hipEvent_t ev_ahead_in = nullptr;
     bool ahead_in_pending = false;
+    // rt_terrain_render's own prepass stream (round 5): frame i+1's prepass waits for frame i's k_order
+    // (ev_order) only, so it runs in frame i's trace tail instead of after it; ev_pre orders the trace
+    // after it.  serial_ok: the last render this device led was such a render (nothing but k_order and
+    // the trace read its CameraResults since)
+    hipStream_t pre_stream = nullptr;
+    hipEvent_t ev_pre = nullptr;
+    bool serial_ok = false;
     // the prepass of the batch this device leads fused into another batch's k_trace (FusedPrepass):
     // STAGED = constants and frame table uploaded by rt_terrain_prepass_ahead, waiting for a trace to
     // take it; FUSED = a k_trace runs it (ev_fuser_done follows that launch).  fctl: its task / ray
@@ -728,6 +735,10 @@ rt_device_s::~rt_device_s()
     if (fuse_state == FUSE_FUSED && ev_fuser_done) (void)hipEventSynchronize(ev_fuser_done); // it writes our frames
     if (stream) (void)hipStreamSynchronize(stream); // the stream in use is alive: a reference is held
     if (hipStream_t side = ahead_stream(ordinal, false)) (void)hipStreamSynchronize(side); // ahead prepasses
+    if (pre_stream) { // rt_terrain_render's prepasses
+        (void)hipStreamSynchronize(pre_stream);
+        (void)hipStreamDestroy(pre_stream);
+    }
     for (auto* c : computes) delete c;              // children die with their device
     for (auto* t : textures) {
         if (t->data) (void)hipFree(t->data);
@@ -740,7 +751,7 @@ rt_device_s::~rt_device_s()
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
     if (graph_trace.exec) (void)hipGraphExecDestroy(graph_trace.exec);
-    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in, ev_fuser_done, ev_fuse_order})
+    for (hipEvent_t e : {sync_ev, ev_order, ev_ahead, ev_ahead_in, ev_fuser_done, ev_fuse_order, ev_pre})
         if (e) (void)hipEventDestroy(e);
     for (auto& pr : ev_pool) {
         (void)hipEventDestroy(pr.first);
@@ -885,6 +896,7 @@ int rt_device_set_stream(rt_device d, void* s)
     if (want != d->own_stream) stream_ref(want);             // borrow (tracked if another device owns it)
     if (d->stream != d->own_stream) stream_unref(d->stream); // return the previous loan
     d->stream = want;
+    d->serial_ok = false;
     return RT_OK;
 }
 
@@ -1175,6 +1187,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     rt_device dev = c->dev;
     int rc = host_flag_check(dev);
     if (rc) return rc;
+    dev->serial_ok = false; // a dispatch of its own (reads / writes the arrays on the stream)
     rc = check_texture(s);
     if (rc) return rc;
     rc = sync_shader(dev, s);
@@ -1276,6 +1289,7 @@ int rt_array_unmap(rt_array a)
     if (!a) return fail(RT_ERR_INVALID, "null array");
     if (!a->uav) return fail(RT_ERR_UNSUPPORTED, "unmap not supported on SRV array %s", a->name.c_str());
     if (!a->dev_ptr) return fail(RT_ERR_STATE, "array not created");
+    a->dev->serial_ok = false; // the upload is ordered on the stream only: the next render prepasses in line
     return a->staging.upload(a->dev->stream, a->dev_ptr, a->host.data(), a->host.size());
 }
 
@@ -1284,6 +1298,7 @@ int rt_array_write(rt_array a, const void* data)
     if (!a || !data) return fail(RT_ERR_INVALID, "bad arguments");
     if (a->uav) return fail(RT_ERR_UNSUPPORTED, "write not supported on UAV array %s", a->name.c_str());
     if (!a->dev_ptr) return fail(RT_ERR_STATE, "array %s not created", a->name.c_str());
+    a->dev->serial_ok = false;
     return a->staging.upload(a->dev->stream, a->dev_ptr, data, (size_t)a->elements * a->stride);
 }
 
@@ -1308,13 +1323,51 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
                                 const TraceFuse* fuse = nullptr, uint8_t* packed_dst = nullptr,
                                 size_t packed_stride = 0);
 
+// Terrain::render (Terrain.cpp:105-136), one frame per call on the device's stream.  Frame i+1's
+// camerarays prepass needs only frame i's k_order to be done (the last reader of CameraResults): on the
+// device's own prepass stream it waits for that k_order (ev_order, recorded between k_order and k_trace)
+// and so runs in frame i's trace tail, where the persistent k_trace's blocks retire, instead of after
+// the whole frame; the trace waits for it (ev_pre).  Same launches, same bits.  The first frame, and a
+// frame after anything else read this device's CameraResults on its stream (a feed render, an ahead or
+// fused prepass, a batch), prepass in line; so do the instrumented, graph and gated devices.
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
-    return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false);
+    rt_device d = (cam && scr && scr->dev && cam->dev == scr->dev) ? scr->dev : nullptr;
+    const bool plain = d && !(d->flags & (RT_DEVICE_GRAPH | RT_DEVICE_STATS | RT_DEVICE_GATED)) && d->stream &&
+                       !d->ahead_pending && !d->ahead_in_pending && d->fuse_state == rt_device_s::FUSE_NONE;
+    if (!plain) {
+        if (d) d->serial_ok = false;
+        return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false);
+    }
+    if (int rc0 = host_flag_check(d)) return rc0;
+    HIP_TRY(hipSetDevice(d->ordinal));
+    if (!d->ev_order) HIP_TRY(hipEventCreateWithFlags(&d->ev_order, hipEventDisableTiming));
+    if (!(d->serial_ok && d->order_recorded)) {
+        int rc = terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false); // records ev_order
+        d->serial_ok = rc == RT_OK;
+        return rc;
+    }
+    if (!d->pre_stream) HIP_TRY(hipStreamCreateWithFlags(&d->pre_stream, hipStreamNonBlocking));
+    if (!d->ev_pre) HIP_TRY(hipEventCreateWithFlags(&d->ev_pre, hipEventDisableTiming));
+    HIP_TRY(hipStreamWaitEvent(d->pre_stream, d->ev_order, 0));
+    hipStream_t main = d->stream;
+    d->stream = d->pre_stream; // the prepass-only call uploads the camerarays constants and launches there
+    int rc = terrain_render_batch(&cam, &scr, 1, 0, 1, false, PH_PRE);
+    d->stream = main;
+    if (rc) {
+        d->serial_ok = false;
+        return rc;
+    }
+    HIP_TRY(hipEventRecord(d->ev_pre, d->pre_stream));
+    HIP_TRY(hipStreamWaitEvent(main, d->ev_pre, 0));
+    rc = terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false, PH_TRACE);
+    d->serial_ok = rc == RT_OK;
+    return rc;
 }
 
 int rt_terrain_render_feed(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
+    if (cam && cam->dev) cam->dev->serial_ok = false; // its CameraResults copy follows the prepass
     return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, true);
 }
 
@@ -1502,6 +1555,8 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
             lead->fuse_state = rt_device_s::FUSE_NONE;
         }
     }
+    for (int f = 0; scrs && f < n && f < RT_MAX_BATCH; ++f) // rt_terrain_render re-arms its own renders
+        if (scrs[f] && scrs[f]->dev) scrs[f]->dev->serial_ok = false;
     int rc;
     Batch b;
     if ((rc = batch_begin(cams, scrs, n, b, (phases & (PH_PRE | PH_STAGE)) != 0, (phases & PH_TRACE) != 0))) return rc;

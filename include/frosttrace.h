@@ -224,7 +224,15 @@ void* rt_array_device_pointer(rt_array arr);
  * screen_cs over the whole screen, all enqueued on the device stream.  Equivalent to the
  * reference sequence run(2,2,1); CameraResults map/unmap; setTargetDepths; CellDistance
  * write; tiled run(...).  With shard_count > 1 only screen tiles t (32x32 pixels,
- * row-major tile index) with t % shard_count == shard_rank are traced. */
+ * row-major tile index) with t % shard_count == shard_rank are traced.
+ * Frames in flight (ABI 7, same bits): from a device's second consecutive rt_terrain_render on,
+ * the prepass runs on the device's own prepass stream, ordered after the previous frame's
+ * setTargetDepths (the last reader of CameraResults) and before this frame's setTargetDepths, so it
+ * overlaps the previous frame's trace; the device stream stays the order a host sees (synchronise,
+ * readbacks, events).  Any other call that touches the device's arrays or launches on it (a batch, the
+ * feed, an ahead prepass, rt_compute_run, rt_array_unmap / write, a stream change) makes the next
+ * render prepass in line.  A host writing CameraResults through rt_array_device_pointer on its own
+ * must synchronise first.  Not for RT_DEVICE_GRAPH, RT_DEVICE_STATS or RT_DEVICE_GATED devices. */
 int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
 /* rt_terrain_render_feed: rt_terrain_render that also hands the frame's 1024 CameraResults
  * (camerarays.hlsl:12-21, Terrain::getCameraView) to the host as soon as the prepass ends,

@@ -1705,3 +1705,42 @@ def test_fused_prepass_camera_change_and_partial_batch():
     for dev, _ in ring.slots:
         dev.check()
     ring.destroy()
+
+
+# --- rt_terrain_render's prepass stream (round 5): frame i+1's prepass in frame i's trace tail ----------------
+@pytest.mark.parametrize("pair", [(0, 1), (4, 5)], ids=["nomadplains", "testing"])
+def test_render_serial_prepass_stream_frames_in_flight(pair):
+    """Frames rendered back to back on ONE device with no host synchronisation, the camera alternating
+    between two golden poses: each rt_terrain_render queues its prepass on the device's prepass stream
+    behind the previous frame's k_order only (so it overlaps that frame's trace) and its trace behind the
+    prepass.  A copy of every frame queued on the device's stream right after it (rt_shard_pack, one shard)
+    equals that pose's golden frame, and the last frame's CameraResults and CellDistance equal its golden
+    arrays: no prepass overwrote CameraResults before the previous k_order read them."""
+    import torch
+    from gpgpuraytrace_amd import engine as E
+    from gpgpuraytrace_amd import parallel as P
+    gold = GI.load()
+    specs = [GI.FRAMES[i] for i in pair]
+    land, _, w, h, aa, ms, ao = GI.unpack(specs[0])
+    cams = [GI.consts(w, h, GI.unpack(s)[1]) for s in specs]
+    keys = [GI.frame_key(*s) for s in specs]
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False)
+    nbytes = P.shard_bytes(w, h, 0, 1)
+    bufs = [torch.zeros(nbytes, dtype=torch.uint8, device="cuda:0") for _ in range(7)]
+    torch.cuda.synchronize()
+    for k, buf in enumerate(bufs):
+        ter.set_camera(FixedCamera(cams[k % 2]))
+        ter.update_terrain()
+        ter.set_time_of_day_vec(cams[k % 2]["sun"])
+        ter.render_device()
+        E.shard_pack(dev, 0, 1, buf.data_ptr())
+    dev.synchronize()
+    for k, buf in enumerate(bufs):
+        frame = P.unpack_host(np.zeros((h, w), np.uint32), buf.cpu().numpy().view(np.uint32), 0, 1)
+        assert np.array_equal(frame.view(np.uint8).reshape(h, w, 4), gold[keys[k % 2] + "_rgba8"]), k
+    last = keys[(len(bufs) - 1) % 2]
+    assert np.array_equal(_device_cells(ter), gold[last + "_cell_distance"])
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, gold[last + "_camera_results"])
+    dev.check()
+    dev.destroy()
