@@ -1272,7 +1272,9 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
 
     // RT_SEG_DRAIN_ALL: after the drain every long ray goes to the segment waves (nomadplains only: the other
     // landscapes have no segment march, so their waves keep refilling)
-    constexpr bool kSegDrainAll = RT_SEG_DRAIN_ALL && L == RT_NOMADPLAINS && kSegLanes > 0u;
+    // (2: no refill after the drain, but a wave keeps the rays it holds: new rays go to segment waves only)
+    constexpr bool kSegDrainAll = RT_SEG_DRAIN_ALL != 0 && L == RT_NOMADPLAINS && kSegLanes > 0u;
+    constexpr bool kSegDrainHandAll = RT_SEG_DRAIN_ALL == 1 && kSegDrainAll;
     // ---- a batch of long rays, lane refill from the ring ----
     auto do_shadow = [&]() {
         March<L, true> st;
@@ -1350,7 +1352,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             const bool drained_now = vload(q.drained) != 0u;
             bool hand_back = lv != 0ull && (uint32_t)__popcll(lv) < compact_live && queued_long() == 0u && !drained_now;
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) // after the drain: few rays go to segment waves
-                hand_back = hand_back || (drained_now && lv != 0ull && (kSegDrainAll ||
+                hand_back = hand_back || (drained_now && lv != 0ull && (kSegDrainHandAll ||
                                           ((uint32_t)__popcll(lv) <= kSegHandBack && queued_long() == 0u)));
             if (lv == 0ull || hand_back) {
                 if (__ballot(!live && (aux < kFinSlots || aux_slot_free(aux)))) {
