@@ -1023,6 +1023,8 @@ struct TraceQueues {
     // the gated launch (GatedPrepass), per block so that no wave holds them in registers: the block's tile
     // scan position, every frame's prepass seen done, the frames whose CellDistance is seen flagged
     uint32_t gscan, gate_all, gate_cells;
+    uint32_t near_end; // a wave of this block took one of the last RT_NEAR_UNITS x (wave slots) units
+
     float4 longs[kLongRing * kShadowRec];
     uint16_t fin_free[kFinSlots];
     uint32_t ao_ctr[kAoSlots / 2]; // AO slot s: bits 16 (s & 1) + 0..4 rays finished, + 5..9 occluded
@@ -1106,6 +1108,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         q.f_top = fin_slots;
         q.overflow = 0;
         q.gscan = q.gate_all = q.gate_cells = 0;
+        q.near_end = 0;
         if constexpr (STATS) s_st = BlockStats{};
     }
     for (uint32_t i = threadIdx.x; i < fin_slots; i += blockDim.x) q.fin_free[i] = (uint16_t)i;
@@ -2023,7 +2026,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         const bool drained = vload(q.drained) != 0u;
         WT(const unsigned long long t0 = __builtin_amdgcn_s_memrealtime(); wt[12]++;
            wt[15] = t0; if (drained && wt[18] == 0) { wt[18] = t0; wt[19] = lp; wt[20] = hp; })
-        if (lp >= long_batch || (drained && lp > 0u)) {
+        // near the queue's end the long rays are taken from a smaller backlog (RT_NEAR_LONG_BATCH), so the
+        // block's backlog at the drain -- what its post-drain tail marches -- is small
+        const uint32_t lb_now = (RT_NEAR_UNITS > 0 && vload(q.near_end) != 0u) ? (uint32_t)RT_NEAR_LONG_BATCH : long_batch;
+        if (lp >= lb_now || (drained && lp > 0u)) {
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
                 if (drained && (kSegDrainAll || lp <= kSegQueue)) { // (drain-all: do_shadow refills nothing now)
                     do_shadow_seg();
@@ -2058,6 +2064,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             } else {
                 const uint32_t qi = first_unit ? first_qi : n_static + wave_fetch(&counters[RT_CTR_PRIMARY], lane);
                 first_unit = false;
+                if (RT_NEAR_UNITS > 0 && qi + (uint32_t)RT_NEAR_UNITS * n_static >= n_total && lane == 0) q.near_end = 1u;
                 if (qi < n_total) {
                     // the batch's tiles longest-first across its frames: entry (frame << 24) | tile
                     const uint32_t e = __builtin_amdgcn_readfirstlane(order[qi >> 4]);

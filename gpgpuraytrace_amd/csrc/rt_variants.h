@@ -8,6 +8,14 @@
 #pragma once
 
 // ---- k_trace's scheduler ----------------------------------------------------------------------
+// near the unit queue's end (a wave took one of its last RT_NEAR_UNITS x wave-slots units; 0: off) the block
+// takes long rays from RT_NEAR_LONG_BATCH queued instead of RT_LONG_BATCH
+#ifndef RT_NEAR_UNITS
+#define RT_NEAR_UNITS 0
+#endif
+#ifndef RT_NEAR_LONG_BATCH
+#define RT_NEAR_LONG_BATCH 16
+#endif
 // lanes idle before a long-ray wave refills them from the ring (amortises the refill's prologue)
 #ifndef RT_REFILL_IDLE
 #define RT_REFILL_IDLE 4
