@@ -9,9 +9,11 @@
 
 // ---- k_trace's scheduler ----------------------------------------------------------------------
 // near the unit queue's end (a wave took one of its last RT_NEAR_UNITS x wave-slots units; 0: off) the block
-// takes long rays from RT_NEAR_LONG_BATCH queued instead of RT_LONG_BATCH
+// takes long rays from RT_NEAR_LONG_BATCH queued instead of RT_LONG_BATCH: the blocks' long-ray backlog at
+// the drain (p50 35 -> 10 rays at N = 8) and the N = 8 shard simulation -1.2%, N = 1 within noise
+// (profiles/r05/tail_ab.md)
 #ifndef RT_NEAR_UNITS
-#define RT_NEAR_UNITS 0
+#define RT_NEAR_UNITS 2
 #endif
 #ifndef RT_NEAR_LONG_BATCH
 #define RT_NEAR_LONG_BATCH 16
