@@ -1362,6 +1362,7 @@ int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_
     HIP_TRY(hipStreamWaitEvent(main, d->ev_pre, 0));
     rc = terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false, PH_TRACE);
     d->serial_ok = rc == RT_OK;
+    if (rc == RT_OK) ++d->prepass_launches; // a render with a prepass launch (rt_device_info), on the prepass stream
     return rc;
 }
 

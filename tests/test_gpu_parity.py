@@ -1735,6 +1735,7 @@ def test_render_serial_prepass_stream_frames_in_flight(pair):
         ter.render_device()
         E.shard_pack(dev, 0, 1, buf.data_ptr())
     dev.synchronize()
+    assert dev.launch_info() == (0, len(bufs))  # every render ran its prepass launch (the first in line)
     for k, buf in enumerate(bufs):
         frame = P.unpack_host(np.zeros((h, w), np.uint32), buf.cpu().numpy().view(np.uint32), 0, 1)
         assert np.array_equal(frame.view(np.uint8).reshape(h, w, 4), gold[keys[k % 2] + "_rgba8"]), k
