@@ -10,11 +10,7 @@
 // device creation and by rt_device_check only): a k_trace queue push that would exceed its bound
 // raises a flag instead of storing (rt_spill_caps)
 // RT_CTR_GATE / RT_CTR_SCAN: the gated launch's prepass task counter and its tile scan's start (GatedPrepass)
-// RT_CTR_STEAL_*: the post-drain cross-block shadow queue (RT_STEAL): records published, taken, the pushers' lock
-enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1, RT_CTR_GATE = 24, RT_CTR_SCAN = 25, RT_CTR_STEAL_PUSH = 26,
-       RT_CTR_STEAL_POP = 27, RT_CTR_STEAL_LOCK = 28 };
-// records of that queue (3 float4 each), after the blocks' long-ray spill stacks in the same allocation
-#define RT_STEAL_CAP 16384
+enum { RT_CTR_PRIMARY = 0, RT_CTR_FIRST = 1, RT_CTR_GATE = 24, RT_CTR_SCAN = 25 };
 #define RT_CTR_BYTES 128
 #define RT_QUEUE_BYTES 192
 enum { RT_FLAG_HIT_OVERFLOW = 1u, RT_FLAG_SPILL_OVERFLOW = 2u, RT_FLAG_PREPASS_TIMEOUT = 4u };

@@ -1130,9 +1130,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     float4* const finp = finpool + (size_t)blockIdx.x * kFinSlots * FinRec<L>::N;
     float4* const cpl = cpool + (size_t)blockIdx.x * RT_AO_POOL_SLOTS; // fitm: the AO slots' hit colours
     float4* const lspill = spill_long + (size_t)blockIdx.x * long_spill_cap * kShadowRec;
-    // RT_STEAL: the cross-block queue of post-drain shadow rays, after every block's spill stack
-    float4* const steal_ring = spill_long + (size_t)gridDim.x * long_spill_cap * kShadowRec;
-    (void)steal_ring;
     // queued work of the block: long rays in the LDS ring + spill stack, hits in the hit queue
     auto queued_long = [&]() { return vload(q.l_tail) - vload(q.l_head) + vload(q.ls_top); };
     auto queued_hits = [&]() { return vload(q.h_top); };
@@ -1276,90 +1273,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         }
     };
 
-    // ---- RT_STEAL: the cross-block queue of post-drain shadow rays ----
-    // A block's long rays are its own (its LDS ring, its fin pool); after the drain, blocks with nothing
-    // left idle while a few march hundreds.  steal_export (lanes ex: live shadow rays of this wave): their
-    // finishing inputs go from the block's fin pool to fin[t] (sc1 stores; the slot returns to the pool),
-    // their records to the global queue under a global lock: written with sc1 stores, waited, then
-    // published by the push counter (MI355X_MICROARCH.md row 1: the hand-off across XCDs).  AO rays never
-    // move: a fit AO ray overwrites the pixel the shading stored and a counted one the byte it flagged,
-    // and two blocks' stores on different XCDs could land in either order.
-    constexpr bool kSteal = RT_STEAL != 0 && L == RT_NOMADPLAINS && kSegLanes > 0u && !FogLive<L>::value;
-    auto st_store = [&](float4* dst, float4 v) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const v4f w = {v.x, v.y, v.z, v.w};
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(w) : "memory");
-    };
-    auto steal_export = [&](bool ex, const March<L, true>& st, uint32_t t, uint32_t& aux, bool& live) {
-        if constexpr (kSteal) {
-            const uint64_t eb = __ballot(ex);
-            if (!eb) return;
-            const uint32_t n = (uint32_t)__popcll(eb), rank = lane_rank(eb);
-            uint32_t base = 0;
-            if (lane == 0) {
-                while (atomicCAS(&counters[RT_CTR_STEAL_LOCK], 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(2);
-                base = __hip_atomic_load(&counters[RT_CTR_STEAL_PUSH], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-            const bool room = base + n <= (uint32_t)RT_STEAL_CAP;
-            if (room) {
-                constexpr uint32_t FR = FinRec<L>::N;
-                if (ex) {
-                    if (aux < kFinSlots) { // the inputs a shadow finishes with, to fin[t] (fog-free: 2 float4)
-                        st_store(fin + (size_t)FR * t, ld_rec(finp, FR * aux));
-                        st_store(fin + (size_t)FR * t + FR - 1u, ld_rec(finp, FR * aux + FR - 1u));
-                    } else { // already at fin[t] (the pool was empty), by the shading's plain stores: write through
-                        const float4 f0 = ld_fresh(fin + (size_t)FR * t), f1 = ld_fresh(fin + (size_t)FR * t + FR - 1u);
-                        st_store(fin + (size_t)FR * t, f0);
-                        st_store(fin + (size_t)FR * t + FR - 1u, f1);
-                    }
-                    float4 r[kShadowRec];
-                    long_pack(st, t, kAuxFinT, r);
-                    float4* dst = steal_ring + (size_t)(base + rank) * kShadowRec;
-                    st_store(dst, r[0]);
-                    st_store(dst + 1, r[1]);
-                }
-                asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
-                if (lane == 0) atomicAdd(&counters[RT_CTR_STEAL_PUSH], n); // publishes [base, base + n)
-            }
-            if (lane == 0) atomicExch(&counters[RT_CTR_STEAL_LOCK], 0u);
-            if (room) {
-                // the exported rays' pool slots return to this block's free list; the lanes are free
-                if (__ballot(ex && aux < kFinSlots)) {
-                    q_lock(&q.lock, lane);
-                    free_fin_locked(!(ex && aux < kFinSlots), aux);
-                    q_unlock(&q.lock, lane);
-                }
-                if (ex) {
-                    live = false;
-                    aux = kAuxAO;
-                }
-            }
-        }
-    };
-    // an idle wave of a block with nothing left: up to 64 / kSegLanes published records, or 0
-    auto steal_claim = [&](uint32_t* first) -> uint32_t {
-        uint32_t got = 0, at = 0;
-        if constexpr (kSteal) {
-            constexpr uint32_t RPW = 64u / (kSegLanes ? kSegLanes : 8u);
-            if (lane == 0) {
-                for (;;) {
-                    const uint32_t pop = __hip_atomic_load(&counters[RT_CTR_STEAL_POP], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t push = __hip_atomic_load(&counters[RT_CTR_STEAL_PUSH], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (pop >= push) break;
-                    const uint32_t k = push - pop < RPW ? push - pop : RPW;
-                    if (atomicCAS(&counters[RT_CTR_STEAL_POP], pop, pop + k) == pop) {
-                        got = k;
-                        at = pop;
-                        break;
-                    }
-                }
-            }
-        }
-        *first = (uint32_t)__builtin_amdgcn_readfirstlane((int)at);
-        return (uint32_t)__builtin_amdgcn_readfirstlane((int)got);
-    };
-
     // RT_SEG_DRAIN_ALL: after the drain every long ray goes to the segment waves (nomadplains only: the other
     // landscapes have no segment march, so their waves keep refilling)
     // (2: no refill after the drain, but a wave keeps the rays it holds: new rays go to segment waves only)
@@ -1374,9 +1287,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         uint32_t t = 0, aux = kAuxAO; // aux: the lane's ray (long_pack); on an idle lane, a fin slot to free
         Ctx cl = c; // cl.eye: the frame of the lane's ray (set on refill)
         cl.nz.phase = RT_PHASE_LONG;
-        bool fresh = false; // RT_STEAL: the lane's ray came with this iteration's refill
         for (;;) {
-            fresh = false;
             if (live && !march_live<L, true, true>(cl, st, aux_ao(aux) ? RT_AO_END : 100.0f, 0)) {
                 WT(wl_rays++; wl_maxit = max(wl_maxit, (uint32_t)st.iters);)
                 stat(aux_ao(aux) ? BlockStats::AO : BlockStats::SHADOW, (uint32_t)st.iters);
@@ -1418,7 +1329,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
                     if (!aux_ao(aux)) st.dir = rtm::mk(fr[3], fr[4], fr[5]);
                     live = true;
-                    fresh = true;
                 };
                 if (mine && rank < take) {
                     const float4* r = &q.longs[((head + rank) % kLongRing) * kShadowRec];
@@ -1438,12 +1348,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
 #if RT_AO_GEN
             refilled:
 #endif
-            if constexpr (kSteal) {
-                // a post-drain block with more long rays queued than its waves march soon: the shadow rays
-                // just refilled go to the cross-block queue (their finishing inputs to fin[t])
-                if (vload(q.drained) != 0u && queued_long() > (uint32_t)RT_STEAL_PUSH)
-                    steal_export(live && fresh && !aux_ao(aux), st, t, aux, live);
-            }
             const uint64_t lv = __ballot(live);
             // The ring ran dry and few lanes are left: rather than march them on
             // mostly empty lanes, hand them back to the ring (another wave will merge
@@ -1473,8 +1377,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     };
 
     // ---- after the drain: up to 64 / kSegLanes queued long rays, a segment of lanes per ray ----
-    // sn > 0 (RT_STEAL): records [sfirst, sfirst + sn) of the cross-block queue instead of the block's own
-    auto do_shadow_seg = [&](uint32_t sfirst, uint32_t sn) {
+    auto do_shadow_seg = [&]() {
         if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
             constexpr uint32_t LPR = kSegLanes ? kSegLanes : 8u, RPW = 64u / LPR; // (8 only to compile the discarded branch when off)
             // late(): the segment's lane values (and the octave scales derived from them) are formed
@@ -1486,19 +1389,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             bool live = false;
             Ctx cl = c;
             cl.nz.phase = RT_PHASE_LONG;
-            if (kSteal && sn != 0u) {
-                // published records (sc1 loads: another XCD's block wrote them with sc1 stores); a shadow
-                // record's aux is kAuxFinT, its finishing inputs at fin[t] (also sc1, read by long_finish)
-                if (const uint32_t grp = late(lane) / (kSegLanes ? kSegLanes : 8u); grp < sn) {
-                    const uint32_t ri = (sfirst + grp) * kShadowRec;
-                    t = long_unpack(ld_rec(steal_ring, ri), ld_rec(steal_ring, ri + 1u), ld_rec(steal_ring, ri + 1u),
-                                    rtm::mk(0.0f, 0.0f, 0.0f), st, &aux);
-                    const float* fr = s_fr.v[frame_of(m, t)];
-                    cl.eye = rtm::mk(fr[0], fr[1], fr[2]);
-                    st.dir = rtm::mk(fr[3], fr[4], fr[5]);
-                    live = true;
-                }
-            } else {
             q_lock(&q.lock, lane);
             const uint32_t head = vload(q.l_head), tail = vload(q.l_tail);
             uint32_t take = (tail - head) < RPW ? (tail - head) : RPW;
@@ -1534,7 +1424,6 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 q.ls_top = sl - more;
             }
             q_unlock(&q.lock, lane);
-            }
             const uint32_t lid = late(lane);
             const uint32_t j = lid & (LPR - 1u), base = lid & ~(LPR - 1u);
             const SegOctaves<LPR> g = seg_octaves<LPR>(c, j);
@@ -2143,7 +2032,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if (lp >= lb_now || (drained && lp > 0u)) {
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
                 if (drained && (kSegDrainAll || lp <= kSegQueue)) { // (drain-all: do_shadow refills nothing now)
-                    do_shadow_seg(0u, 0u);
+                    do_shadow_seg();
                     WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
                     continue;
                 }
@@ -2194,20 +2083,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if (lane == 0) atomicSub(&q.active, 1u);
             continue;
         }
-        // drained and nothing queued: leave once no wave of the block can still push (RT_STEAL: after the
-        // cross-block queue of other blocks' shadow rays is empty too)
-        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) {
-            if constexpr (kSteal) {
-                uint32_t sf;
-                const uint32_t sn = steal_claim(&sf);
-                if (sn != 0u) {
-                    do_shadow_seg(sf, sn);
-                    WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
-                    continue;
-                }
-            }
-            break;
-        }
+        // drained and nothing queued: leave once no wave of the block can still push
+        if (vload(q.active) == 0u && queued_long() == 0u && queued_hits() == 0u) break;
         __builtin_amdgcn_s_sleep(2);
         WT(wt[9] += __builtin_amdgcn_s_memrealtime() - t0;)
     }

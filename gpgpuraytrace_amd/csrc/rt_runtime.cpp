@@ -608,7 +608,7 @@ int ensure_split_buffers(rt_device dev, int aa, int ao, int n_frames)
         dev->finpool = nullptr;
         dev->hitq_n = dev->spill_long_n = 0;
         HIP_TRY(hipMalloc(&dev->hitq, hq_need * 3 * sizeof(float4)));
-        HIP_TRY(hipMalloc(&dev->spill_long, (ls_need + RT_STEAL_CAP) * 3 * sizeof(float4))); // + the steal queue
+        HIP_TRY(hipMalloc(&dev->spill_long, ls_need * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->finpool, (size_t)dev->num_cus * RT_FIN_SLOTS * 3 * sizeof(float4)));
         HIP_TRY(hipMalloc(&dev->cpool, (size_t)dev->num_cus * RT_AO_POOL_SLOTS * sizeof(float4)));
         if (!dev->gate) HIP_TRY(hipMalloc(&dev->gate, (size_t)RT_MAX_BATCH * RT_GATE_WORDS * sizeof(uint32_t)));

@@ -114,16 +114,6 @@
 #define RT_FBM_EXIT 0
 #endif
 
-// RT_STEAL=1 (A/B): after the drain a block whose long-ray queue holds more than RT_STEAL_PUSH records exports
-// the shadow rays it refills into a global queue, which blocks with nothing left march as segments
-// (nomadplains; AO rays stay: their pixel / count stores race the shading's across XCDs)
-#ifndef RT_STEAL
-#define RT_STEAL 0
-#endif
-#ifndef RT_STEAL_PUSH
-#define RT_STEAL_PUSH 32
-#endif
-
 // ---- diagnostic builds (never in the product) ------------------------------------------------
 // RT_WAVE_TRACE          per-wave timeline of k_trace (make trace; scripts/wave_trace.py)
 // RT_LIVE_HIST           histogram of live lanes per primary march step (rt_debug_live_hist)
