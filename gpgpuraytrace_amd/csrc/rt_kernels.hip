@@ -1073,7 +1073,9 @@ struct TraceThreads {
 static_assert(RT_CTR_FIRST + RT_TRACE_WAVES_FAST <= RT_CTR_BYTES / 4 && RT_CTR_FIRST + RT_TRACE_WAVES_WIDE <= RT_CTR_BYTES / 4,
               "a first-unit counter per wave slot inside the zeroed work counters");
 
-template <int L, bool STATS>
+// GATED: the gated launch's instantiation (GatedPrepass, opt-in RT_DEVICE_GATED; nomadplains, no STATS).  The
+// product instantiations (GATED false) carry none of its task, scan and claim paths.
+template <int L, bool STATS, bool GATED = false>
 __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts* __restrict__ k, const FrameTable* __restrict__ ft,
                                                 const uint32_t* __restrict__ perm2d,
                                                 const float4* __restrict__ grad,
@@ -1853,7 +1855,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     // ---- one 8x8 primary unit ----
     auto do_unit = [&](uint32_t f, uint32_t u) {
         bool cells_in = true; // (the gated launch: the frame's CellDistance is stored, flagged by its last task)
-        if (gp.tasks) {
+        if constexpr (GATED) {
             cells_in = (vload(q.gate_cells) >> f) & 1u;
             if (!cells_in && ld_sc1(gp.gate + f * RT_GATE_WORDS + RT_GATE_CTR + 1) != 0u) {
                 cells_in = true;
@@ -1869,13 +1871,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if (valid) {
             float spx = pxf * k->rcp_w, spy = pyf * k->rcp_h;
             const uint32_t cell = (uint32_t)rtm::fma(rtm::floor(spy * 32.0f), 32.0f, rtm::floor(spx * 32.0f));
-            if (!cells_in) {
+            if (GATED && !cells_in) {
                 // the gated launch before the frame's CellDistance is flagged: the cell's setTargetDepths from
                 // its CameraResults (gate_ready passed)
                 const float4* cam = ft->cam[f];
                 plane_x = cell_bracket([&](int x, int y) { return cam_depth_sc1(cam, x, y); }, (int)(cell % RT_CAMERA_RES),
                                        (int)(cell / RT_CAMERA_RES)).x;
-            } else if (gp.tasks) { // flagged in this launch: an sc1 load of the bracket the frame's last task stored
+            } else if (GATED) { // flagged in this launch: an sc1 load of the bracket the frame's last task stored
                 typedef const float __attribute__((address_space(1))) gcfloat;
                 plane_x = __hip_atomic_load((gcfloat*)(ft->cells[f] + cell), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             } else {
@@ -1983,7 +1985,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
     const uint32_t first_qi = first_unit_index(counters, lane); // scalar, formed before the loop
     bool first_unit = true;
     bool np_open = np.tasks != 0u; // the next batch's prepass tasks may remain (FusedPrepass)
-    bool gp_open = gp.tasks != 0u; // this batch's own prepass tasks may remain (GatedPrepass)
+    bool gp_open = GATED && gp.tasks != 0u; // this batch's own prepass tasks may remain (GatedPrepass)
 #if RT_GATE_STATIC
     uint32_t gp_next = first_qi;
 #endif
@@ -1992,7 +1994,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         if constexpr (L == RT_NOMADPLAINS) {
             // the gated launch: this batch's own prepass before anything else (every unit waits for some
             // of its rays).  Tasks are taken by resident waves, so every taken task finishes.
-            if (gp_open) {
+            if (GATED && gp_open) {
 #if RT_GATE_STATIC
                 // static: the wave's tasks are its first-unit index and every n_static-th after it, so the
                 // first ones go to wave 0 of each block in the order the blocks start, then wave 1, ...: one
@@ -2048,12 +2050,12 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             WT(wt[3] += __builtin_amdgcn_s_memrealtime() - t0; wt[6]++;)
             continue;
         }
-        if (gp.tasks != 0u ? !drained : (!drained || first_unit)) {
+        if (GATED ? !drained : (!drained || first_unit)) {
             // (without the gated launch a wave's static first unit is taken even after the queue drained)
             if (lane == 0) atomicAdd(&q.active, 1u);
             bool run = false;
             uint32_t f = 0, u = 0;
-            if (gp.tasks != 0u) { // the gated launch: the first unit of a ready tile, longest-first
+            if constexpr (GATED) { // the gated launch: the first unit of a ready tile, longest-first
                 const int got = __builtin_amdgcn_readfirstlane(gated_fetch(&f, &u)); // (wave-uniform)
                 run = got > 0;
                 if (got < 0) {
@@ -2332,7 +2334,10 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
     auto primary = [&](auto stats_tag) {
         constexpr bool S = decltype(stats_tag)::value;
         const RtConsts* k0 = a.frames_host.k[0];
-        hipLaunchKernelGGL((k_trace<L, S>), dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
+        // the gated launch's own instantiation (nomadplains without STATS: the runtime never gates others)
+        constexpr bool kCanGate = L == RT_NOMADPLAINS && !S;
+        auto* kern = (kCanGate && a.gated.tasks) ? k_trace<L, S, kCanGate> : k_trace<L, S, false>;
+        hipLaunchKernelGGL(kern, dim3(pblocks), dim3(TraceThreads<L>::value), 0, a.stream, k0, a.frames,
                            a.perm2d, a.grad, m,
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.cpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,

@@ -141,7 +141,7 @@ struct rt_device_s {
     } graph_pre, graph_trace;
     unsigned long long graph_captures = 0, graph_launches = 0;
     // renders this device led: gated launches (prepass inside the trace) and prepass launches (rt_device_info)
-    unsigned long long gated_launches = 0, prepass_launches = 0;
+    unsigned long long gated_launches = 0, prepass_launches = 0, prestream_renders = 0;
     // frame tables (rt_kernels.h FrameTable): the batch's, and the split prepass's frame subset
     struct DevTable {
         FrameTable* d = nullptr;
@@ -958,6 +958,7 @@ int rt_device_info(rt_device d, int key, unsigned long long* out)
     switch (key) {
     case RT_INFO_GATED_LAUNCHES: *out = d->gated_launches; return RT_OK;
     case RT_INFO_PREPASS_LAUNCHES: *out = d->prepass_launches; return RT_OK;
+    case RT_INFO_PRESTREAM_RENDERS: *out = d->prestream_renders; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown rt_device_info key %d", key);
     }
 }
@@ -976,6 +977,10 @@ int rt_device_wait_event(rt_device d, void* ev)
     if (!d || !ev) return fail(RT_ERR_INVALID, "null device or event");
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipStreamWaitEvent(d->stream, (hipEvent_t)ev, 0));
+    // every later launch waits for the caller's event, the prepass-stream prepass of rt_terrain_render
+    // included: the next render prepasses in line on d->stream (which now waits), so it neither reads
+    // inputs the caller is still writing nor overwrites CameraResults the caller's stream still reads
+    d->serial_ok = false;
     return RT_OK;
 }
 
@@ -1362,7 +1367,10 @@ int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_
     HIP_TRY(hipStreamWaitEvent(main, d->ev_pre, 0));
     rc = terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false, PH_TRACE);
     d->serial_ok = rc == RT_OK;
-    if (rc == RT_OK) ++d->prepass_launches; // a render with a prepass launch (rt_device_info), on the prepass stream
+    if (rc == RT_OK) { // a render with a prepass launch (rt_device_info), on the prepass stream
+        ++d->prepass_launches;
+        ++d->prestream_renders;
+    }
     return rc;
 }
 
@@ -2152,6 +2160,9 @@ static int recorder_capture(rt_recorder r)
     if (int rc = device_bgrx(d)) return rc;
     HIP_TRY(hipMemcpyAsync(r->host, d->bgrx, (size_t)d->width * d->height * 4, hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
+    // the fail-safe word after the sync: a fused-prepass timeout raised by this frame's own k_order
+    // (asynchronous to rt_device_present's check) keeps the possibly wrong frame out of the video
+    if (int rc = host_flag_check(d)) return rc;
     return recorder_sample(r, r->host);
 }
 

@@ -224,8 +224,16 @@ class Device:
     def launch_info(self):
         """(gated launches, prepass launches) of the renders this device led (rt_device_info, ABI 7): the
         gated launch runs the prepass inside the trace kernel, a prepass launch is the ABI <= 6 sequence."""
+        return self._info((0, 1))
+
+    def prestream_renders(self):
+        """Renders whose prepass ran on the device's prepass stream, behind the previous frame's k_order
+        (rt_terrain_render with a frame in flight; RT_INFO_PRESTREAM_RENDERS)."""
+        return self._info((2,))[0]
+
+    def _info(self, keys):
         out = []
-        for key in (0, 1):
+        for key in keys:
             v = C.c_ulonglong()
             check(lib().rt_device_info(self._h, key, C.byref(v)), "device info")
             out.append(int(v.value))

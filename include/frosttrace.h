@@ -144,8 +144,10 @@ int rt_device_kernel_time(rt_device dev, double* total_ms, int* launches);
 int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned long long* launches);
 /* (ABI 7) Counters of the renders a device led: RT_INFO_GATED_LAUNCHES = renders whose prepass ran inside
  * their trace kernel (the gated launch), RT_INFO_PREPASS_LAUNCHES = renders with a prepass launch of
- * their own.  No reference counterpart (the tests check which sequence ran). */
-enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1 };
+ * their own, RT_INFO_PRESTREAM_RENDERS = those of them whose prepass ran on the device's prepass stream
+ * (rt_terrain_render with a frame in flight).  No reference counterpart (the tests check which sequence
+ * ran). */
+enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1, RT_INFO_PRESTREAM_RENDERS = 2 };
 int rt_device_info(rt_device dev, int key, unsigned long long* out);
 /* (ABI 6) Stream handoff without a host synchronisation.  `hip_event` is a hipEvent_t the caller
  * owns (a C++ host's, or torch.cuda.Event.cuda_event).  rt_device_wait_event: the work the device
@@ -230,8 +232,8 @@ void* rt_array_device_pointer(rt_array arr);
  * setTargetDepths (the last reader of CameraResults) and before this frame's setTargetDepths, so it
  * overlaps the previous frame's trace; the device stream stays the order a host sees (synchronise,
  * readbacks, events).  Any other call that touches the device's arrays or launches on it (a batch, the
- * feed, an ahead prepass, rt_compute_run, rt_array_unmap / write, a stream change) makes the next
- * render prepass in line.  A host writing CameraResults through rt_array_device_pointer on its own
+ * feed, an ahead prepass, rt_compute_run, rt_array_unmap / write, a stream change, rt_device_wait_event)
+ * makes the next render prepass in line.  A host writing CameraResults through rt_array_device_pointer on its own
  * must synchronise first.  Not for RT_DEVICE_GRAPH, RT_DEVICE_STATS or RT_DEVICE_GATED devices. */
 int rt_terrain_render(rt_compute camera_cs, rt_compute screen_cs, int shard_rank, int shard_count);
 /* rt_terrain_render_feed: rt_terrain_render that also hands the frame's 1024 CameraResults

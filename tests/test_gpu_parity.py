@@ -1628,11 +1628,14 @@ def test_fused_prepass_cameras_change_every_batch():
     ring.destroy()
 
 
-def test_fused_prepass_timeout_fails_safe():
+@pytest.mark.parametrize("recording", [False, True], ids=["plain", "recording"])
+def test_fused_prepass_timeout_fails_safe(recording, tmp_path):
     """a batch whose fused prepass never runs (RT_DEVICE_DEBUG_WITHHOLD_FUSE on the
     fusing device) times out in k_order; from then on every call that launches on or reads a device of
     the GPU fails with RT_ERR_STATE (a reference-shaped host that never calls rt_device_check cannot
-    read the frame), rt_device_check reports and clears it, and the next frames are bit-exact again."""
+    read the frame), rt_device_check reports and clears it, and the next frames are bit-exact again.
+    recording: a present() right after the trace -- before the asynchronous timeout fired --
+    still fails and writes no frame to the recorder's video."""
     import gpgpuraytrace_amd as G
     from gpgpuraytrace_amd import engine as E
     gold = GI.load()
@@ -1652,7 +1655,15 @@ def test_fused_prepass_timeout_fails_safe():
     E.prepass_ahead([a_ter])   # staged; traced before any other trace: in line
     E.prepass_ahead([b_ter])   # staged, then "fused" into a's trace, which withholds its tasks
     E.trace_ahead([a_ter])
+    rec = None
+    if recording:
+        rec = G.RecorderFactory.construct(b_dev, 25, True, str(tmp_path / "out.rgb32"))
+        rec.start()
     E.trace_ahead([b_ter])     # k_order waits 0.5 s for rays no kernel computes, then flags
+    if recording:
+        with pytest.raises(G.NativeError):
+            b_dev.present()    # the recorder's sync sees the flag: no frame written
+        assert rec.info()["frames"] == 0
     with pytest.raises(G.NativeError):
         b_dev.synchronize()
     with pytest.raises(G.NativeError):
@@ -1664,6 +1675,11 @@ def test_fused_prepass_timeout_fails_safe():
     b_dev.check()              # cleared
     b_ter.render_device()
     assert np.array_equal(b_dev.readback(), gold[key + "_rgba8"])
+    if rec is not None:
+        b_dev.present()
+        assert rec.info()["frames"] == 1
+        rec.stop()
+        rec.destroy()
     a_dev.destroy()
     b_dev.destroy()
 
@@ -1736,6 +1752,7 @@ def test_render_serial_prepass_stream_frames_in_flight(pair):
         E.shard_pack(dev, 0, 1, buf.data_ptr())
     dev.synchronize()
     assert dev.launch_info() == (0, len(bufs))  # every render ran its prepass launch (the first in line)
+    assert dev.prestream_renders() == len(bufs) - 1  # ... and every render after the first on the prepass stream
     for k, buf in enumerate(bufs):
         frame = P.unpack_host(np.zeros((h, w), np.uint32), buf.cpu().numpy().view(np.uint32), 0, 1)
         assert np.array_equal(frame.view(np.uint8).reshape(h, w, 4), gold[keys[k % 2] + "_rgba8"]), k
@@ -1743,5 +1760,51 @@ def test_render_serial_prepass_stream_frames_in_flight(pair):
     assert np.array_equal(_device_cells(ter), gold[last + "_cell_distance"])
     ter.get_camera_results()
     assert np.array_equal(ter.camera_view, gold[last + "_camera_results"])
+    dev.check()
+    dev.destroy()
+
+
+def test_render_wait_event_orders_prepass_stream():
+    """rt_device_wait_event orders EVERY later launch of the device, the next rt_terrain_render's
+    prepass included.  Frames A (reset pose) and B (look-down, its prepass on the prepass stream) render back
+    to back; the caller's stream waits for B (rt_device_record_event), spins ~20 ms, then copies B's
+    CameraResults, and hands back by rt_device_wait_event.  Frame C (reset pose) must not prepass into
+    CameraResults before that copy: the copy equals B's golden CameraResults, C equals its golden frame, and
+    C prepassed in line (the prepass-stream count stays at 1)."""
+    import torch
+    gold = GI.load()
+    specs = [GI.FRAMES[0], GI.FRAMES[1]]
+    land, _, w, h, aa, ms, ao = GI.unpack(specs[0])
+    cams = [GI.consts(w, h, GI.unpack(s)[1]) for s in specs]
+    keys = [GI.frame_key(*s) for s in specs]
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False)
+    torch.cuda.synchronize()
+
+    def render(i):
+        ter.set_camera(FixedCamera(cams[i]))
+        ter.update_terrain()
+        ter.set_time_of_day_vec(cams[i]["sun"])
+        ter.render_device()
+
+    render(0)
+    render(1)
+    assert dev.prestream_renders() == 1
+    done_b = torch.cuda.Event()
+    done_b.record()
+    dev.record_event(done_b.cuda_event)
+    stream = torch.cuda.current_stream()
+    stream.wait_event(done_b)
+    torch.cuda._sleep(50_000_000)  # ~20 ms on the caller's stream before it reads CameraResults
+    copy = torch.empty(1024 * 16, dtype=torch.uint8, device="cuda:0")
+    assert _hip().hipMemcpyAsync(copy.data_ptr(), ter.var_cam_results.device_pointer(), copy.numel(), 3,
+                                 stream.cuda_stream) == 0
+    read = torch.cuda.Event()
+    read.record(stream)
+    dev.wait_event(read.cuda_event)
+    render(0)
+    assert dev.prestream_renders() == 1  # C prepassed in line, behind the caller's event
+    got = copy.cpu().numpy().view(np.float32).reshape(1024, 4)
+    assert np.array_equal(got, gold[keys[1] + "_camera_results"])
+    assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
     dev.check()
     dev.destroy()
