@@ -17,7 +17,8 @@ with D batches in flight (engine.FrameRing).  Exactly --steps frames are timed: 
 split into ceil(steps / B) batches of near-equal size.  Every frame is computed in full and
 independently; value / ms_per_step are the steady-state frame rate; config.frame_latency_ms is
 one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
-in flight, config.single_frame_serial one frame at a time with no overlap, config.moving_camera
+in flight, config.single_frame_serial the reference's frame loop (render + present, one frame per call)
+on one device, config.moving_camera
 the timed loop's batching over --steps distinct frames of a camera path, config.sustained the
 timed loop's batches back to back for ~5 s (rates per ~1 s window: clocks under a long load), and
 (C3) config.ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
@@ -674,9 +675,9 @@ def main():
             "value": round(rays_per_frame * a.steps / dt_serial / 1e6, 3), "unit": "Mray/s",
             "ms_per_frame": round(dt_serial / a.steps * 1e3, 4),
             "primary_plus_shadow_mrays": round(ps * a.steps / dt_serial / 1e6, 3),
-            "how": f"rt_terrain_render, one frame per call on one device and its stream (B=1; each frame's prepass "
-                   f"on the device's prepass stream behind the previous frame's k_order, overlapping that frame's "
-                   f"trace tail), {a.steps} frames"}
+            "how": f"rt_terrain_render + rt_device_present, one frame per call on one device and its stream (B=1; "
+                   f"each frame's prepass on the device's prepass stream behind the previous frame's k_order, "
+                   f"overlapping that frame's trace tail), {a.steps} frames"}
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)

@@ -20,7 +20,7 @@ RT_DEVICE_GRAPH = 4
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
 RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the next batch's prepass tasks (timeout test)
 RT_DEVICE_GATED = 128  # ABI 7 (opt-in): the prepass inside the trace kernel, units gated on their cells' rays
-ABI_VERSION = 7  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
+ABI_VERSION = 8  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 
@@ -63,6 +63,7 @@ SIGNATURES = {
     "rt_device_kernel_time": (_i, [_vp, C.POINTER(C.c_double), C.POINTER(_i)]),
     "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     "rt_device_info": (_i, [_vp, _i, C.POINTER(C.c_ulonglong)]),
+    "rt_device_reserve_cus": (_i, [_vp, _i]),
     "rt_debug_spin": (_i, [_vp, _vp, C.c_ulonglong, C.c_ulonglong, _vp]),
     "rt_device_wait_event": (_i, [_vp, _vp]),
     "rt_device_record_event": (_i, [_vp, _vp]),

@@ -646,8 +646,29 @@ __device__ __forceinline__ void ao_count(uint32_t* __restrict__ aocc, uint32_t t
 {
     atomicAdd(&aocc[t >> 2], 1u << ((t & 3u) * 8u));
 }
-// UnitMap::fit with AO: a sample k_finish finishes carries kFinFlag in its byte (plain stores, k_trace)
+// UnitMap::fitm with AO: a sample k_finish finishes carries kFinFlag in its byte (plain stores, k_trace)
 constexpr uint32_t kFinFlag = 0x80u;
+// UnitMap::fit with its one AO ray per hit: a hit whose shadow ray outlived its first step has two rays left,
+// the long shadow S and the AO ray A, and whichever ends second stores the pixel (no k_finish).  Each ends
+// with one device atomic OR on the sample's aocc byte -- kRaceS, or kRaceA | occluded -- and the one whose OR
+// returns the other's bit is second.  S stores its colour (samples) and waits for it before its OR, so a
+// second A reads it from the L2 with sc1; both rays of a hit are one block's (one CU, one L2).  The second
+// clears the byte for the next launch.  k_finish's arithmetic (fit_pixel), so the same bits.
+constexpr uint32_t kRaceS = 0x40u, kRaceA = 0x20u;
+__device__ __forceinline__ uint32_t race_or(uint32_t* __restrict__ aocc, uint32_t t, uint32_t bits)
+{
+    const uint32_t sh = (t & 3u) * 8u;
+    return (atomicOr(&aocc[late(t) >> 2], bits << sh) >> sh) & 0xffu;
+}
+// a hit's 12-byte colour record (sample_store, one sample per pixel), written by another wave: sc1, waited
+__device__ __forceinline__ float4 ld_colour_fresh(const float4* samples, uint32_t t)
+{
+    typedef float v3f __attribute__((ext_vector_type(3)));
+    const float* p = reinterpret_cast<const float*>(samples) + 3u * late(t);
+    v3f v;
+    asm volatile("global_load_dwordx3 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+    return make_float4(v.x, v.y, v.z, 1.0f);
+}
 __device__ __forceinline__ uint32_t ao_occluded(const uint32_t* __restrict__ aocc, uint32_t t)
 {
     return (aocc[t >> 2] >> ((t & 3u) * 8u)) & 0x7fu;
@@ -922,10 +943,18 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
                                             uint32_t aux, const March<L, true>& st)
 {
     if (aux_ao(aux)) {
+        if (RT_FIT_RACE && m.fit && aux == kAuxAO) { // fit: the AO ray of a hit with a long shadow races it (kRaceS)
+            const uint32_t occ = st.d > 0.0f ? 1u : 0u;
+            if (race_or(aocc, t, kRaceA | occ) & kRaceS) { // second: the shadow's colour is in
+                if (!(RT_DIAG_SKIP & 2)) fit_store(k, m, fr, t, fit_pixel(ld_colour_fresh(samples, t), ao_factor(occ, 1)));
+                reinterpret_cast<uint8_t*>(aocc)[late(t)] = 0u;
+            }
+            return;
+        }
         if (st.d > 0.0f) {
             if (aux == kAuxAO) {
-                // fit: the hit's one AO ray, after the shading's kFinFlag store (ordered by the push)
-                if (m.fit) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)(kFinFlag | 1u);
+                // (RT_FIT_RACE 0) fit: the hit's one AO ray, after the shading's kFinFlag store (ordered by the push)
+                if (!RT_FIT_RACE && m.fit) reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)(kFinFlag | 1u);
                 // one AO ray per hit: its count has one writer, a plain byte store (no device atomic)
                 else if (k->ao_samples == 1) reinterpret_cast<uint8_t*>(aocc)[late(t)] = 1u;
                 else if (!(RT_DIAG_SKIP & 8)) ao_count(aocc, t);
@@ -949,6 +978,14 @@ __device__ __forceinline__ void long_finish(const RtConsts* k, const UnitMap& m,
         const float4 v = shade_finish(k, f0, fog, f1, st.d, st.f.w);
         if (m.fit && k->ao_samples == 0) {
             if (!(RT_DIAG_SKIP & 2)) fit_store(k, m, fr, t, fit_pixel(v, 1.0f));
+        } else if (RT_FIT_RACE && m.fit) { // its AO ray races it (kRaceA): the colour first, in L2 before the OR
+            sample_store(k, samples, t, v);
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint32_t ob = race_or(aocc, t, kRaceS);
+            if (ob & kRaceA) { // second
+                if (!(RT_DIAG_SKIP & 2)) fit_store(k, m, fr, t, fit_pixel(v, ao_factor(ob & 1u, 1)));
+                reinterpret_cast<uint8_t*>(aocc)[late(t)] = 0u;
+            }
         } else if (!(RT_DIAG_SKIP & 4)) {
             sample_store(k, samples, t, v);
         }
@@ -1374,6 +1411,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 count_noise(cl.nz);
                 cl.nz.phase = RT_PHASE_LONG;
             })
+            WT(wt[26]++;)
             if (live) march_step<L, true, true>(cl, st);
         }
     };
@@ -1439,6 +1477,7 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                     live = false;
                 }
                 if (!__ballot(live)) break;
+                WT(wt[25]++;)
                 if (live) {
                     auto dens = [&](f3 q0) {
                         uint32_t used;
@@ -1611,14 +1650,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
                 if (more && !(RT_DIAG_SKIP & 16)) fin_store<L>(aux == kAuxFinT ? fin + (size_t)FinRec<L>::N * t : finp + (size_t)FinRec<L>::N * aux, h);
             }
         });
-        // fit with AO: the hits whose long shadow races their AO ray are k_finish's.  Plain stores, no
-        // atomics (a device-scope atomic costs a 32-B HBM write on gfx950, L2 or not:
-        // scripts/ubench_atomic.hip): the sample's aocc byte becomes kFinFlag (its AO ray adds 1 if
-        // occluded) and the unit's hitmask word, zero from the unit, becomes nonzero (every writer
-        // stores the same value)
-        // fitm: the same for every hit whose pixel the AO counter's completion does not store (a long
-        // shadow, or no slot); a long shadow's slot marks it (bit 10: its completion stores the flagged count)
-        const bool kfin = valid && ((m.fit && k->ao_samples && more) || (m.fitm && (more || !aux_ao_slot(ao_aux))));
+        // fitm: the hits whose pixel the AO counter's completion does not store (a long shadow, or no slot)
+        // are k_finish's.  Plain stores, no atomics (a device-scope atomic costs a 32-B HBM write on gfx950,
+        // L2 or not: scripts/ubench_atomic.hip): the sample's aocc byte becomes kFinFlag and the unit's
+        // hitmask word, zero from the unit, becomes nonzero (every writer stores the same value); a long
+        // shadow's slot marks it (bit 10: its completion stores the flagged count).  (fit: no k_finish; a long
+        // shadow and its AO ray race in long_finish, kRaceS / kRaceA)
+        const bool kfin = valid && ((!RT_FIT_RACE && m.fit && k->ao_samples && more) ||
+                                    (m.fitm && (more || !aux_ao_slot(ao_aux)))); // (fit: the race, long_finish)
         if (kfin) {
             reinterpret_cast<uint8_t*>(aocc)[late(t)] = (uint8_t)kFinFlag;
             hitmask[t >> 6] = 1ull;
@@ -2035,12 +2074,13 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
                 if (drained && (kSegDrainAll || lp <= kSegQueue)) { // (drain-all: do_shadow refills nothing now)
                     do_shadow_seg();
-                    WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
+                    WT(const unsigned long long ds = __builtin_amdgcn_s_memrealtime() - t0; wt[4] += ds; wt[7]++;
+                       wt[23] += ds; wt[24]++;)
                     continue;
                 }
             }
             do_shadow();
-            WT(wt[4] += __builtin_amdgcn_s_memrealtime() - t0; wt[7]++;)
+            WT(const unsigned long long dl = __builtin_amdgcn_s_memrealtime() - t0; wt[4] += dl; wt[7]++; wt[27] += dl;)
             continue;
         }
         if (hp >= 64u || (drained && hp > 0u)) {
@@ -2269,9 +2309,8 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
                                    a.perm2d, a.grad, out, a.stats, ft);
         };
         using C512 = std::integral_constant<int, 512>;
-        using C256 = std::integral_constant<int, 256>;
         using L32 = std::integral_constant<int, 32>;
-        if (n <= 2) go(C256{}, L32{});
+        if (n <= 2) go(std::integral_constant<int, RT_PREPASS_BS1>{}, L32{});
         else if (n <= 4) go(C512{}, L32{});
         else if (n <= 16) go(C512{}, std::integral_constant<int, 8>{}); // 64 rays of 16 lanes per 1024 threads: same
         else go(C512{}, std::integral_constant<int, 4>{}); // > 16 frames: 128 rays of 4 lanes, <= 192 blocks for 24
@@ -2342,8 +2381,8 @@ void launch_split_l(const RtLaunch& a, uint32_t ox, uint32_t oy, uint32_t ex, ui
                            a.order, a.hitmask, a.samples, a.fin, a.finpool, a.cpool, a.hitq, a.spill_long, a.hit_cap,
                            a.long_spill_cap, a.aocc, a.queue, a.stats, kLongBatch, kRefillIdle, kCompactLive,
                            a.small_rings ? 64u : kLongRing, a.small_rings ? 8u : kFinSlots, a.fuse_next, a.gated);
-        // fit without AO: every hit pixel is final in k_trace
-        if (!(m.fit && a.ao_samples == 0))
+        // fit: every hit pixel is final in k_trace (with its AO ray, by the race of long_finish)
+        if (!(m.fit && (RT_FIT_RACE || a.ao_samples == 0)))
             hipLaunchKernelGGL(k_finish, dim3(fblocks), blk, 0, a.stream, k0, a.frames, m, a.hitmask, a.samples, a.aocc);
     };
     if (a.stats) primary(std::true_type{});

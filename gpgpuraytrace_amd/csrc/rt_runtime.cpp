@@ -116,6 +116,7 @@ struct rt_device_s {
     float4* scratch_cam = nullptr; // camera results for rt_terrain_render when the compute has none
     uint32_t* queue = nullptr;     // persistent-kernel work counters (RT_CTR_BYTES)
     int num_cus = 256;
+    int reserve_cus = 0;           // CUs the trace kernel leaves free (rt_device_reserve_cus)
     float4* samples = nullptr;     // per-sample buffers, sized for samples_cap samples
     float4* hitq = nullptr;       // k_trace's per-block hit queues and long-ray spill stacks (rt_spill_caps per block)
     float4* spill_long = nullptr;
@@ -534,7 +535,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.grad = s->d_grad;
     a.stats = (dev->flags & RT_DEVICE_STATS) ? dev->stats : nullptr;
     a.queue = dev->queue;
-    a.num_cus = dev->num_cus;
+    a.num_cus = dev->num_cus - dev->reserve_cus;
     a.samples = dev->samples;
     a.order = dev->order;
     a.hitmask = dev->hitmask;
@@ -961,6 +962,14 @@ int rt_device_info(rt_device d, int key, unsigned long long* out)
     case RT_INFO_PRESTREAM_RENDERS: *out = d->prestream_renders; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown rt_device_info key %d", key);
     }
+}
+
+int rt_device_reserve_cus(rt_device d, int n)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (n < 0 || n >= d->num_cus) return fail(RT_ERR_INVALID, "reserve 0..%d CUs, not %d", d->num_cus - 1, n);
+    d->reserve_cus = n;
+    return RT_OK;
 }
 
 int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned long long* launches)

@@ -523,7 +523,9 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
         const uint32_t v = (uint32_t)(r * LPR) + j;
         const bool need = v < (uint32_t)NV && (v == 0u || (int)v <= n_oct);
         float n = 0.0f;
-        if (__ballot(need)) {
+        // RT_SEG_ILP (not LOWREG): every round is evaluated, so the rounds' LDS round trips overlap
+        // (no branch between them); a dead round's value is masked to +0 below
+        if ((RT_SEG_ILP && !LOWREG) || __ballot(need)) {
             float sx = g.sx[r], sy = g.sy[r];
             if constexpr (LOWREG) { // the same scales from the LDS octave table, per round (no VGPRs held)
                 typedef __attribute__((address_space(3))) const float lds_f;

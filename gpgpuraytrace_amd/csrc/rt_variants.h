@@ -53,6 +53,11 @@
 #ifndef RT_SEG_QUEUE
 #define RT_SEG_QUEUE 4096
 #endif
+// 1: the octave-parallel density of the segment marches (not the LOWREG primary tail) evaluates all its
+// rounds without a branch between them, so their LDS round trips overlap (latency-bound tail steps)
+#ifndef RT_SEG_ILP
+#define RT_SEG_ILP 0
+#endif
 // 1: after the drain a long-ray wave refills nothing and hands back all its rays, so every post-drain long
 // ray marches on a segment (with RT_SEG_QUEUE large enough that waves take them as segments)
 #ifndef RT_SEG_DRAIN_ALL
@@ -101,6 +106,21 @@
 #define RT_ORDER_BATCH -1
 #endif
 
+// UnitMap::fit with one AO ray: 1 = a hit's long shadow and its AO ray race for its pixel (device atomic OR on
+// its aocc byte, the second stores it) and no k_finish runs; 0 = k_finish finishes those hits.  A/B only:
+// bit-exact (all GPU tests), but HBM 3.44x -> 5.38x the RGBA8 frame and 1.0% slower same box
+// (profiles/r06/fit_race_ab.md)
+#ifndef RT_FIT_RACE
+#define RT_FIT_RACE 0
+#endif
+
+// threads per block of a one-frame (and two-frame) camerarays prepass: 32 lanes per ray, so 8 (256) / 16 (512) /
+// 32 (1024) rays per block and 128 / 64 / 32 blocks of one CU each.  A serial frame's prepass runs in the previous
+// trace's tail, where CUs free one by one: fewer, larger blocks can start sooner
+#ifndef RT_PREPASS_BS1
+#define RT_PREPASS_BS1 256
+#endif
+
 // AO generator records (AO_SAMPLES >= 2): a hit's AO rays as one ring record expanded at refill (A/B only:
 // bit-exact, C5 HBM 5.9x -> 5.0x but 24% slower; profiles/r05/ao_gen_ab.md)
 #ifndef RT_AO_GEN
@@ -115,7 +135,8 @@
 #endif
 
 // ---- diagnostic builds (never in the product) ------------------------------------------------
-// RT_WAVE_TRACE          per-wave timeline of k_trace (make trace; scripts/wave_trace.py)
+// RT_WAVE_TRACE          per-wave timeline of k_trace (make trace; scripts/wave_trace.py); fields 23-27: segment-job
+//                        time / jobs / loop steps, lane-refill long-ray loop steps / time
 // RT_LIVE_HIST           histogram of live lanes per primary march step (rt_debug_live_hist)
 // RT_COUNT_PRIMARY_STEPS count live lanes per primary march step as noise (scripts/phase_util.py)
 // RT_COUNT_LONG_STEPS=k  the same for long-ray steps (1 always, 2 after the drain, 3 before)
@@ -132,7 +153,7 @@
 #define RT_DIAG_HITPAD 0
 #endif
 #ifdef RT_WAVE_TRACE
-#define RT_WT_FIELDS 23
+#define RT_WT_FIELDS 28
 #define RT_WT_MAX_WAVES 8192
 #define WT(...) __VA_ARGS__
 #else

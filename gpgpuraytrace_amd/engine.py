@@ -231,6 +231,11 @@ class Device:
         (rt_terrain_render with a frame in flight; RT_INFO_PRESTREAM_RENDERS)."""
         return self._info((2,))[0]
 
+    def reserve_cus(self, n):
+        """rt_device_reserve_cus (ABI 8): this device's trace kernels leave n CUs free for other streams'
+        kernels (rank 0's RCCL receive at N > 1)."""
+        check(lib().rt_device_reserve_cus(self._h, int(n)), "reserve_cus")
+
     def _info(self, keys):
         out = []
         for key in keys:

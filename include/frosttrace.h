@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 enum {
     RT_OK = 0,
@@ -149,6 +149,11 @@ int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned l
  * ran). */
 enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1, RT_INFO_PRESTREAM_RENDERS = 2 };
 int rt_device_info(rt_device dev, int key, unsigned long long* out);
+/* (ABI 8) The trace kernel of the renders this device leads launches (CUs - n) persistent blocks instead of
+ * one per CU (0 <= n < CUs; default 0), so n CUs stay free beside it for another stream's kernels -- a
+ * collective's (RCCL's receive on rank 0 at N > 1, which otherwise queues behind the other batch's trace
+ * until its tail) or a transport copy.  Same bits.  No reference counterpart. */
+int rt_device_reserve_cus(rt_device dev, int n);
 /* (ABI 6) Stream handoff without a host synchronisation.  `hip_event` is a hipEvent_t the caller
  * owns (a C++ host's, or torch.cuda.Event.cuda_event).  rt_device_wait_event: the work the device
  * queues from now on waits for the event -- e.g. buffers the caller filled on its own stream, then

@@ -74,6 +74,10 @@ def main():
                          "trace (rt_terrain_trace_batch) after an event recorded behind the previous batch's pack, "
                          "so the previous batch's finish and pack run before this k_trace takes the CUs and its "
                          "gather finds a CU beside it")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="N > 1: the trace kernels of the ranks below (--reserve-ranks) leave this many CUs free "
+                         "(rt_device_reserve_cus), so rank 0's receive need not wait for its other-batch trace")
+    ap.add_argument("--reserve-ranks", choices=["first", "all"], default="first")
     a = ap.parse_args()
     if a.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(a.hw_queues)  # before HIP starts (torch below)
@@ -113,10 +117,18 @@ def main():
         # coupled model: rank 0's receive starts (100 MHz GPU clock, per timed batch) and each pass's t0
         clock = torch.zeros(64, dtype=torch.int64, device="cuda:0")  # [0] t0 of the pass, [1 + i] rank 0's recv i
         recv_off = {}  # n -> [rank 0's receive start of timed batch i - its t0] (ticks)
+        trace_end_ms = {}  # n -> [rank 0's trace end of timed batch i - the pass's start] (ms, HIP events)
         xfer_ticks = int(a.transport_us * 100)  # 100 MHz
+
+        trace_end = {}  # timed batch i -> a timing event recorded on its stream right after its trace (rank 0)
 
         def transport(r, n, i):
             """i: the timed batch's index (-1: warm-up)"""
+            if r == 0 and i >= 0 and n > 1:
+                g = ((ring.frame - B) // B) % ring.depth
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(torch.cuda.ExternalStream(ring.slots[g * B][0].stream(), device="cuda:0"))
+                trace_end[i] = ev
             if n == 1 or a.transport_us <= 0:
                 return
             plan, packed = plan_for(n)
@@ -185,11 +197,17 @@ def main():
         for n in [int(x) for x in a.ns.split(",")]:
             worst, per = 0.0, []
             for r in (range(n) if a.ranks == "all" else [0]):
+                res = a.reserve_cus if n > 1 and (r == 0 or a.reserve_ranks == "all") else 0
+                for d, _ in ring.slots:
+                    d.reserve_cus(res)
                 for i in range(2 * a.depth):  # (lookahead: no ahead prepass across the timed region's edges)
                     step(r, n, ahead=i + 1 < 2 * a.depth)
                 torch.cuda.synchronize()
                 nb = max(1, a.frames // B)
                 G.lib().rt_debug_spin(None, None, 0, 0, clock.data_ptr())  # the pass's t0 (GPU clock)
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                trace_end.clear()
                 t0 = time.perf_counter()
                 for i in range(nb):
                     step(r, n, ahead=i + 1 < nb, i=i)
@@ -198,6 +216,8 @@ def main():
                 if r == 0 and n > 1 and a.transport_model == "coupled" and a.transport_us > 0:
                     c = clock.cpu().tolist()
                     recv_off[n] = [max(0, c[1 + i] - c[0]) for i in range(nb)]
+                if r == 0 and n > 1:
+                    trace_end_ms[n] = [round(ev0.elapsed_time(trace_end[i]), 4) for i in sorted(trace_end)]
                 per.append(round(ms, 4))
                 worst = max(worst, ms)
             if base is None:
@@ -206,6 +226,8 @@ def main():
                               "transport_us": a.transport_us, "transport_model": a.transport_model,
                               "direct_pack": a.direct_pack, "gate": a.gate,
                               **({"rank0_recv_start_ms": [round(x / 1e5, 4) for x in recv_off[n]]} if n in recv_off else {}),
+                              **({"rank0_trace_end_ms": trace_end_ms[n]} if n in trace_end_ms else {}),
+                              "reserve_cus": a.reserve_cus, "reserve_ranks": a.reserve_ranks,
                               "lookahead": int(ring.lookahead), "n": n, "worst_frame_ms": round(worst, 4),
                               "ceiling_vs_first": round(base / worst, 3), "ranks_ms": per}), flush=True)
         ring.destroy()

@@ -15,6 +15,7 @@
 #   prof=<bench.py args>         rocprofv3 --kernel-trace --stats over bench.py -> prof<i>/
 #   smoke                        __graft_entry__.smoke()
 #   py=<script and args>         any python script of the repo (diagnostics)
+#   pyprof=<script and args>     the same under rocprofv3 --kernel-trace -> prof<i>/
 #   vpy=<variant>:<script args>  the same against an A/B build _build/librt_hip_<variant>.so
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -69,6 +70,10 @@ for step in "$@"; do
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --traffic off --no-companions $arg) \
         > "$out/prof$i.log" 2>&1 || { tail -20 "$out/prof$i.log"; exit 1; }
       tail -1 "$out/prof$i.log";;
+    pyprof)  # pyprof=<script and args>: rocprofv3 --kernel-trace over a python script of the repo -> prof<i>/
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$out/prof$i" \
+        -o run -- python3 $GRAFT_REPO_ROOT/$arg) > "$out/prof$i.log" 2>&1 || { tail -20 "$out/prof$i.log"; exit 1; }
+      tail -3 "$out/prof$i.log";;
     py)
       timeout -k 10 600 python3 $arg > "$out/py$i.log" 2>&1 || { tail -20 "$out/py$i.log"; exit 1; }
       tail -5 "$out/py$i.log";;

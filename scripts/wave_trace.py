@@ -17,7 +17,7 @@ import with_variant  # noqa: E402
 
 with_variant.apply()
 
-F = 23
+F = 28
 
 
 def main():
@@ -80,6 +80,14 @@ def main():
     if tw.any():
         print(f"prepass tasks: {tw.sum()} waves, task time mean {tot(21)[tw].mean():.1f} max {tot(21)[tw].max():.1f} us; "
               f"last task end p50 {np.percentile(us(t[tw, 22] - t0), 50):.1f} max {us(t[tw, 22] - t0).max():.1f} us")
+    # long-ray march latency: segment jobs (fields 23-25: time, jobs, loop steps = the job's longest ray) and
+    # lane-refill long-ray batches (26, 27: loop steps, time), per loop step
+    sj, ss, lst, lt = t[:, 24].sum(), t[:, 25].sum(), t[:, 26].sum(), t[:, 27].sum()
+    if sj:
+        print(f"segment jobs: {sj}, {us(t[:, 23].sum()) / sj:.1f} us per job, {ss / sj:.1f} steps per job, "
+              f"{us(t[:, 23].sum()) / max(ss, 1):.3f} us per step")
+    if lst:
+        print(f"lane-refill long-ray loops: {lst} steps, {us(lt) / lst:.3f} us per step")
     # per SIMD busy (unit+shade+long) from hw_id: simd [5:4], cu [11:8], sh [12], se [15:13], + xcc
     hw = t[:, 10]
     simd = (hw >> 4) & 3

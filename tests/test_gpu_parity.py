@@ -1808,3 +1808,27 @@ def test_render_wait_event_orders_prepass_stream():
     assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
     dev.check()
     dev.destroy()
+
+
+
+@pytest.mark.parametrize("reserve", [1, 200])
+def test_reserve_cus_golden(reserve):
+    """rt_device_reserve_cus (ABI 8): the trace kernel launches (CUs - n) persistent blocks, leaving n CUs to
+    other streams' kernels (rank 0's receive at N > 1): the same frames bit for bit, at 1 and 200 CUs left out;
+    out-of-range counts are rejected."""
+    import gpgpuraytrace_amd as G
+    gold = GI.load()
+    spec = GI.FRAMES[1]
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    key = GI.frame_key(*spec)
+    dev, ter = make(GI.consts(w, h, pose), land, aa=aa, max_steps=ms, ao=ao)
+    for bad in (-1, 1 << 16):
+        with pytest.raises(G.NativeError):
+            dev.reserve_cus(bad)
+    dev.reserve_cus(reserve)
+    for _ in range(2):
+        ter.render_device()
+        assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])
+        assert np.array_equal(dev.readback(), gold[key + "_rgba8"])
+    dev.check()
+    dev.destroy()
