@@ -20,6 +20,7 @@ RT_DEVICE_GRAPH = 4
 RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries, its fin pool 8 (spill / fallback tests)
 RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the next batch's prepass tasks (timeout test)
 RT_DEVICE_GATED = 128  # ABI 7 (opt-in): the prepass inside the trace kernel, units gated on their cells' rays
+RT_DEVICE_DEBUG_GATE_STRESS = 512  # ABI 8, diagnostic: L1-warm consumers and a late CellDistance (gated hand-off test)
 ABI_VERSION = 8  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3

@@ -66,6 +66,10 @@ struct GatedPrepass {
     uint32_t* gate;   // RT_MAX_BATCH x RT_GATE_WORDS
     uint32_t* claims; // per order entry (tile of the batch): its units claimed so far
     uint32_t tasks;
+    // RT_DEVICE_DEBUG_GATE_STRESS (diagnostic): 1 = every wave first reads its frames' previous CellDistance with
+    // plain loads (the CU's L1 then holds lines the frame's last task rewrites), 2 = that task waits ~200 us
+    // before it stores CellDistance (more units start from CameraResults, the rest read the flagged cells late)
+    uint32_t debug;
 };
 
 struct RtLaunch {

@@ -1757,6 +1757,10 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
             if ((uint32_t)__builtin_amdgcn_readfirstlane(old) == RT_CAMERA_RES * RT_CAMERA_RES - RT_FUSE_RAYS_PER_TASK) {
                 // the frame's last task (its add returned last): every ray is in.  Its CellDistance (8-B sc1
                 // stores), waited, then the cells flag: later units read their brackets from it (gate_cells)
+                if (gp.debug & 2u) { // (RT_DEVICE_DEBUG_GATE_STRESS: late, ~200 us of the 100 MHz clock)
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__builtin_amdgcn_s_memrealtime() - t0 < 20000ull) __builtin_amdgcn_s_sleep(8);
+                }
                 const float4* cam = pft->cam[f];
                 typedef unsigned long long __attribute__((address_space(1))) gu64;
                 gu64* cells = (gu64*)pft->cells[f];
@@ -2028,6 +2032,14 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
 #if RT_GATE_STATIC
     uint32_t gp_next = first_qi;
 #endif
+    if constexpr (GATED) {
+        if (gp.debug & 1u) { // RT_DEVICE_DEBUG_GATE_STRESS: this CU's L1 holds the frames' previous CellDistance
+            float acc = 0.0f;
+            for (uint32_t f = 0; f < m.n_frames; ++f)
+                for (uint32_t i = lane; i < RT_CAMERA_RES * RT_CAMERA_RES; i += 64u) acc += ft->cells[f][i].x;
+            asm volatile("" : : "v"(acc));
+        }
+    }
     WT(wt[0] = __builtin_amdgcn_s_memrealtime();)
     for (;;) {
         if constexpr (L == RT_NOMADPLAINS) {

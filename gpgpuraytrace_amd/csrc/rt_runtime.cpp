@@ -561,7 +561,7 @@ RtLaunch make_launch(rt_device dev, Shader* s)
     a.wait_total = 0;
     a.after_order_fuse = nullptr;
     a.host_flag = host_flag_device(dev->ordinal);
-    a.gated = GatedPrepass{nullptr, nullptr, 0u};
+    a.gated = GatedPrepass{nullptr, nullptr, 0u, 0u};
     a.packed = 0;
     return a;
 }
@@ -767,7 +767,7 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
     const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS |
-                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED;
+                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED | RT_DEVICE_DEBUG_GATE_STRESS;
     if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -1635,7 +1635,9 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
                        (!fuse || (fuse->wait_ctl == nullptr && fuse->next.ctl == nullptr)) &&
                        b.s0->landscape == RT_NOMADPLAINS &&
                        (dev->flags & RT_DEVICE_GATED) && !(dev->flags & RT_DEVICE_STATS);
-    if (gated) la_scr.gated = GatedPrepass{dev->gate, dev->claims, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+    if (gated)
+        la_scr.gated = GatedPrepass{dev->gate, dev->claims, (uint32_t)n * (uint32_t)RT_FUSE_TASKS_PER_FRAME,
+                                    (dev->flags & RT_DEVICE_DEBUG_GATE_STRESS) ? 3u : 0u};
     // rt_terrain_prepass_ahead: ev_order follows the last read of the frames' CameraResults -- k_order's,
     // or with the gated launch k_trace's (recorded after the trace below)
     if (!graphs && dev->ev_order && !gated) {

@@ -108,7 +108,14 @@ __device__ __forceinline__ float noise3d_lattice(const NoiseView& nz, uint32_t t
                                                  float x1, float y1, float z, float ux_, float uy_, float uz)
 {
     // Pu = texel + Pu.z per channel (bytes <= 127+127: no carry), % 128
+#if RT_Z_MAD24
+    // (A/B) the replication as one v_mad_u32_u24 (4.2 issue cycles) instead of the v_mad_u64_u32 (4.9) LLVM picks
+    uint32_t w;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(w) : "v"(Z), "s"(0x01010101u), "v"(t));
+    w &= 0x7f7f7f7fu;
+#else
     uint32_t w = (t + Z * 0x01010101u) & 0x7f7f7f7fu; // AA, AB, BA, BB column indices at z
+#endif
     // entry i of either plane starts at byte i*256: one v_perm_b32 per corner builds
     // base | (index byte << 8) | lane slot ({w, so16} byte pick: 4+k = byte k of w, 0 / 2 = bytes
     // 0 / 2 of so16, 12 = 0); gz is the same address + 32768 (the load's offset field)

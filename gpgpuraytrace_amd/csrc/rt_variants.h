@@ -121,6 +121,11 @@
 #define RT_PREPASS_BS1 256
 #endif
 
+// (A/B) noise3d's z-layer replication t + Z * 0x01010101 as an inline v_mad_u32_u24
+#ifndef RT_Z_MAD24
+#define RT_Z_MAD24 0
+#endif
+
 // AO generator records (AO_SAMPLES >= 2): a hit's AO rays as one ring record expanded at refill (A/B only:
 // bit-exact, C5 HBM 5.9x -> 5.0x but 24% slower; profiles/r05/ao_gen_ab.md)
 #ifndef RT_AO_GEN

@@ -160,7 +160,7 @@ class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
     def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False,
-                 debug_withhold_fuse=False, gated=False):
+                 debug_withhold_fuse=False, gated=False, debug_gate_stress=False):
         """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
         entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
         shadows the fin[t] fallback; same bits).  debug_withhold_fuse: diagnostic
@@ -173,7 +173,8 @@ class Device:
                       | (_native.RT_DEVICE_GRAPH if graph else 0)
                       | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0)
                       | (_native.RT_DEVICE_DEBUG_WITHHOLD_FUSE if debug_withhold_fuse else 0)
-                      | (_native.RT_DEVICE_GATED if gated else 0))
+                      | (_native.RT_DEVICE_GATED if gated else 0)
+                      | (_native.RT_DEVICE_DEBUG_GATE_STRESS if debug_gate_stress else 0))
         self._h = None
 
     def create(self):

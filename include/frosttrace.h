@@ -49,7 +49,8 @@ enum {
      * rt_device_create rejects them, as every unknown flag */
     RT_DEVICE_DEBUG_SMALL_RINGS = 32u,
     RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64u,
-    RT_DEVICE_GATED = 128u
+    RT_DEVICE_GATED = 128u,
+    RT_DEVICE_DEBUG_GATE_STRESS = 512u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
@@ -68,7 +69,11 @@ enum {
  * units march 2-3x slower than alone), so it is not the default.
  * RT_DEVICE_DEBUG_WITHHOLD_FUSE (ABI 7, diagnostic): a trace this device leads that would run the next
  * batch's fused prepass (rt_terrain_trace_ahead) runs none of its tasks, so that batch's bounded wait
- * times out: the fail-safe's test (rt_device_check below). */
+ * times out: the fail-safe's test (rt_device_check below).
+ * RT_DEVICE_DEBUG_GATE_STRESS (ABI 8, diagnostic, with RT_DEVICE_GATED): the gated launch's cross-CU hand-off of a
+ * frame's CellDistance under stress -- every trace wave first reads the frame's previous CellDistance with
+ * plain loads (its CU's L1 holds lines that the frame's last prepass task then rewrites) and that task waits
+ * ~200 us before it stores them, so units read the flagged cells late, on CUs whose L1 holds the old ones. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };

@@ -31,12 +31,12 @@ class FixedCamera:
 
 
 def make(consts, land="nomadplains", aa=1, recording=False, max_steps=0, seed=300, rand_kind=0, stats=False,
-         ao=0, graph=False, small_rings=False, float_output=True, gated=False):
+         ao=0, graph=False, small_rings=False, float_output=True, gated=False, **dev_kw):
     """float_output=False: the product's device (RGBA8 only), where one sample per pixel with at most one
     AO ray finishes hit pixels in k_trace (UnitMap::fit) instead of through per-sample colours."""
     import gpgpuraytrace_amd as G
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, consts["width"], consts["height"], float_output=float_output,
-                                    stats=stats, graph=graph, small_rings=small_rings, gated=gated)
+                                    stats=stats, graph=graph, small_rings=small_rings, gated=gated, **dev_kw)
     assert dev is not None, G.lib().rt_last_error()
     ter = G.Terrain(dev, land, record_mode=recording, aa_samples=aa, max_steps=max_steps, noise_seed=seed,
                     rand_kind=rand_kind, ao_samples=ao)
@@ -1830,5 +1830,31 @@ def test_reserve_cus_golden(reserve):
         ter.render_device()
         assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"])
         assert np.array_equal(dev.readback(), gold[key + "_rgba8"])
+    dev.check()
+    dev.destroy()
+
+
+@pytest.mark.parametrize("spec", [GI.FRAMES[0], GI.FRAMES[1]], ids=["reset", "lookdown"])
+def test_gated_cells_handoff_l1_warm_late(spec):
+    """the gated launch's cross-CU CellDistance hand-off (the frame's last prepass task stores
+    it with 8-B sc1 stores, waits, then stores an sc1 flag; units poll the flag and read their cell with 4-B sc1
+    loads -- MI355X_MICROARCH.md's first hand-off row) under RT_DEVICE_DEBUG_GATE_STRESS: every trace wave
+    first reads the previous CellDistance with plain loads, so the consumers' L1 holds the old lines, and the
+    last task stores the new ones ~200 us late.  The previous CellDistance is poisoned; frames, CellDistance and
+    CameraResults equal the golden ones, twice (the second over the first's cells)."""
+    gold = GI.load()
+    land, pose, w, h, aa, ms, ao = GI.unpack(spec)
+    key = GI.frame_key(*spec)
+    dev, ter = make(GI.consts(w, h, pose), land, aa=aa, max_steps=ms, ao=ao, gated=True, debug_gate_stress=True)
+    junk = np.random.default_rng(11).uniform(-1e3, 1e3, (1024, 2)).astype(np.float32)
+    ter.var_cell_distance.write(junk)
+    for rep in range(2):
+        ter.render_device()
+        assert dev.launch_info()[0] == rep + 1
+        assert bits_equal(dev.readback_float(), gold[key + "_rgba32f"]), rep
+        assert np.array_equal(dev.readback(), gold[key + "_rgba8"]), rep
+        assert np.array_equal(_device_cells(ter), gold[key + "_cell_distance"]), rep
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, gold[key + "_camera_results"]), rep
     dev.check()
     dev.destroy()
