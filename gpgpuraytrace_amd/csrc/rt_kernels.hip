@@ -2083,6 +2083,8 @@ __global__ void __launch_bounds__(TraceThreads<L>::value) k_trace(const RtConsts
         // block's backlog at the drain -- what its post-drain tail marches -- is small
         const uint32_t lb_now = (RT_NEAR_UNITS > 0 && vload(q.near_end) != 0u) ? (uint32_t)RT_NEAR_LONG_BATCH : long_batch;
         if (lp >= lb_now || (drained && lp > 0u)) {
+            // (A/B) near the queue's end the long-ray waves issue ahead of the unit waves (RT_LONG_PRIO)
+            if (RT_LONG_PRIO > 0 && lb_now != long_batch) __builtin_amdgcn_s_setprio(RT_LONG_PRIO);
             if constexpr (L == RT_NOMADPLAINS && kSegLanes > 0u) {
                 if (drained && (kSegDrainAll || lp <= kSegQueue)) { // (drain-all: do_shadow refills nothing now)
                     do_shadow_seg();
@@ -2322,7 +2324,7 @@ void launch_camerarays_l(const RtLaunch& a, float4* out, const FrameTable* ft, u
         };
         using C512 = std::integral_constant<int, 512>;
         using L32 = std::integral_constant<int, 32>;
-        if (n <= 2) go(std::integral_constant<int, RT_PREPASS_BS1>{}, L32{});
+        if (n <= 2) go(std::integral_constant<int, RT_PREPASS_BS1>{}, std::integral_constant<int, RT_PREPASS_LPR1>{});
         else if (n <= 4) go(C512{}, L32{});
         else if (n <= 16) go(C512{}, std::integral_constant<int, 8>{}); // 64 rays of 16 lanes per 1024 threads: same
         else go(C512{}, std::integral_constant<int, 4>{}); // > 16 frames: 128 rays of 4 lanes, <= 192 blocks for 24

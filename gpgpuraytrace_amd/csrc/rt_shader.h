@@ -506,11 +506,45 @@ __device__ __forceinline__ SegOctaves<LPR> seg_octaves(const Ctx& c, uint32_t j)
     return g;
 }
 
-// LOWREG: the octave values are gathered one at a time inside the weighted sum (each gather
-// waits for the previous fma), so one gathered value is live instead of all 18, and each round's
-// octave scales come from the LDS octave table (nz.oct: the same np_scale / np_scale_y values)
-// instead of registers: for callers that hold other rays' state across the march (k_trace's
-// primary_seg), at the cost of a serial chain.
+// The weighted sum for segments of LPR <= 16 lanes (a segment then lies inside one 16-lane DPP row):
+// octave N's value is nv[N / LPR] of lane base + N % LPR, and the segment's first lane reads it with a
+// DPP row shift (v_mov_b32 row_shl:k, lane i <- lane i + k of its row) that the fma takes as its
+// operand: no LDS round trip, no lane-index VGPR, and the chain's 17 fmas are its only serial part.
+// The other lanes of the segment run the same instructions on values from the wrong lanes; the
+// caller broadcasts the first lane's result (seg_bcast).
+template <int LPR, int N, int R>
+__device__ __forceinline__ float seg_chain_dpp(const float (&nv)[R], const float (&rcp)[RT_NP_OCTAVES + 1], float s)
+{
+    if constexpr (N > RT_NP_OCTAVES) {
+        return s;
+    } else {
+        constexpr int k = N % LPR;
+        float x;
+        if constexpr (k == 0) x = nv[N / LPR];
+        else x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(nv[N / LPR]), 0x100 + k, 0xf, 0xf, false));
+        return seg_chain_dpp<LPR, N + 1>(nv, rcp, fma(x, rcp[N], s));
+    }
+}
+
+// every lane of an LPR-lane segment (LPR 4, 8 or 16) <- the segment's first lane, in DPP moves:
+// quad_perm [0,0,0,0] (each quad <- its lane 0), then row_shr:4 into banks 1 and 3 and row_shr:8 into
+// banks 2 and 3 (the lanes outside the bank mask keep their value)
+template <int LPR>
+__device__ __forceinline__ float seg_bcast(float x)
+{
+    static_assert(LPR == 4 || LPR == 8 || LPR == 16, "DPP broadcast within one 16-lane row");
+    int v = __float_as_int(x);
+    v = __builtin_amdgcn_update_dpp(v, v, 0x00, 0xf, 0xf, false);
+    if constexpr (LPR >= 8) v = __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xa, false);
+    if constexpr (LPR >= 16) v = __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xc, false);
+    return __int_as_float(v);
+}
+
+// LOWREG (LPR 32 only; the DPP form holds no gathered values): the octave values are gathered one at a
+// time inside the weighted sum (each gather waits for the previous fma), so one gathered value is live
+// instead of all 18.  LOWREG (any LPR): each round's octave scales come from the LDS octave table
+// (nz.oct: the same np_scale / np_scale_y values) instead of registers: for callers that hold other
+// rays' state across the march (k_trace's primary_seg).
 template <int LPR, bool LOWREG = false>
 __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const SegOctaves<LPR>& g, f3 p, uint32_t j,
                                                          uint32_t base, uint32_t* octaves)
@@ -552,7 +586,11 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
         nv[r] = need ? n : 0.0f;
     }
     float s = 0.0f, on0;
-    if constexpr (LOWREG) {
+    constexpr bool kDpp = RT_SEG_DPP && LPR <= 16;
+    if constexpr (kDpp) {
+        s = seg_chain_dpp<LPR, 1>(nv, g.rcp, s);
+        on0 = nv[0]; // (the first lane's own v = 0)
+    } else if constexpr (LOWREG) {
 #pragma unroll
         for (int N = 1; N <= RT_NP_OCTAVES; ++N) {
             int idx = (int)(base + (uint32_t)(N % LPR));
@@ -577,6 +615,7 @@ __device__ __forceinline__ float density_nomadplains_seg(const Ctx& c, const Seg
     const float lb = rtm::sat((-p1.y + 10.0f) * 1.6f);
     const float lift = __ballot(lb != 0.0f) ? rtm::pow_nonneg_flat(lb, 1.5f) : 0.0f;
     s = fma(lift, 19.0f, s);
+    if constexpr (kDpp) return seg_bcast<LPR>(d + s); // the first lane's density to its segment
     return d + s;
 }
 

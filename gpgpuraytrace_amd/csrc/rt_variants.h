@@ -18,6 +18,11 @@
 #ifndef RT_NEAR_LONG_BATCH
 #define RT_NEAR_LONG_BATCH 16
 #endif
+// (A/B) s_setprio of a long-ray wave once the near-end mode is on (0: off; a unit resets it to 0).  2: the N = 8
+// shard simulation and bench within noise, the post-drain tail unchanged (profiles/r06/dpp_ab.md)
+#ifndef RT_LONG_PRIO
+#define RT_LONG_PRIO 0
+#endif
 // lanes idle before a long-ray wave refills them from the ring (amortises the refill's prologue)
 #ifndef RT_REFILL_IDLE
 #define RT_REFILL_IDLE 4
@@ -57,6 +62,12 @@
 // rounds without a branch between them, so their LDS round trips overlap (latency-bound tail steps)
 #ifndef RT_SEG_ILP
 #define RT_SEG_ILP 0
+#endif
+// 1: density_nomadplains_seg with LPR <= 16 (k_trace's segment marches, primary tail and prepass tasks) sums
+// the octaves on the segment's first lane from DPP row shifts and broadcasts the density (DPP); 0: every lane
+// gathers the 18 values with ds_bpermute (through the LDS pipe)
+#ifndef RT_SEG_DPP
+#define RT_SEG_DPP 1
 #endif
 // 1: after the drain a long-ray wave refills nothing and hands back all its rays, so every post-drain long
 // ray marches on a segment (with RT_SEG_QUEUE large enough that waves take them as segments)
@@ -114,11 +125,17 @@
 #define RT_FIT_RACE 0
 #endif
 
-// threads per block of a one-frame (and two-frame) camerarays prepass: 32 lanes per ray, so 8 (256) / 16 (512) /
-// 32 (1024) rays per block and 128 / 64 / 32 blocks of one CU each.  A serial frame's prepass runs in the previous
-// trace's tail, where CUs free one by one: fewer, larger blocks can start sooner
+// threads per block of a one-frame (and two-frame) camerarays prepass (RT_PREPASS_LPR1 lanes per ray; one block per
+// CU, as it holds the noise tables).  A serial frame's prepass runs in the previous trace's tail, where CUs free one
+// by one: fewer, larger blocks can start sooner, but 32 rays to a CU march slower than 8 or 16
 #ifndef RT_PREPASS_BS1
 #define RT_PREPASS_BS1 256
+#endif
+// lanes per ray of that prepass (32: one noise round per step and ds_bpermute gathers; 16 / 8: 2 / 3 rounds and
+// the DPP sum, RT_SEG_DPP).  16 lanes (16 rays a block, 64 blocks): the serial frame loop 3.369 -> 3.311 ms per
+// frame same box (4 runs each; 8 lanes / 128 blocks and 16 lanes / 32 blocks slower; profiles/r06/dpp_ab.md)
+#ifndef RT_PREPASS_LPR1
+#define RT_PREPASS_LPR1 16
 #endif
 
 // (A/B) noise3d's z-layer replication t + Z * 0x01010101 as an inline v_mad_u32_u24
