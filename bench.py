@@ -18,7 +18,8 @@ split into ceil(steps / B) batches of near-equal size.  Every frame is computed 
 independently; value / ms_per_step are the steady-state frame rate; config.frame_latency_ms is
 one batch at a time, config.single_frame one frame per launch sequence (B = 1) with three frames
 in flight, config.single_frame_serial the reference's frame loop (render + present, one frame per call)
-on one device, config.moving_camera
+on one device, config.single_frame_deferred the same loop on an RT_DEVICE_DEFERRED device (each render
+launches the previous frame's trace with its own prepass inside it), config.moving_camera
 the timed loop's batching over --steps distinct frames of a camera path, config.sustained the
 timed loop's batches back to back for ~5 s (rates per ~1 s window: clocks under a long load), and
 (C3) config.ref_semantics the same machinery at the reference's own semantics (uncapped, no AO).
@@ -648,6 +649,26 @@ def main():
             d0.present()
         d0.synchronize()
         dt_serial = time.perf_counter() - ts
+        # the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each render launches the previous frame's
+        # trace with its own frame's prepass inside it
+        ddev = E.DeviceFactory.construct(E.DeviceAPI.HIP, W, H, gpu=local, deferred=True)
+        dter = E.Terrain(ddev, a.landscape, max_steps=a.max_steps, ao_samples=a.ao)
+        dter.create()
+        assert dter.reload(), G.lib().rt_last_error()
+        dter.set_camera(camera)
+        dter.set_time_of_day(0.3)
+        for _ in range(3):
+            dter.render_device()
+            ddev.present()
+        ddev.synchronize()
+        ts = time.perf_counter()
+        for _ in range(a.steps):
+            dter.render_device()
+            ddev.present()
+        ddev.synchronize()
+        dt_deferred = time.perf_counter() - ts
+        deferred_fused = ddev.deferred_fused()
+        ddev.destroy()
     ring.destroy()
     if world == 1 and not a.no_companions:
         # B = 1 with three frames in flight (D3D11's default maximum frame latency, the reference
@@ -678,6 +699,14 @@ def main():
             "how": f"rt_terrain_render + rt_device_present, one frame per call on one device and its stream (B=1; "
                    f"each frame's prepass on the device's prepass stream behind the previous frame's k_order, "
                    f"overlapping that frame's trace tail), {a.steps} frames"}
+        companions["single_frame_deferred"] = {
+            "value": round(rays_per_frame * a.steps / dt_deferred / 1e6, 3), "unit": "Mray/s",
+            "ms_per_frame": round(dt_deferred / a.steps * 1e3, 4),
+            "primary_plus_shadow_mrays": round(ps * a.steps / dt_deferred / 1e6, 3),
+            "fused_prepasses": deferred_fused,
+            "how": f"the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each rt_terrain_render launches the "
+                   f"previous frame's setTargetDepths + trace with its own frame's prepass inside that trace "
+                   f"kernel, the last frame by rt_device_synchronize, {a.steps} frames"}
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)

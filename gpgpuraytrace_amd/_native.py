@@ -21,7 +21,8 @@ RT_DEVICE_DEBUG_SMALL_RINGS = 32  # ABI 4: k_trace's long ring holds 64 entries,
 RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the next batch's prepass tasks (timeout test)
 RT_DEVICE_GATED = 128  # ABI 7 (opt-in): the prepass inside the trace kernel, units gated on their cells' rays
 RT_DEVICE_DEBUG_GATE_STRESS = 512  # ABI 8, diagnostic: L1-warm consumers and a late CellDistance (gated hand-off test)
-ABI_VERSION = 8  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
+RT_DEVICE_DEFERRED = 1024  # ABI 9: a render's trace launches with the next render (which fuses its prepass into it)
+ABI_VERSION = 9  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3
 

@@ -142,7 +142,17 @@ struct rt_device_s {
     } graph_pre, graph_trace;
     unsigned long long graph_captures = 0, graph_launches = 0;
     // renders this device led: gated launches (prepass inside the trace) and prepass launches (rt_device_info)
-    unsigned long long gated_launches = 0, prepass_launches = 0, prestream_renders = 0;
+    unsigned long long gated_launches = 0, prepass_launches = 0, prestream_renders = 0, deferred_fused = 0;
+    // RT_DEVICE_DEFERRED: the last rt_terrain_render's frame, its prepass queued (or run inside the trace before)
+    // and both constant blocks up, whose setTargetDepths + trace are not launched yet: the next rt_terrain_render
+    // launches them with its own frame's prepass fused into that trace; any other call that launches on, reads
+    // or reconfigures the device launches them first (defer_flush)
+    struct Deferred {
+        struct rt_compute_s* cam = nullptr;
+        struct rt_compute_s* scr = nullptr;
+        int rank = 0, count = 1;
+        bool pending = false;
+    } defer;
     // frame tables (rt_kernels.h FrameTable): the batch's, and the split prepass's frame subset
     struct DevTable {
         FrameTable* d = nullptr;
@@ -191,6 +201,7 @@ struct rt_device_s {
 
 static int recorder_capture(rt_recorder r);
 static void recorder_detach(rt_recorder r);
+static int defer_flush(rt_device d);
 
 namespace {
 // Work on stream s that touches device d's frames (their CameraResults) comes after a pending ahead
@@ -767,7 +778,8 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     if (!out || width <= 0 || height <= 0) return fail(RT_ERR_INVALID, "bad device arguments");
     *out = nullptr;
     const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS |
-                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED | RT_DEVICE_DEBUG_GATE_STRESS;
+                           RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED | RT_DEVICE_DEBUG_GATE_STRESS |
+                           RT_DEVICE_DEFERRED;
     if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -803,7 +815,11 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     return RT_OK;
 }
 
-void rt_device_destroy(rt_device d) { delete d; }
+void rt_device_destroy(rt_device d)
+{
+    if (d) (void)defer_flush(d); // a pending frame is traced (the destructor then drains the stream)
+    delete d;
+}
 
 int rt_stream_refs(void* hip_stream)
 {
@@ -818,14 +834,19 @@ int rt_device_present(rt_device d)
     HIP_TRY(hipGetLastError());
     if (int rc = host_flag_check(d)) return rc;
     // DeviceDirect3D.cpp:242-256: while recording, the frame goes to the recorder
-    if (d->recorder && rt_recorder_is_recording(d->recorder) == 1) return recorder_capture(d->recorder);
+    if (d->recorder && rt_recorder_is_recording(d->recorder) == 1) {
+        if (int rc = defer_flush(d)) return rc;
+        return recorder_capture(d->recorder);
+    }
     return RT_OK;
 }
 
 int rt_device_flush(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
-    // HIP submits at launch; flush only surfaces asynchronous launch errors.
+    // HIP submits at launch; flush launches a deferred frame (RT_DEVICE_DEFERRED) and surfaces asynchronous
+    // launch errors.
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipGetLastError());
     return RT_OK;
 }
@@ -833,6 +854,7 @@ int rt_device_flush(rt_device d)
 int rt_device_synchronize(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipStreamSynchronize(d->stream));
     return host_flag_check(d);
 }
@@ -842,6 +864,7 @@ int rt_device_readback(rt_device d, void* dst, size_t row_pitch)
     if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
     if (row_pitch == 0) row_pitch = (size_t)d->width * 4;
     if (row_pitch < (size_t)d->width * 4) return fail(RT_ERR_INVALID, "row pitch smaller than a row");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->fb8, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
                              hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -862,6 +885,7 @@ int rt_device_readback_bgrx(rt_device d, void* dst, size_t row_pitch)
     if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
     if (row_pitch == 0) row_pitch = (size_t)d->width * 4;
     if (row_pitch < (size_t)d->width * 4) return fail(RT_ERR_INVALID, "row pitch smaller than a row");
+    if (int rc = defer_flush(d)) return rc;
     if (int rc = device_bgrx(d)) return rc;
     HIP_TRY(hipMemcpy2DAsync(dst, row_pitch, d->bgrx, (size_t)d->width * 4, (size_t)d->width * 4, d->height,
                              hipMemcpyDeviceToHost, d->stream));
@@ -873,6 +897,7 @@ int rt_device_readback_float(rt_device d, float* dst)
 {
     if (!d || !dst) return fail(RT_ERR_INVALID, "bad readback arguments");
     if (!d->fb32) return fail(RT_ERR_STATE, "device created without RT_DEVICE_FLOAT_OUTPUT");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipMemcpyAsync(dst, d->fb32, (size_t)d->width * d->height * 16, hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
     return host_flag_check(d);
@@ -886,14 +911,24 @@ int rt_device_size(rt_device d, int* w, int* h)
     return RT_OK;
 }
 
-void* rt_device_framebuffer(rt_device d) { return d ? (void*)d->fb8 : nullptr; }
-void* rt_device_stream(rt_device d) { return d ? (void*)d->stream : nullptr; }
+// (the caller reads or enqueues behind the frame: a deferred one is launched first)
+void* rt_device_framebuffer(rt_device d)
+{
+    if (!d || defer_flush(d)) return nullptr;
+    return (void*)d->fb8;
+}
+void* rt_device_stream(rt_device d)
+{
+    if (!d || defer_flush(d)) return nullptr;
+    return (void*)d->stream;
+}
 
 int rt_device_set_stream(rt_device d, void* s)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
     hipStream_t want = s ? (hipStream_t)s : d->own_stream;
     if (want == d->stream) return RT_OK;
+    if (int rc = defer_flush(d)) return rc; // a pending frame goes on the stream it was queued behind
     if (want != d->own_stream) stream_ref(want);             // borrow (tracked if another device owns it)
     if (d->stream != d->own_stream) stream_unref(d->stream); // return the previous loan
     d->stream = want;
@@ -904,6 +939,7 @@ int rt_device_set_stream(rt_device d, void* s)
 int rt_device_stats_sized(rt_device d, rt_stats* out, size_t size, int reset)
 {
     if (!d || !out) return fail(RT_ERR_INVALID, "bad arguments");
+    if (int rc = defer_flush(d)) return rc;
     RtStats h;
     HIP_TRY(hipMemcpyAsync(&h, d->stats, sizeof(h), hipMemcpyDeviceToHost, d->stream));
     HIP_TRY(hipStreamSynchronize(d->stream));
@@ -932,6 +968,7 @@ int rt_device_set_profiling(rt_device d, int enable)
 int rt_device_kernel_time(rt_device d, double* total_ms, int* launches)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipStreamSynchronize(d->stream));
     double tot = 0.0;
     for (size_t i = 0; i < d->ev_used; ++i) {
@@ -960,6 +997,7 @@ int rt_device_info(rt_device d, int key, unsigned long long* out)
     case RT_INFO_GATED_LAUNCHES: *out = d->gated_launches; return RT_OK;
     case RT_INFO_PREPASS_LAUNCHES: *out = d->prepass_launches; return RT_OK;
     case RT_INFO_PRESTREAM_RENDERS: *out = d->prestream_renders; return RT_OK;
+    case RT_INFO_DEFERRED_FUSED: *out = d->deferred_fused; return RT_OK;
     default: return fail(RT_ERR_INVALID, "unknown rt_device_info key %d", key);
     }
 }
@@ -984,6 +1022,7 @@ int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned lon
 int rt_device_wait_event(rt_device d, void* ev)
 {
     if (!d || !ev) return fail(RT_ERR_INVALID, "null device or event");
+    if (int rc = defer_flush(d)) return rc; // a pending frame was asked for before the caller's event
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipStreamWaitEvent(d->stream, (hipEvent_t)ev, 0));
     // every later launch waits for the caller's event, the prepass-stream prepass of rt_terrain_render
@@ -996,6 +1035,7 @@ int rt_device_wait_event(rt_device d, void* ev)
 int rt_device_record_event(rt_device d, void* ev)
 {
     if (!d || !ev) return fail(RT_ERR_INVALID, "null device or event");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipEventRecord((hipEvent_t)ev, d->stream));
     return RT_OK;
@@ -1004,6 +1044,7 @@ int rt_device_record_event(rt_device d, void* ev)
 int rt_device_check(rt_device d)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (int rc = defer_flush(d)) return rc;
     HIP_TRY(hipSetDevice(d->ordinal));
     HIP_TRY(hipStreamSynchronize(d->stream));
     uint32_t flags = 0;
@@ -1032,6 +1073,7 @@ int rt_texture_init(rt_texture t, int dims, int fmt, int w, int h, const void* d
     (void)binding;
     (void)cpu;
     if (!t || !data || w <= 0) return fail(RT_ERR_INVALID, "bad texture arguments");
+    if (int rc = defer_flush(t->dev)) return rc; // a pending frame reads the texels it replaces
     if (dims != RT_TEXTURE_2D) return fail(RT_ERR_UNSUPPORTED, "only 2D textures are used on the hot path");
     if (fmt == RT_FORMAT_UNKNOWN) return fail(RT_ERR_UNSUPPORTED, "unknown texture format");
     if (t->data) HIP_TRY(hipFree(t->data));
@@ -1051,6 +1093,7 @@ int rt_texture_init(rt_texture t, int dims, int fmt, int w, int h, const void* d
 void rt_texture_destroy(rt_texture t)
 {
     if (!t) return;
+    (void)defer_flush(t->dev);
     auto& v = t->dev->textures;
     v.erase(std::remove(v.begin(), v.end(), t), v.end());
     if (t->data) (void)hipFree(t->data);
@@ -1071,6 +1114,7 @@ int rt_compute_create(rt_device d, rt_compute* out)
 void rt_compute_destroy(rt_compute c)
 {
     if (!c) return;
+    (void)defer_flush(c->dev);
     (void)hipStreamSynchronize(c->dev->stream);
     auto& v = c->dev->computes;
     v.erase(std::remove(v.begin(), v.end(), c), v.end());
@@ -1144,6 +1188,7 @@ int rt_compute_swap(rt_compute c)
 {
     if (!c) return fail(RT_ERR_INVALID, "null compute");
     if (!c->new_shader) return 0;
+    if (int rc = defer_flush(c->dev)) return rc;
     if (c->shader) {
         (void)hipStreamSynchronize(c->dev->stream); // kernels may still read the old shader's buffers
         delete c->shader;
@@ -1189,6 +1234,8 @@ int rt_compute_set_texture(rt_compute c, int stage, rt_texture t)
 {
     if (!c || stage < 0 || stage >= 16) return fail(RT_ERR_INVALID, "bad arguments");
     if (!c->shader) return fail(RT_ERR_STATE, "no current shader");
+    if (c->shader->textures[stage] != t)
+        if (int rc = defer_flush(c->dev)) return rc;
     c->shader->textures[stage] = t;
     return RT_OK;
 }
@@ -1201,6 +1248,7 @@ int rt_compute_run(rt_compute c, unsigned dx, unsigned dy, unsigned dz)
     rt_device dev = c->dev;
     int rc = host_flag_check(dev);
     if (rc) return rc;
+    if ((rc = defer_flush(dev))) return rc;
     dev->serial_ok = false; // a dispatch of its own (reads / writes the arrays on the stream)
     rc = check_texture(s);
     if (rc) return rc;
@@ -1287,6 +1335,7 @@ void* rt_array_map(rt_array a)
         fail(RT_ERR_STATE, "array %s not created", a->name.c_str());
         return nullptr;
     }
+    if (defer_flush(a->dev)) return nullptr;
     hipStream_t s = a->dev->stream;
     if (ahead_wait(a->dev, s) != 0 ||
         hipMemcpyAsync(a->host.data(), a->dev_ptr, a->host.size(), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1303,6 +1352,7 @@ int rt_array_unmap(rt_array a)
     if (!a) return fail(RT_ERR_INVALID, "null array");
     if (!a->uav) return fail(RT_ERR_UNSUPPORTED, "unmap not supported on SRV array %s", a->name.c_str());
     if (!a->dev_ptr) return fail(RT_ERR_STATE, "array not created");
+    if (int rc = defer_flush(a->dev)) return rc;
     a->dev->serial_ok = false; // the upload is ordered on the stream only: the next render prepasses in line
     return a->staging.upload(a->dev->stream, a->dev_ptr, a->host.data(), a->host.size());
 }
@@ -1312,17 +1362,23 @@ int rt_array_write(rt_array a, const void* data)
     if (!a || !data) return fail(RT_ERR_INVALID, "bad arguments");
     if (a->uav) return fail(RT_ERR_UNSUPPORTED, "write not supported on UAV array %s", a->name.c_str());
     if (!a->dev_ptr) return fail(RT_ERR_STATE, "array %s not created", a->name.c_str());
+    if (int rc = defer_flush(a->dev)) return rc;
     a->dev->serial_ok = false;
     return a->staging.upload(a->dev->stream, a->dev_ptr, data, (size_t)a->elements * a->stride);
 }
 
 size_t rt_array_stride(rt_array a) { return a ? (size_t)a->stride : 0; }
-void* rt_array_device_pointer(rt_array a) { return a ? a->dev_ptr : nullptr; }
+void* rt_array_device_pointer(rt_array a) // (the caller reads it behind the frame: a deferred one is launched first)
+{
+    if (!a || defer_flush(a->dev)) return nullptr;
+    return a->dev_ptr;
+}
 
 // ---- Terrain::render on the device -------------------------------------------
 // PH_STAGE (rt_terrain_prepass_ahead, fused): upload the camerarays constants and the frame table a
-// fusing k_trace reads, launch nothing
-enum { PH_PRE = 1, PH_TRACE = 2, PH_STAGE = 4 };
+// fusing k_trace reads, launch nothing.  PH_KEEP (with PH_TRACE; RT_DEVICE_DEFERRED): upload no constant
+// block -- the frame's went up when it was rendered, and the host copies may hold the next frame's since
+enum { PH_PRE = 1, PH_TRACE = 2, PH_STAGE = 4, PH_KEEP = 8 };
 // the tracescreen launch's fused-prepass roles (FusedPrepass): the next batch's prepass it runs, and
 // the wait of its k_order for this batch's prepass that the previous k_trace ran
 struct TraceFuse {
@@ -1344,9 +1400,12 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
 // the whole frame; the trace waits for it (ev_pre).  Same launches, same bits.  The first frame, and a
 // frame after anything else read this device's CameraResults on its stream (a feed render, an ahead or
 // fused prepass, a batch), prepass in line; so do the instrumented, graph and gated devices.
+static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shard_rank, int shard_count);
+
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
     rt_device d = (cam && scr && scr->dev && cam->dev == scr->dev) ? scr->dev : nullptr;
+    if (d && (d->flags & RT_DEVICE_DEFERRED)) return deferred_render(d, cam, scr, shard_rank, shard_count);
     const bool plain = d && !(d->flags & (RT_DEVICE_GRAPH | RT_DEVICE_STATS | RT_DEVICE_GATED)) && d->stream &&
                        !d->ahead_pending && !d->ahead_in_pending && d->fuse_state == rt_device_s::FUSE_NONE;
     if (!plain) {
@@ -1558,6 +1617,9 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
     if (feed && n != 1) return fail(RT_ERR_INVALID, "the camera feed is per frame");
     if (scrs && n >= 1 && scrs[0] && scrs[0]->dev)
         if (int rc0 = host_flag_check(scrs[0]->dev)) return rc0;
+    for (int f = 0; scrs && f < n && f < RT_MAX_BATCH; ++f) // a deferred frame of these devices goes first
+        if (scrs[f] && scrs[f]->dev)
+            if (int rc0 = defer_flush(scrs[f]->dev)) return rc0;
     if (cams && scrs && n >= 1 && n <= RT_MAX_BATCH && scrs[0] && scrs[0]->dev) {
         // a pending ahead prepass writes these frames' CameraResults: it comes before anything this
         // call queues, the constant uploads of batch_begin included (they rewrite the block the
@@ -1577,7 +1639,10 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
         if (scrs[f] && scrs[f]->dev) scrs[f]->dev->serial_ok = false;
     int rc;
     Batch b;
-    if ((rc = batch_begin(cams, scrs, n, b, (phases & (PH_PRE | PH_STAGE)) != 0, (phases & PH_TRACE) != 0))) return rc;
+    const bool keep = (phases & PH_KEEP) != 0;
+    phases &= ~PH_KEEP;
+    if ((rc = batch_begin(cams, scrs, n, b, !keep && (phases & (PH_PRE | PH_STAGE)) != 0, !keep && (phases & PH_TRACE) != 0)))
+        return rc;
     rt_device dev = b.dev;
     FrameTable& ft = b.ft;
     if (count < 0) count = n;
@@ -1725,6 +1790,75 @@ int rt_terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int 
     return terrain_render_batch(cams, scrs, n, shard_rank, shard_count, false);
 }
 
+// RT_DEVICE_DEFERRED: launch the device's pending frame (its setTargetDepths + trace; its prepass and constant
+// blocks are queued already) with nothing fused.  Every call that launches on, reads or reconfigures the
+// device calls this first.
+static int defer_flush(rt_device d)
+{
+    if (!d || !d->defer.pending) return RT_OK;
+    const rt_device_s::Deferred p = d->defer;
+    d->defer.pending = false;
+    return terrain_render_batch(&p.cam, &p.scr, 1, p.rank, p.count, false, PH_TRACE | PH_KEEP);
+}
+
+// rt_terrain_render on an RT_DEVICE_DEFERRED device (Terrain.cpp:105-136, one frame per call).  The frame's
+// setTargetDepths + trace wait for the next call; that call launches them with ITS frame's prepass run inside
+// the trace kernel by the waves that finish their first unit (FusedPrepass; on the same stream, so this
+// frame's k_order, launched later behind that whole kernel, needs no wait).  The prepass then rides on the
+// trace's throughput instead of a latency-bound launch that gets CUs only as the trace retires (the plain
+// path's ~0.2-0.3 ms per frame, profiles/r06/swap_chain.md).  Stream order keeps every buffer safe:
+//   [camerarays constants of frame i+1] [k_order i: reads CameraResults] [k_trace i: frame i+1's prepass
+//   writes CameraResults; reads only frame i's tracescreen constants] [tracescreen constants of frame i+1]
+// (the prepass kernels are the only readers of the camerarays block).  Anything else falls back to a flush
+// and the full render.
+static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
+{
+    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return fail(RT_ERR_INVALID, "bad shard");
+    const bool np = cam->shader && scr->shader && cam->shader->landscape == RT_NOMADPLAINS &&
+                    scr->shader->landscape == RT_NOMADPLAINS;
+    const bool plain = np && d->stream && !(d->flags & (RT_DEVICE_GRAPH | RT_DEVICE_STATS | RT_DEVICE_GATED)) &&
+                       !d->ahead_pending && !d->ahead_in_pending && d->fuse_state == rt_device_s::FUSE_NONE;
+    if (!plain) {
+        if (int rc = defer_flush(d)) return rc;
+        return terrain_render_batch(&cam, &scr, 1, shard_rank, shard_count, false);
+    }
+    if (int rc0 = host_flag_check(d)) return rc0;
+    HIP_TRY(hipSetDevice(d->ordinal));
+    const rt_device_s::Deferred p = d->defer;
+    // the pending frame's trace must run a k_trace (a single frame's shard past the last tile launches none)
+    // with the noise tables this prepass reads
+    // (the trace loads its noise tables from the pending frame's tracescreen gradients, which are up to date on the
+    // device unless a later write dirtied them)
+    const bool fuse = p.pending && p.scr->shader && p.scr->shader->landscape == RT_NOMADPLAINS &&
+                      !p.scr->shader->grad_dirty && same_tables(cam->shader, p.scr->shader) &&
+                      (size_t)p.rank < rt_shard_tiles(d->width, d->height, 0, 1);
+    if (!fuse) {
+        if (int rc = defer_flush(d)) return rc;
+        // this frame's prepass in line (its camerarays constants go up with it)
+        if (int rc = terrain_render_batch(&cam, &scr, 1, 0, 1, false, PH_PRE)) return rc;
+        ++d->prepass_launches; // (a render with a prepass launch, rt_device_info)
+    } else {
+        Batch b; // this frame's camerarays constants (only the prepass kernels read that block)
+        if (int rc = batch_begin(&cam, &scr, 1, b, true, false)) return rc;
+        FrameTable sub{};
+        sub.k[0] = b.ft.k[0];
+        sub.kcam[0] = b.ft.kcam[0];
+        sub.cam[0] = b.ft.cam[0];
+        if (int rc = upload_frames(d, d->fuse_table, sub)) return rc;
+        TraceFuse tf;
+        tf.next = FusedPrepass{d->fuse_table.d, d->fctl, (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+        d->defer.pending = false;
+        if (int rc = terrain_render_batch(&p.cam, &p.scr, 1, p.rank, p.count, false, PH_TRACE | PH_KEEP, 0, -1,
+                                          nullptr, nullptr, &tf))
+            return rc;
+        ++d->deferred_fused;
+    }
+    // this frame's tracescreen constants (and noise gradients), behind the trace that read the previous frame's
+    if (int rc = sync_shader(d, scr->shader)) return rc;
+    d->defer = rt_device_s::Deferred{cam, scr, shard_rank, shard_count, true};
+    return RT_OK;
+}
+
 int rt_terrain_render_batch_packed(const rt_compute* cams, const rt_compute* scrs, int n, int shard_rank,
                                    int shard_count, void* dst_device, size_t frame_stride)
 {
@@ -1772,6 +1906,8 @@ int rt_terrain_prepass_ahead(const rt_compute* cams, const rt_compute* scrs, int
         if (!cams[f] || !scrs[f] || cams[f]->dev != scrs[f]->dev) return fail(RT_ERR_INVALID, "computes must share a device");
     rt_device lead = scrs[0]->dev;
     if (int rc0 = host_flag_check(lead)) return rc0;
+    for (int f = 0; f < n; ++f)
+        if (int rc0 = defer_flush(scrs[f]->dev)) return rc0;
     if (lead->flags & RT_DEVICE_GRAPH) return fail(RT_ERR_STATE, "the ahead prepass runs on a side stream: not with RT_DEVICE_GRAPH");
     if (lead->ahead_pending) return fail(RT_ERR_STATE, "a prepass is already ahead for this device's batch: trace it first");
     if (lead->fuse_state == rt_device_s::FUSE_FUSED && lead->ev_fuser_done) {
@@ -1837,6 +1973,9 @@ int rt_terrain_trace_ahead(const rt_compute* cams, const rt_compute* scrs, int n
     if (!cams || !scrs || n < 1 || n > RT_MAX_BATCH || !scrs[0] || !scrs[0]->shader) return fail(RT_ERR_INVALID, "a batch holds 1..%d frames", RT_MAX_BATCH);
     rt_device lead = scrs[0]->dev;
     if (int rc0 = host_flag_check(lead)) return rc0;
+    for (int f = 0; f < n; ++f)
+        if (scrs[f] && scrs[f]->dev)
+            if (int rc0 = defer_flush(scrs[f]->dev)) return rc0;
     HIP_TRY(hipSetDevice(lead->ordinal));
     bool ahead = lead->ahead_pending && (size_t)n <= lead->ahead_cams.size();
     for (int f = 0; ahead && f < n; ++f)
@@ -1933,6 +2072,7 @@ static int shard_copy(const rt_device* devs, const int* shards, int count, void*
     if (d0 && host_flag_check(d0)) return RT_ERR_STATE;
     for (int i = 0; i < n; ++i) {
         if (!devs[i] || !bufs[i] || shards[i] < 0 || shards[i] >= count) return fail(RT_ERR_INVALID, "bad arguments");
+        if (int rc = defer_flush(devs[i])) return rc; // the pending frame is what the shard copy reads or overwrites
         if (devs[i]->width != d0->width || devs[i]->height != d0->height)
             return fail(RT_ERR_INVALID, "shard batch: devices differ in size");
     }

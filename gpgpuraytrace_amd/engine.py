@@ -160,21 +160,24 @@ class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
     def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False,
-                 debug_withhold_fuse=False, gated=False, debug_gate_stress=False):
+                 debug_withhold_fuse=False, gated=False, debug_gate_stress=False, deferred=False):
         """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
         entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
         shadows the fin[t] fallback; same bits).  debug_withhold_fuse: diagnostic
         RT_DEVICE_DEBUG_WITHHOLD_FUSE (a trace this device leads runs none of the next batch's fused
         prepass tasks, so that batch's wait times out: the fail-safe's test).  gated:
         RT_DEVICE_GATED (the gated launch: the prepass inside the trace kernel instead of its own launch
-        before it; same bits, measured slower)."""
+        before it; same bits, measured slower).  deferred: RT_DEVICE_DEFERRED (ABI 9; a render's trace
+        launches with the next render, which runs its own frame's prepass inside that trace kernel; every
+        other call that launches on or reads the device launches a pending frame first)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
                       | (_native.RT_DEVICE_GRAPH if graph else 0)
                       | (_native.RT_DEVICE_DEBUG_SMALL_RINGS if small_rings else 0)
                       | (_native.RT_DEVICE_DEBUG_WITHHOLD_FUSE if debug_withhold_fuse else 0)
                       | (_native.RT_DEVICE_GATED if gated else 0)
-                      | (_native.RT_DEVICE_DEBUG_GATE_STRESS if debug_gate_stress else 0))
+                      | (_native.RT_DEVICE_DEBUG_GATE_STRESS if debug_gate_stress else 0)
+                      | (_native.RT_DEVICE_DEFERRED if deferred else 0))
         self._h = None
 
     def create(self):
@@ -231,6 +234,11 @@ class Device:
         """Renders whose prepass ran on the device's prepass stream, behind the previous frame's k_order
         (rt_terrain_render with a frame in flight; RT_INFO_PRESTREAM_RENDERS)."""
         return self._info((2,))[0]
+
+    def deferred_fused(self):
+        """RT_DEVICE_DEFERRED renders whose prepass ran inside the previous frame's trace kernel
+        (RT_INFO_DEFERRED_FUSED, ABI 9)."""
+        return self._info((3,))[0]
 
     def reserve_cus(self, n):
         """rt_device_reserve_cus (ABI 8): this device's trace kernels leave n CUs free for other streams'

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 enum {
     RT_OK = 0,
@@ -50,7 +50,8 @@ enum {
     RT_DEVICE_DEBUG_SMALL_RINGS = 32u,
     RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64u,
     RT_DEVICE_GATED = 128u,
-    RT_DEVICE_DEBUG_GATE_STRESS = 512u
+    RT_DEVICE_DEBUG_GATE_STRESS = 512u,
+    RT_DEVICE_DEFERRED = 1024u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
@@ -73,7 +74,19 @@ enum {
  * RT_DEVICE_DEBUG_GATE_STRESS (ABI 8, diagnostic, with RT_DEVICE_GATED): the gated launch's cross-CU hand-off of a
  * frame's CellDistance under stress -- every trace wave first reads the frame's previous CellDistance with
  * plain loads (its CU's L1 holds lines that the frame's last prepass task then rewrites) and that task waits
- * ~200 us before it stores them, so units read the flagged cells late, on CUs whose L1 holds the old ones. */
+ * ~200 us before it stores them, so units read the flagged cells late, on CUs whose L1 holds the old ones.
+ * RT_DEVICE_DEFERRED (ABI 9): deferred submission for the one-frame-per-call loop.  rt_terrain_render queues
+ * its frame's prepass (or has it queued) and uploads both constant blocks, but its setTargetDepths + trace are
+ * launched by the NEXT rt_terrain_render, whose own frame's prepass then runs inside that trace kernel
+ * (nomadplains, a trace that has tiles, the same noise tables): a D3D driver's batching of a frame's
+ * dispatches until the next submission, without a prepass launch that waits for the trace's CUs.  Every other
+ * call that launches on, reads, waits on or reconfigures the device -- rt_device_flush, _synchronize,
+ * _readback*, _stats*, _kernel_time, _set_stream, _wait_event, _record_event, _check, _framebuffer, _stream,
+ * _destroy, rt_device_present while recording, any other render, prepass or shard call, a map / unmap / write
+ * of its arrays, a compute run / swap / destroy / set_texture, a texture init / destroy -- launches a pending
+ * frame first.  rt_device_present without a recorder launches nothing (there is no display): a caller that
+ * reads the framebuffer through its own stream calls rt_device_flush or rt_device_record_event first.  Same
+ * bits as without the flag. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };
@@ -152,7 +165,9 @@ int rt_device_graph_info(rt_device dev, unsigned long long* captures, unsigned l
  * their own, RT_INFO_PRESTREAM_RENDERS = those of them whose prepass ran on the device's prepass stream
  * (rt_terrain_render with a frame in flight).  No reference counterpart (the tests check which sequence
  * ran). */
-enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1, RT_INFO_PRESTREAM_RENDERS = 2 };
+/* (ABI 9) RT_INFO_DEFERRED_FUSED: RT_DEVICE_DEFERRED renders whose prepass ran inside the previous frame's
+ * trace kernel. */
+enum { RT_INFO_GATED_LAUNCHES = 0, RT_INFO_PREPASS_LAUNCHES = 1, RT_INFO_PRESTREAM_RENDERS = 2, RT_INFO_DEFERRED_FUSED = 3 };
 int rt_device_info(rt_device dev, int key, unsigned long long* out);
 /* (ABI 8) The trace kernel of the renders this device leads launches (CUs - n) persistent blocks instead of
  * one per CU (0 <= n < CUs; default 0), so n CUs stay free beside it for another stream's kernels -- a

@@ -1,0 +1,169 @@
+"""GPU tests of RT_DEVICE_DEFERRED (ABI 9): rt_terrain_render's setTargetDepths + trace launch with the next
+rt_terrain_render, whose own frame's prepass runs inside that trace kernel (FusedPrepass on one stream), and
+every other call that launches on or reads the device launches a pending frame first.  Bar: the same bits as
+the golden frames / the oracle, for every frame of a serial loop, whichever call ends the deferral."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import golden_index as GI
+from test_gpu_parity import FixedCamera, _config_rows, _device_cells, _hip, make
+
+pytestmark = pytest.mark.gpu
+
+
+def _pose(ter, consts):
+    ter.set_camera(FixedCamera(consts))
+    ter.update_terrain()
+    ter.set_time_of_day_vec(consts["sun"])
+
+
+def _golden_pair(i=0, j=1):
+    gold = GI.load()
+    specs = [GI.FRAMES[i], GI.FRAMES[j]]
+    land, _, w, h, aa, ms, ao = GI.unpack(specs[0])
+    cams = [GI.consts(w, h, GI.unpack(s)[1]) for s in specs]
+    keys = [GI.frame_key(*s) for s in specs]
+    return gold, land, w, h, aa, ms, ao, cams, keys
+
+
+@pytest.mark.parametrize("float_output", [False, True], ids=["rgba8", "rgba32f"])
+def test_deferred_serial_frames_golden(float_output):
+    """Seven frames back to back on one deferred device, the camera alternating between two golden poses, no
+    host synchronisation.  Right after render k returns, frame k-1's trace (with frame k's prepass inside it)
+    is on the device's stream: a copy queued there (through the stream and framebuffer pointers taken before
+    the loop, so no C-ABI call ends the deferral) holds frame k-1, and equals that pose's golden frame.  The
+    last frame comes out through rt_device_readback; its CameraResults and CellDistance equal the golden
+    arrays.  Six of the seven prepasses ran fused, one (the first) as its own launch."""
+    import torch
+    import gpgpuraytrace_amd as G
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, deferred=True)
+    stream = G.lib().rt_device_stream(dev._h)
+    fb = G.lib().rt_device_framebuffer(dev._h)
+    assert stream and fb
+    n = 7
+    bufs = [torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0") for _ in range(n - 1)]
+    torch.cuda.synchronize()
+    hip = _hip()
+    for k in range(n):
+        _pose(ter, cams[k % 2])
+        ter.render_device()
+        if k >= 1:
+            assert hip.hipMemcpyAsync(bufs[k - 1].data_ptr(), fb, w * h * 4, 3, stream) == 0
+    last = dev.readback()
+    assert dev.deferred_fused() == n - 1
+    assert dev.launch_info() == (0, 1)
+    for k, buf in enumerate(bufs):
+        got = buf.cpu().numpy().reshape(h, w, 4)
+        assert np.array_equal(got, gold[keys[k % 2] + "_rgba8"]), k
+    kl = keys[(n - 1) % 2]
+    assert np.array_equal(last, gold[kl + "_rgba8"])
+    if float_output:
+        f32 = dev.readback_float()
+        assert np.array_equal(f32.view(np.uint32), gold[kl + "_rgba32f"].view(np.uint32))
+    assert np.array_equal(_device_cells(ter), gold[kl + "_cell_distance"])
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, gold[kl + "_camera_results"])
+    dev.check()
+    dev.destroy()
+
+
+def test_deferred_flush_points():
+    """Each way a pending frame is launched: a readback, rt_device_synchronize, a map of CameraResults, an
+    event recorded for the caller's stream, rt_device_flush, a render of another kind, and the device's
+    destruction.  Every frame read equals its pose's golden frame; renders that followed a pending frame fused
+    their prepass into its trace, the others launched their own."""
+    import torch
+    import gpgpuraytrace_amd as G
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    A, B = 0, 1
+
+    def render(i):
+        _pose(ter, cams[i])
+        ter.render_device()
+
+    render(A)
+    assert np.array_equal(dev.readback(), gold[keys[A] + "_rgba8"])     # readback
+    assert dev.deferred_fused() == 0
+    render(B)
+    render(A)
+    dev.synchronize()                                                   # synchronize
+    assert dev.deferred_fused() == 1
+    assert np.array_equal(dev.readback(), gold[keys[A] + "_rgba8"])
+    render(B)
+    ter.get_camera_results()                                            # map of CameraResults
+    assert np.array_equal(ter.camera_view, gold[keys[B] + "_camera_results"])
+    assert np.array_equal(dev.readback(), gold[keys[B] + "_rgba8"])
+    render(A)
+    ev = torch.cuda.Event()
+    ev.record()  # (torch creates the HIP event at its first record)
+    dev.record_event(ev.cuda_event)                                     # an event for the caller's stream
+    stream = torch.cuda.current_stream()
+    stream.wait_event(ev)
+    fb = torch.empty(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    assert _hip().hipMemcpyAsync(fb.data_ptr(), G.lib().rt_device_framebuffer(dev._h), fb.numel(), 3,
+                                 stream.cuda_stream) == 0
+    assert np.array_equal(fb.cpu().numpy().reshape(h, w, 4), gold[keys[A] + "_rgba8"])
+    render(B)
+    render(A)
+    dev.flush()                                                         # rt_device_flush
+    assert dev.deferred_fused() == 2
+    assert np.array_equal(dev.readback(), gold[keys[A] + "_rgba8"])
+    render(B)
+    ter.render_device(feed=True)                                        # a render of another kind
+    ter.camera_feed()
+    assert np.array_equal(dev.readback(), gold[keys[B] + "_rgba8"])
+    assert dev.deferred_fused() == 2
+    render(A)
+    dev.check()                                                         # rt_device_check launches it too
+    assert np.array_equal(dev.readback(), gold[keys[A] + "_rgba8"])
+    render(B)
+    render(A)
+    dev.destroy()                                                       # destruction with a frame pending
+
+
+def test_deferred_other_landscape_renders_in_line():
+    """A landscape whose trace kernel has no fused prepass (testing): a deferred device renders every frame in
+    line (a flush, then the full render), so each frame is complete when the call returns."""
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair(4, 5)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    for k in range(3):
+        _pose(ter, cams[k % 2])
+        ter.render_device()
+    assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
+    assert dev.deferred_fused() == 0 and dev.launch_info() == (0, 3)
+    dev.destroy()
+
+
+def test_deferred_c3_rows_bitexact():
+    """BASELINE C3 at full size (1920x1080, 512-step cap, 1 AO ray, RGBA8 device) on a deferred device: the
+    look-down frame, then the reset frame whose prepass runs inside the look-down frame's trace.  The
+    look-down frame (copied on the device's stream right after the second render) and the reset frame (read
+    back) are UNORM8-bit-exact against the oracle's row sample; the reset frame's CameraResults and
+    CellDistance are exact."""
+    import torch
+    import gpgpuraytrace_amd as G
+    c_ld, (_, ref8_ld, _, _, _), rows = _config_rows("c3", "lookdown", 5)
+    c_rs, (_, ref8_rs, cr_rs, cd_rs, _), _ = _config_rows("c3", "reset", 5)
+    w, h = c_rs["width"], c_rs["height"]
+    dev, ter = make(c_ld, max_steps=512, ao=1, float_output=False, deferred=True)
+    stream, fb = G.lib().rt_device_stream(dev._h), G.lib().rt_device_framebuffer(dev._h)
+    buf = torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    ter.render_device()
+    _pose(ter, c_rs)
+    ter.render_device()
+    assert _hip().hipMemcpyAsync(buf.data_ptr(), fb, w * h * 4, 3, stream) == 0
+    img8 = dev.readback()
+    assert dev.deferred_fused() == 1
+    ld = buf.cpu().numpy().reshape(h, w, 4)
+    assert np.array_equal(ld[rows], ref8_ld[rows])
+    assert np.array_equal(img8[rows], ref8_rs[rows])
+    assert np.all(img8[..., 3] == 255) and np.all(ld[..., 3] == 255)
+    assert np.array_equal(_device_cells(ter), cd_rs)
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, cr_rs)
+    dev.destroy()

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     # the ctypes binding covers the whole header
     assert set(names) <= set(_native.SIGNATURES), set(names) - set(_native.SIGNATURES)
-    assert L.rt_abi_version() == _native.ABI_VERSION == 8
+    assert L.rt_abi_version() == _native.ABI_VERSION == 9
 
 
 def test_product_reads_no_environment_and_has_no_experiment_switches():
