@@ -651,24 +651,29 @@ def main():
         dt_serial = time.perf_counter() - ts
         # the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each render launches the previous frame's
         # trace with its own frame's prepass inside it
-        ddev = E.DeviceFactory.construct(E.DeviceAPI.HIP, W, H, gpu=local, deferred=True)
-        dter = E.Terrain(ddev, a.landscape, max_steps=a.max_steps, ao_samples=a.ao)
-        dter.create()
-        assert dter.reload(), G.lib().rt_last_error()
-        dter.set_camera(camera)
-        dter.set_time_of_day(0.3)
-        for _ in range(3):
-            dter.render_device()
-            ddev.present()
-        ddev.synchronize()
-        ts = time.perf_counter()
-        for _ in range(a.steps):
-            dter.render_device()
-            ddev.present()
-        ddev.synchronize()
-        dt_deferred = time.perf_counter() - ts
-        deferred_fused = ddev.deferred_fused()
-        ddev.destroy()
+        # (and with 2 frames to a deferred launch, rt_device_defer_batch)
+        dt_deferred, deferred_fused = {}, {}
+        for kdef in (1, 2):
+            ddev = E.DeviceFactory.construct(E.DeviceAPI.HIP, W, H, gpu=local, deferred=True)
+            ddev.defer_batch(kdef)
+            dter = E.Terrain(ddev, a.landscape, max_steps=a.max_steps, ao_samples=a.ao)
+            dter.create()
+            assert dter.reload(), G.lib().rt_last_error()
+            dter.set_camera(camera)
+            dter.set_time_of_day(0.3)
+            for _ in range(4):
+                dter.render_device()
+                ddev.present()
+            ddev.synchronize()
+            f0 = ddev.deferred_fused()
+            ts = time.perf_counter()
+            for _ in range(a.steps):
+                dter.render_device()
+                ddev.present()
+            ddev.synchronize()
+            dt_deferred[kdef] = time.perf_counter() - ts
+            deferred_fused[kdef] = ddev.deferred_fused() - f0
+            ddev.destroy()
     ring.destroy()
     if world == 1 and not a.no_companions:
         # B = 1 with three frames in flight (D3D11's default maximum frame latency, the reference
@@ -699,14 +704,19 @@ def main():
             "how": f"rt_terrain_render + rt_device_present, one frame per call on one device and its stream (B=1; "
                    f"each frame's prepass on the device's prepass stream behind the previous frame's k_order, "
                    f"overlapping that frame's trace tail), {a.steps} frames"}
-        companions["single_frame_deferred"] = {
-            "value": round(rays_per_frame * a.steps / dt_deferred / 1e6, 3), "unit": "Mray/s",
-            "ms_per_frame": round(dt_deferred / a.steps * 1e3, 4),
-            "primary_plus_shadow_mrays": round(ps * a.steps / dt_deferred / 1e6, 3),
-            "fused_prepasses": deferred_fused,
-            "how": f"the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each rt_terrain_render launches the "
-                   f"previous frame's setTargetDepths + trace with its own frame's prepass inside that trace "
-                   f"kernel, the last frame by rt_device_synchronize, {a.steps} frames"}
+        for kdef, key in ((1, "single_frame_deferred"), (2, "single_frame_deferred2")):
+            companions[key] = {
+                "value": round(rays_per_frame * a.steps / dt_deferred[kdef] / 1e6, 3), "unit": "Mray/s",
+                "ms_per_frame": round(dt_deferred[kdef] / a.steps * 1e3, 4),
+                "primary_plus_shadow_mrays": round(ps * a.steps / dt_deferred[kdef] / 1e6, 3),
+                "fused_prepasses": deferred_fused[kdef],
+                "how": (f"the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each rt_terrain_render launches the "
+                        f"previous frame's setTargetDepths + trace with its own frame's prepass inside that trace "
+                        f"kernel, the last frame by rt_device_synchronize, {a.steps} frames") if kdef == 1 else
+                       (f"the same loop on an RT_DEVICE_DEFERRED device tracing 2 frames to a launch "
+                        f"(rt_device_defer_batch(2)): every second rt_terrain_render launches the two oldest queued "
+                        f"frames' setTargetDepths + trace with the next two frames' prepasses inside it; every frame "
+                        f"in full, the intermediate ones into frame slots (a DISCARD swap chain), {a.steps} frames")}
 
     if world == 1 and not a.no_companions and a.config == "c3" and (a.max_steps, a.ao) == (512, 1):
         rc = frame_counts(0, 0, batch_stats=False)

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rt_device_graph_info": (_i, [_vp, C.POINTER(C.c_ulonglong), C.POINTER(C.c_ulonglong)]),
     "rt_device_info": (_i, [_vp, _i, C.POINTER(C.c_ulonglong)]),
     "rt_device_reserve_cus": (_i, [_vp, _i]),
+    "rt_device_defer_batch": (_i, [_vp, _i]),
     "rt_debug_spin": (_i, [_vp, _vp, C.c_ulonglong, C.c_ulonglong, _vp]),
     "rt_device_wait_event": (_i, [_vp, _vp]),
     "rt_device_record_event": (_i, [_vp, _vp]),

@@ -20,6 +20,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -153,6 +154,31 @@ struct rt_device_s {
         int rank = 0, count = 1;
         bool pending = false;
     } defer;
+    // RT_DEVICE_DEFERRED with rt_device_defer_batch(K >= 2): frames are traced K to a launch.  Each render takes a
+    // frame slot (its constant blocks snapshotted there, its own CameraResults, CellDistance and framebuffers)
+    // and queues it; every K-th render launches the oldest K queued frames' setTargetDepths + trace as one batch,
+    // with the next K frames' prepasses fused into that trace kernel.  A flush launches everything queued; its
+    // last frame writes the device's framebuffers and the API's CellDistance / CameraResults.
+    struct FrameSlot {
+        RtConsts* k = nullptr;    // the frame's tracescreen constant block, as at its render
+        RtConsts* kcam = nullptr; // its camerarays block
+        float4* cam = nullptr;    // its CameraResults
+        float2* cells = nullptr;  // its CellDistance
+        uint32_t* fb8 = nullptr;  // its framebuffers (scratch: only a flush's last frame is read)
+        float4* fb32 = nullptr;
+        Staging stage_k, stage_kcam;
+        ~FrameSlot()
+        {
+            for (void* p : {(void*)k, (void*)kcam, (void*)cam, (void*)cells, (void*)fb8, (void*)fb32})
+                if (p) (void)hipFree(p);
+        }
+    };
+    std::vector<std::unique_ptr<FrameSlot>> slots;
+    int defer_k = 1;         // frames per deferred launch (1: the Deferred path above)
+    int slot_next = 0;
+    std::deque<int> dq;      // queued frames' slots, oldest first; the first dq_pre have their prepass done
+    int dq_pre = 0;
+    struct rt_compute_s *dq_cam = nullptr, *dq_scr = nullptr;
     // frame tables (rt_kernels.h FrameTable): the batch's, and the split prepass's frame subset
     struct DevTable {
         FrameTable* d = nullptr;
@@ -1010,6 +1036,18 @@ int rt_device_reserve_cus(rt_device d, int n)
     return RT_OK;
 }
 
+int rt_device_defer_batch(rt_device d, int frames)
+{
+    if (!d) return fail(RT_ERR_INVALID, "null device");
+    if (frames < 1 || frames > 4) return fail(RT_ERR_INVALID, "1..4 frames per deferred launch, not %d", frames);
+    if (!(d->flags & RT_DEVICE_DEFERRED)) return fail(RT_ERR_STATE, "rt_device_defer_batch needs RT_DEVICE_DEFERRED");
+    if (frames == d->defer_k) return RT_OK;
+    if (int rc = defer_flush(d)) return rc;
+    d->defer_k = frames;
+    d->slot_next = 0;
+    return RT_OK;
+}
+
 int rt_device_graph_info(rt_device d, unsigned long long* captures, unsigned long long* launches)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");
@@ -1793,12 +1831,22 @@ int rt_terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, int 
 // RT_DEVICE_DEFERRED: launch the device's pending frame (its setTargetDepths + trace; its prepass and constant
 // blocks are queued already) with nothing fused.  Every call that launches on, reads or reconfigures the
 // device calls this first.
-static int defer_flush(rt_device d)
+static int defer_flush_batch(rt_device d);
+static int deferred_render_batch(rt_device d, rt_compute cam, rt_compute scr);
+
+static int defer_flush_one(rt_device d)
 {
-    if (!d || !d->defer.pending) return RT_OK;
+    if (!d->defer.pending) return RT_OK;
     const rt_device_s::Deferred p = d->defer;
     d->defer.pending = false;
     return terrain_render_batch(&p.cam, &p.scr, 1, p.rank, p.count, false, PH_TRACE | PH_KEEP);
+}
+
+static int defer_flush(rt_device d)
+{
+    if (!d) return RT_OK;
+    if (!d->dq.empty()) return defer_flush_batch(d); // (a device has frames queued one way or the other, not both)
+    return defer_flush_one(d);
 }
 
 // rt_terrain_render on an RT_DEVICE_DEFERRED device (Terrain.cpp:105-136, one frame per call).  The frame's
@@ -1824,6 +1872,11 @@ static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shar
     }
     if (int rc0 = host_flag_check(d)) return rc0;
     HIP_TRY(hipSetDevice(d->ordinal));
+    if (d->defer_k >= 2 && shard_count == 1 && same_tables(cam->shader, scr->shader)) {
+        if (int rc = defer_flush_one(d)) return rc; // (a K = 1 frame pending: traced alone first)
+        return deferred_render_batch(d, cam, scr);
+    }
+    if (int rc = defer_flush_batch(d)) return rc; // (frames queued for a batch, then a sharded render: they go first)
     const rt_device_s::Deferred p = d->defer;
     // the pending frame's trace must run a k_trace (a single frame's shard past the last tile launches none)
     // with the noise tables this prepass reads
@@ -1856,6 +1909,160 @@ static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shar
     // this frame's tracescreen constants (and noise gradients), behind the trace that read the previous frame's
     if (int rc = sync_shader(d, scr->shader)) return rc;
     d->defer = rt_device_s::Deferred{cam, scr, shard_rank, shard_count, true};
+    return RT_OK;
+}
+
+// ---- RT_DEVICE_DEFERRED, K frames to a launch (rt_device_defer_batch) ----
+// frame slot i of the device (made on first use)
+static int slot_get(rt_device d, int i, rt_device_s::FrameSlot** out)
+{
+    while ((int)d->slots.size() <= i) d->slots.emplace_back(new rt_device_s::FrameSlot());
+    rt_device_s::FrameSlot& f = *d->slots[i];
+    if (!f.k) {
+        const size_t px = (size_t)d->width * d->height;
+        HIP_TRY(hipMalloc(&f.k, sizeof(RtConsts)));
+        HIP_TRY(hipMalloc(&f.kcam, sizeof(RtConsts)));
+        HIP_TRY(hipMalloc(&f.cam, 1024 * sizeof(float4)));
+        HIP_TRY(hipMalloc(&f.cells, 1024 * sizeof(float2)));
+        HIP_TRY(hipMalloc(&f.fb8, px * 4));
+        if (d->fb32) HIP_TRY(hipMalloc(&f.fb32, px * 16));
+    }
+    *out = &f;
+    return RT_OK;
+}
+
+// launch the first n of the queued frames (their prepass done): setTargetDepths + one trace over the n frames
+// (the shard is the whole frame), with the prepasses of the next m queued frames fused into it (FusedPrepass on
+// the same stream: the next launch's k_order comes after this whole kernel).  last: the n-th frame is the
+// flush's last, so it writes the device's framebuffers and the API's CellDistance; its CameraResults are
+// copied to the API's array behind the trace.
+static int batch_trace(rt_device d, int n, int m, bool last)
+{
+    rt_compute cam = d->dq_cam, scr = d->dq_scr;
+    Shader* s = scr->shader;
+    FrameTable ft{}, nx{};
+    for (int i = 0; i < n; ++i) {
+        rt_device_s::FrameSlot& f = *d->slots[d->dq[i]];
+        const bool out = last && i == n - 1;
+        ft.k[i] = f.k;
+        ft.kcam[i] = f.kcam;
+        ft.cam[i] = f.cam;
+        ft.cells[i] = out ? (float2*)s->array("CellDistance")->dev_ptr : f.cells;
+        ft.out8[i] = out ? d->fb8 : f.fb8;
+        ft.out32[i] = out ? d->fb32 : f.fb32;
+    }
+    for (int i = 0; i < m; ++i) {
+        rt_device_s::FrameSlot& f = *d->slots[d->dq[n + i]];
+        nx.k[i] = f.k;
+        nx.kcam[i] = f.kcam;
+        nx.cam[i] = f.cam;
+    }
+    if (int rc = ensure_split_buffers(d, s->aa, s->ao, n)) return rc;
+    RtLaunch a = make_launch(d, s);
+    a.consts = ft.k[0];
+    if (int rc = upload_frames(d, d->table, ft)) return rc;
+    a.frames = d->table.d;
+    a.frames_host = ft;
+    a.n_frames = (uint32_t)n;
+    a.cells_from_cam = 1;
+    if (m > 0) {
+        if (int rc = upload_frames(d, d->fuse_table, nx)) return rc;
+        a.fuse_next = FusedPrepass{d->fuse_table.d, d->fctl, (uint32_t)m * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+        d->deferred_fused += (unsigned long long)m;
+    }
+    // (as terrain_render_batch: hit pixels finish in k_trace with one sample, <= 1 AO ray and no float output)
+    a.fit = s->aa == 1 && s->ao <= 1 && !d->fb32;
+    a.fitm = s->aa == 1 && s->ao >= 2 && !d->fb32 && (size_t)d->width * (size_t)d->height < ((size_t)1 << 23);
+    {
+        KernelTimer kt(d);
+        rt_launch_tracescreen(a, 0, 0, (uint32_t)d->width, (uint32_t)d->height, 0u, 1u);
+    }
+    if (last) {
+        rt_array_s* cr = cam->shader->array("CameraResults");
+        if (cr && cr->dev_ptr && cr->elements >= 1024)
+            HIP_TRY(hipMemcpyAsync(cr->dev_ptr, ft.cam[n - 1], 1024 * sizeof(float4), hipMemcpyDeviceToDevice, d->stream));
+    }
+    HIP_TRY(hipGetLastError());
+    for (int i = 0; i < n; ++i) d->dq.pop_front();
+    d->dq_pre = m;
+    return RT_OK;
+}
+
+// the standalone prepass of the first n queued frames (nothing queued before them runs a trace to fuse it into)
+static int batch_prepass(rt_device d, int n)
+{
+    FrameTable sub{};
+    for (int i = 0; i < n; ++i) {
+        rt_device_s::FrameSlot& f = *d->slots[d->dq[i]];
+        sub.k[i] = f.k;
+        sub.kcam[i] = f.kcam;
+        sub.cam[i] = f.cam;
+    }
+    RtLaunch a = make_launch(d, d->dq_cam->shader);
+    a.consts = sub.kcam[0];
+    if (int rc = upload_frames(d, d->pre_table, sub)) return rc;
+    a.frames = d->pre_table.d;
+    a.frames_host = sub;
+    a.n_frames = (uint32_t)n;
+    rt_launch_camerarays_batch(a);
+    HIP_TRY(hipGetLastError());
+    ++d->prepass_launches;
+    d->dq_pre = n;
+    return RT_OK;
+}
+
+// launch every queued frame, K to a launch, the last into the device's own buffers
+static int defer_flush_batch(rt_device d)
+{
+    const int K = d->defer_k;
+    while (!d->dq.empty()) {
+        if (d->dq_pre == 0)
+            if (int rc = batch_prepass(d, std::min<int>(K, (int)d->dq.size()))) return rc;
+        const int n = d->dq_pre, m = std::min<int>(K, (int)d->dq.size() - n);
+        if (int rc = batch_trace(d, n, m, (int)d->dq.size() == n)) {
+            d->dq.clear();
+            d->dq_pre = 0;
+            return rc;
+        }
+    }
+    return RT_OK;
+}
+
+// rt_terrain_render with K >= 2 frames to a deferred launch: queue this frame (its constant blocks into its
+// slot); the K-th queued frame beyond a launch-ready group launches that group with this group's prepasses
+// fused.  Slots are reused by stream order: a slot's next upload follows the launch that read it.
+static int deferred_render_batch(rt_device d, rt_compute cam, rt_compute scr)
+{
+    const int K = d->defer_k;
+    Shader *sc = cam->shader, *ss = scr->shader;
+    // another compute pair, or new noise tables: what is queued goes first, then the tables go up
+    if (!d->dq.empty() && (cam != d->dq_cam || scr != d->dq_scr || sc->grad_dirty || ss->grad_dirty))
+        if (int rc = defer_flush_batch(d)) return rc;
+    if (d->dq.empty()) {
+        if (int rc = check_texture(sc)) return rc;
+        if (int rc = check_texture(ss)) return rc;
+        rt_array_s* cd = ss->array("CellDistance");
+        if (!cd || !cd->dev_ptr || cd->elements < 1024) return fail(RT_ERR_STATE, "CellDistance not created with 1024 elements");
+        if (int rc = sync_shader(d, sc)) return rc; // the noise gradients (and the shaders' own blocks) up
+        if (int rc = sync_shader(d, ss)) return rc;
+        d->dq_cam = cam;
+        d->dq_scr = scr;
+    }
+    const int slot = d->slot_next;
+    d->slot_next = (d->slot_next + 1) % (2 * K);
+    rt_device_s::FrameSlot* f = nullptr;
+    if (int rc = slot_get(d, slot, &f)) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_cb_mu);
+        RtConsts kc, ks;
+        build_consts(*sc, *d, kc);
+        build_consts(*ss, *d, ks);
+        if (int rc = f->stage_kcam.upload(d->stream, f->kcam, &kc, sizeof(RtConsts))) return rc;
+        if (int rc = f->stage_k.upload(d->stream, f->k, &ks, sizeof(RtConsts))) return rc;
+    }
+    d->dq.push_back(slot);
+    if (d->dq_pre == 0 && (int)d->dq.size() == K) return batch_prepass(d, K); // the first group: nothing to ride on
+    if (d->dq_pre == K && (int)d->dq.size() == 2 * K) return batch_trace(d, K, K, false);
     return RT_OK;
 }
 

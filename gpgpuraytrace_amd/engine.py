@@ -240,6 +240,11 @@ class Device:
         (RT_INFO_DEFERRED_FUSED, ABI 9)."""
         return self._info((3,))[0]
 
+    def defer_batch(self, frames):
+        """rt_device_defer_batch (ABI 9, RT_DEVICE_DEFERRED devices): trace `frames` (1..4) frames to a launch, the
+        next group's prepasses inside it; a flush launches all queued frames, the last into the device's buffers."""
+        check(lib().rt_device_defer_batch(self._h, int(frames)), "defer_batch")
+
     def reserve_cus(self, n):
         """rt_device_reserve_cus (ABI 8): this device's trace kernels leave n CUs free for other streams'
         kernels (rank 0's RCCL receive at N > 1)."""

@@ -174,6 +174,16 @@ int rt_device_info(rt_device dev, int key, unsigned long long* out);
  * collective's (RCCL's receive on rank 0 at N > 1, which otherwise queues behind the other batch's trace
  * until its tail) or a transport copy.  Same bits.  No reference counterpart. */
 int rt_device_reserve_cus(rt_device dev, int n);
+/* (ABI 9) An RT_DEVICE_DEFERRED device traces `frames` (1..4; default 1) frames to a launch: each rt_terrain_render
+ * of the whole frame (shard 0 of 1) snapshots its frame's constant blocks into a frame slot of the device (its own
+ * CameraResults, CellDistance and framebuffers) and queues it; every frames-th render launches the oldest
+ * `frames` queued frames' setTargetDepths + trace as one batch, with the next `frames` frames' prepasses inside
+ * that trace kernel.  A flush (the calls listed under RT_DEVICE_DEFERRED) launches everything queued; its last
+ * frame writes the device's framebuffers and the compute pair's CellDistance and CameraResults, the others write
+ * their slots (scratch: the reference's DISCARD swap chain never shows a frame that was not presented to a
+ * reader).  Same bits per frame.  Changing it launches what is queued.  No reference counterpart (the D3D
+ * runtime queues up to three frames). */
+int rt_device_defer_batch(rt_device dev, int frames);
 /* (ABI 6) Stream handoff without a host synchronisation.  `hip_event` is a hipEvent_t the caller
  * owns (a C++ host's, or torch.cuda.Event.cuda_event).  rt_device_wait_event: the work the device
  * queues from now on waits for the event -- e.g. buffers the caller filled on its own stream, then

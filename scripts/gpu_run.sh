@@ -27,10 +27,10 @@ summ() {  # one summary line of a bench json
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 r, c = d["roofline"], d["config"]
-sf = c.get("single_frame", {}); ss = c.get("single_frame_serial", {}); sd = c.get("single_frame_deferred", {})
-print("== %-40s %8.2f Mray/s %.4f ms/frame frac %.4f kernel %.3f ms  hbm x%s  sf %s  serial p+s %s  deferred p+s %s" % (
+sf = c.get("single_frame", {}); ss = c.get("single_frame_serial", {}); sd = c.get("single_frame_deferred", {}); s2 = c.get("single_frame_deferred2", {})
+print("== %-40s %8.2f Mray/s %.4f ms/frame frac %.4f kernel %.3f ms  hbm x%s  sf %s  serial p+s %s  deferred p+s %s / %s" % (
     sys.argv[1][:40], d["value"], d["ms_per_step"], r["frac"], r["kernel_avg_ms"], r.get("traffic_per_frame_vs_rgba8"),
-    sf.get("primary_plus_shadow_mrays"), ss.get("primary_plus_shadow_mrays"), sd.get("primary_plus_shadow_mrays")))
+    sf.get("primary_plus_shadow_mrays"), ss.get("primary_plus_shadow_mrays"), sd.get("primary_plus_shadow_mrays"), s2.get("primary_plus_shadow_mrays")))
 PY
 }
 for step in "$@"; do

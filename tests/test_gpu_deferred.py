@@ -167,3 +167,56 @@ def test_deferred_c3_rows_bitexact():
     ter.get_camera_results()
     assert np.array_equal(ter.camera_view, cr_rs)
     dev.destroy()
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_deferred_batch_sequences_golden(k):
+    """rt_device_defer_batch(k): frames queue in the device's frame slots and trace k to a launch, each group's
+    prepasses inside the previous group's trace.  For every sequence length L = 1 .. 2k+1 (so the last frame
+    sits at every position of a group, its prepass standalone or fused, its trace alone or beside other frames),
+    L renders with the camera alternating between two golden poses, then a readback: the last frame's RGBA8
+    frame, CameraResults and CellDistance equal its pose's golden arrays.  All but the first k frames of a
+    sequence prepass inside a trace; each sequence launches one prepass of its own."""
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev.defer_batch(k)
+    fused = 0
+    for L in range(1, 2 * k + 2):
+        for i in range(L):
+            _pose(ter, cams[(L - 1 - i) % 2])  # the last frame is pose 0
+            ter.render_device()
+        assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"]), L
+        fused += max(0, L - k)
+        assert dev.deferred_fused() == fused, L
+        assert np.array_equal(_device_cells(ter), gold[keys[0] + "_cell_distance"]), L
+        ter.get_camera_results()
+        assert np.array_equal(ter.camera_view, gold[keys[0] + "_camera_results"]), L
+    assert dev.launch_info() == (0, 2 * k + 1)
+    dev.defer_batch(1)
+    _pose(ter, cams[1])
+    ter.render_device()
+    assert np.array_equal(dev.readback(), gold[keys[1] + "_rgba8"])
+    dev.check()
+    dev.destroy()
+
+
+def test_deferred_batch_c3_rows_bitexact():
+    """BASELINE C3 at full size on a deferred device tracing 2 frames to a launch: look-down, reset, look-down,
+    reset, then a readback.  The last reset frame (its prepass inside the first pair's trace, its trace beside
+    the third frame's) is UNORM8-bit-exact against the oracle's row sample, its CameraResults and CellDistance
+    exact."""
+    c_ld = _config_rows("c3", "lookdown", 5)[0]
+    c_rs, (_, ref8_rs, cr_rs, cd_rs, _), rows = _config_rows("c3", "reset", 5)
+    dev, ter = make(c_ld, max_steps=512, ao=1, float_output=False, deferred=True)
+    dev.defer_batch(2)
+    for c in (c_ld, c_rs, c_ld, c_rs):
+        _pose(ter, c)
+        ter.render_device()
+    img8 = dev.readback()
+    assert dev.deferred_fused() == 2
+    assert np.array_equal(img8[rows], ref8_rs[rows])
+    assert np.all(img8[..., 3] == 255)
+    assert np.array_equal(_device_cells(ter), cd_rs)
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, cr_rs)
+    dev.destroy()
