@@ -68,6 +68,7 @@ SIGNATURES = {
     "rt_device_reserve_cus": (_i, [_vp, _i]),
     "rt_device_defer_batch": (_i, [_vp, _i]),
     "rt_debug_spin": (_i, [_vp, _vp, C.c_ulonglong, C.c_ulonglong, _vp]),
+    "rt_debug_defer_slot": (_i, [_vp, _i, _vp, _vp, _vp]),
     "rt_device_wait_event": (_i, [_vp, _vp]),
     "rt_device_record_event": (_i, [_vp, _vp]),
     "rt_device_check": (_i, [_vp]),

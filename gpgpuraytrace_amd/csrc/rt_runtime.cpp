@@ -1036,6 +1036,17 @@ int rt_device_reserve_cus(rt_device d, int n)
     return RT_OK;
 }
 
+int rt_debug_defer_slot(rt_device d, int slot, void** fb8, void** camera_results, void** cell_distance)
+{
+    if (!d || slot < 0 || slot >= (int)d->slots.size() || !d->slots[slot]->k) return fail(RT_ERR_INVALID, "no frame slot %d", slot);
+    if (int rc = defer_flush(d)) return rc;
+    const rt_device_s::FrameSlot& f = *d->slots[slot];
+    if (fb8) *fb8 = f.fb8;
+    if (camera_results) *camera_results = f.cam;
+    if (cell_distance) *cell_distance = f.cells;
+    return RT_OK;
+}
+
 int rt_device_defer_batch(rt_device d, int frames)
 {
     if (!d) return fail(RT_ERR_INVALID, "null device");

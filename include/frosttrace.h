@@ -372,6 +372,12 @@ int rt_debug_sky(rt_compute cs, const float* dirs, float* out, int n);
  *   spins `ticks` more -- the CU a collective's kernel holds while it waits for its peer and transfers. */
 int rt_debug_spin(void* hip_stream, const unsigned long long* base_device, unsigned long long until_ticks,
                   unsigned long long ticks, unsigned long long* stamp_device);
+/* rt_debug_defer_slot (ABI 9, tests): the device pointers of frame slot `slot` of an RT_DEVICE_DEFERRED device
+ *   tracing K >= 2 frames to a launch (rt_device_defer_batch): its RGBA8 framebuffer, CameraResults (1024
+ *   float4) and CellDistance (1024 float2), where a queued frame that was not a flush's last one wrote them.
+ *   Frame i of a sequence that started with an empty queue takes slot i % (2K).  RT_ERR_INVALID for a slot
+ *   never used. */
+int rt_debug_defer_slot(rt_device dev, int slot, void** fb8, void** camera_results, void** cell_distance);
 
 /* ---- IRecorder (Factories/IRecorder.h; RecorderWinAPI.cpp; RecorderFactory.cpp) ----
  * rt_recorder_create   <- RecorderFactory::construct(device, frameRate, fixedSpeed) + create():

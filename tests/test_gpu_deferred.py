@@ -220,3 +220,36 @@ def test_deferred_batch_c3_rows_bitexact():
     ter.get_camera_results()
     assert np.array_equal(ter.camera_view, cr_rs)
     dev.destroy()
+
+
+def test_deferred_batch_intermediate_frames_golden():
+    """Every frame of a deferred-batch sequence, not only the flush's last: 2 frames to a launch, seven frames
+    alternating between two golden poses, then a readback.  Frame i takes slot i % 4 (rt_debug_defer_slot), so
+    after the flush slots 0 and 1 hold frames 4 and 5, slot 3 frame 3, and slot 2 frame 2's framebuffer and
+    CellDistance beside frame 6's CameraResults (the flush's last frame prepasses into its slot, then traces into
+    the device's own buffers; frames 2 and 6 share a pose).  Every one equals its pose's golden arrays."""
+    import gpgpuraytrace_amd as G
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev.defer_batch(2)
+    n = 7
+    for i in range(n):
+        _pose(ter, cams[i % 2])
+        ter.render_device()
+    assert np.array_equal(dev.readback(), gold[keys[(n - 1) % 2] + "_rgba8"])
+    lib = C.CDLL("libamdhip64.so")
+    lib.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    for slot, frame in ((0, 4), (1, 5), (2, 2), (3, 3)):
+        fb, cr, cd = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        assert G.lib().rt_debug_defer_slot(dev._h, slot, C.byref(fb), C.byref(cr), C.byref(cd)) == 0
+        img = np.empty((h, w, 4), np.uint8)
+        cam = np.empty((1024, 4), np.float32)
+        cells = np.empty((1024, 2), np.float32)
+        for dst, src in ((img, fb), (cam, cr), (cells, cd)):
+            assert lib.hipMemcpy(dst.ctypes.data, src, dst.nbytes, 2) == 0
+        key = keys[frame % 2]
+        assert np.array_equal(img, gold[key + "_rgba8"]), (slot, frame)
+        assert np.array_equal(cam, gold[key + "_camera_results"]), (slot, frame)
+        assert np.array_equal(cells, gold[key + "_cell_distance"]), (slot, frame)
+    assert dev.deferred_fused() == n - 2
+    dev.destroy()
