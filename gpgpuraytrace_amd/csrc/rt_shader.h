@@ -331,13 +331,25 @@ __device__ __forceinline__ float np_fbm(const Ctx& c, f3 q0, int n_oct)
     // cycles of ~40 per octave; rt_variants.h RT_OCT_SMEM)
     const KPtr kc = (KPtr)c.k;
     int N = 1;
+#if RT_OCT_SCALAR_EXIT
+    int Ne;
+#endif
     #pragma unroll 1
     do {
         count_noise(c.nz);
         const float sx = kc->np_scale[N], sy = kc->np_scale_y[N], w = kc->np_rcp[N];
         s = fma(noise3d_finish(c.nz, noise3d_cell<FAST>(c.nz, q0.x * sx, q0.y * sy, q0.z * sx)), w, s);
         ++N;
+#if RT_OCT_SCALAR_EXIT
+        // (A/B) the exit compares an opaque SGPR copy of N against each lane's count (one v_cmp), where loop
+        // strength reduction counts every lane down (a v_add and a v_cmp per octave); N itself still
+        // strides the constant loads
+        Ne = N;
+        asm volatile("" : "+s"(Ne));
+    } while (Ne <= n_oct);
+#else
     } while (N <= n_oct);
+#endif
 #elif !defined(RT_EXTRA_OCTAVE)
     // The octave-table pointer is the trip counter: a per-lane register from the start (the asm
     // keeps it out of SGPRs, which would cost a v_mov per iteration for the LDS address), one

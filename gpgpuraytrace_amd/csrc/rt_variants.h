@@ -107,6 +107,12 @@
 #ifndef RT_OCT_SMEM
 #define RT_OCT_SMEM 1
 #endif
+// (A/B) the SMEM octave loop's exit: 1 = a v_cmp of the scalar octave index against each lane's count, 53 VALU
+// per octave instead of 54 (no per-lane countdown).  Bit-exact, measured within noise: 1505.4 / 1504.3 / 1475.9
+// against 1505.2 / 1503.3 / 1504.2 Mray/s, alternating on one box (profiles/r06/oct_exit_ab.txt)
+#ifndef RT_OCT_SCALAR_EXIT
+#define RT_OCT_SCALAR_EXIT 0
+#endif
 // wave priority (s_setprio) of a fused prepass task (FusedPrepass) while it marches
 #ifndef RT_FUSE_PRIO
 #define RT_FUSE_PRIO 3
