@@ -253,3 +253,55 @@ def test_deferred_batch_intermediate_frames_golden():
         assert np.array_equal(cells, gold[key + "_cell_distance"]), (slot, frame)
     assert dev.deferred_fused() == n - 2
     dev.destroy()
+
+
+def test_deferred_differential_sequence():
+    """A seeded random sequence of 60 operations, applied to a plain device and to a deferred one: renders
+    with the camera, sun and time changing, readbacks, CameraResults maps, CellDistance reads, flushes,
+    synchronisations and changes of the frames traced to a launch (1, 2, 3, 4).  At every observation the
+    deferred device shows what the plain device shows, bit for bit (RGBA8 and RGBA32F)."""
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    suns = [np.asarray(cams[0]["sun"], np.float32), np.asarray(cams[1]["sun"], np.float32),
+            np.asarray([0.3, 0.8, -0.52], np.float32)]
+    dp, tp = make(cams[0], land, aa=aa, max_steps=ms, ao=1, float_output=True)
+    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=1, float_output=True, deferred=True)
+    rng = np.random.default_rng(7)
+    renders = observed = 0
+    for step in range(60):
+        op = rng.choice(["render"] * 7 + ["readback", "float", "map", "cells", "flush", "sync", "k"])
+        if op == "render":
+            pose, sun = cams[int(rng.integers(2))], suns[int(rng.integers(3))]
+            for ter in (tp, td):
+                ter.set_camera(FixedCamera(pose))
+                ter.update_terrain(float(rng.integers(4)))
+                ter.set_time_of_day_vec(sun)
+                ter.render_device()
+            renders += 1
+        elif renders == 0:
+            continue
+        elif op == "readback":
+            assert np.array_equal(dd.readback(), dp.readback()), step
+            observed += 1
+        elif op == "float":
+            assert np.array_equal(dd.readback_float().view(np.uint32), dp.readback_float().view(np.uint32)), step
+            observed += 1
+        elif op == "map":
+            tp.get_camera_results()
+            td.get_camera_results()
+            assert np.array_equal(td.camera_view, tp.camera_view), step
+            observed += 1
+        elif op == "cells":
+            assert np.array_equal(_device_cells(td), _device_cells(tp)), step
+            observed += 1
+        elif op == "flush":
+            dd.flush()
+        elif op == "sync":
+            dd.synchronize()
+        else:
+            dd.defer_batch(int(rng.integers(1, 5)))
+    assert np.array_equal(dd.readback(), dp.readback())
+    assert observed >= 8 and renders >= 20, (observed, renders)
+    assert dd.deferred_fused() > 0
+    dd.check()
+    dp.destroy()
+    dd.destroy()
