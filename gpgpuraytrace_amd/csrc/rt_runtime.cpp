@@ -160,20 +160,30 @@ struct rt_device_s {
     // with the next K frames' prepasses fused into that trace kernel.  A flush launches everything queued; its
     // last frame writes the device's framebuffers and the API's CellDistance / CameraResults.
     struct FrameSlot {
-        RtConsts* k = nullptr;    // the frame's tracescreen constant block, as at its render
-        RtConsts* kcam = nullptr; // its camerarays block
-        float4* cam = nullptr;    // its CameraResults
-        float2* cells = nullptr;  // its CellDistance
-        uint32_t* fb8 = nullptr;  // its framebuffers (scratch: only a flush's last frame is read)
+        RtConsts hk{}, hkcam{};             // the frame's tracescreen and camerarays blocks, as at its render
+        const RtConsts* dk = nullptr;       // where they went up (in the launch block of its prepass)
+        const RtConsts* dkcam = nullptr;
+        float4* cam = nullptr;   // its CameraResults
+        float2* cells = nullptr; // its CellDistance
+        uint32_t* fb8 = nullptr; // its framebuffers (scratch: only a flush's last frame is read)
         float4* fb32 = nullptr;
-        Staging stage_k, stage_kcam;
         ~FrameSlot()
         {
-            for (void* p : {(void*)k, (void*)kcam, (void*)cam, (void*)cells, (void*)fb8, (void*)fb32})
+            for (void* p : {(void*)cam, (void*)cells, (void*)fb8, (void*)fb32})
                 if (p) (void)hipFree(p);
         }
     };
     std::vector<std::unique_ptr<FrameSlot>> slots;
+    // one upload per deferred launch: the frame tables it reads and the constant blocks of the frames whose
+    // prepass it runs (a ring of 3: a block's frames are traced by the next launch, so a block is rewritten
+    // three launches later, in stream order behind both)
+    struct LaunchBlock {
+        FrameTable ft, nx;
+        RtConsts k[4], kcam[4];
+    };
+    LaunchBlock* blocks = nullptr;
+    Staging block_stage[3];
+    int block_next = 0;
     int defer_k = 1;         // frames per deferred launch (1: the Deferred path above)
     int slot_next = 0;
     std::deque<int> dq;      // queued frames' slots, oldest first; the first dq_pre have their prepass done
@@ -784,7 +794,7 @@ rt_device_s::~rt_device_s()
     }
     for (void* p : {(void*)fb8, (void*)fb32, (void*)stats, (void*)scratch_cam, (void*)queue, (void*)samples,
                     (void*)hitq, (void*)finpool, (void*)cpool, (void*)gate, (void*)claims, (void*)order, (void*)hitmask, (void*)spill_long, (void*)fin, (void*)aocc,
-                    (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl})
+                    (void*)bgrx, (void*)table.d, (void*)pre_table.d, (void*)fuse_table.d, (void*)fctl, (void*)blocks})
         if (p) (void)hipFree(p);
     if (recorder) recorder_detach(recorder); // the recorder outlives its device: it stops capturing
     if (graph_pre.exec) (void)hipGraphExecDestroy(graph_pre.exec);
@@ -1038,7 +1048,7 @@ int rt_device_reserve_cus(rt_device d, int n)
 
 int rt_debug_defer_slot(rt_device d, int slot, void** fb8, void** camera_results, void** cell_distance)
 {
-    if (!d || slot < 0 || slot >= (int)d->slots.size() || !d->slots[slot]->k) return fail(RT_ERR_INVALID, "no frame slot %d", slot);
+    if (!d || slot < 0 || slot >= (int)d->slots.size() || !d->slots[slot]->cam) return fail(RT_ERR_INVALID, "no frame slot %d", slot);
     if (int rc = defer_flush(d)) return rc;
     const rt_device_s::FrameSlot& f = *d->slots[slot];
     if (fb8) *fb8 = f.fb8;
@@ -1929,16 +1939,37 @@ static int slot_get(rt_device d, int i, rt_device_s::FrameSlot** out)
 {
     while ((int)d->slots.size() <= i) d->slots.emplace_back(new rt_device_s::FrameSlot());
     rt_device_s::FrameSlot& f = *d->slots[i];
-    if (!f.k) {
+    if (!f.cam) {
         const size_t px = (size_t)d->width * d->height;
-        HIP_TRY(hipMalloc(&f.k, sizeof(RtConsts)));
-        HIP_TRY(hipMalloc(&f.kcam, sizeof(RtConsts)));
         HIP_TRY(hipMalloc(&f.cam, 1024 * sizeof(float4)));
         HIP_TRY(hipMalloc(&f.cells, 1024 * sizeof(float2)));
         HIP_TRY(hipMalloc(&f.fb8, px * 4));
         if (d->fb32) HIP_TRY(hipMalloc(&f.fb32, px * 16));
     }
     *out = &f;
+    return RT_OK;
+}
+
+// the next launch block: the frames' tables and the constant blocks of the m frames from queue position `from`
+// (their prepass runs in this launch), uploaded in one copy; those frames' constants are read from there on
+static int block_upload(rt_device d, rt_device_s::LaunchBlock& hb, int from, int m, rt_device_s::LaunchBlock** out)
+{
+    if (!d->blocks) HIP_TRY(hipMalloc(&d->blocks, 3 * sizeof(rt_device_s::LaunchBlock)));
+    const int b = d->block_next;
+    d->block_next = (b + 1) % 3;
+    rt_device_s::LaunchBlock* db = d->blocks + b;
+    for (int i = 0; i < m; ++i) {
+        rt_device_s::FrameSlot& f = *d->slots[d->dq[from + i]];
+        hb.k[i] = f.hk;
+        hb.kcam[i] = f.hkcam;
+        f.dk = db->k + i;
+        f.dkcam = db->kcam + i;
+        hb.nx.k[i] = f.dk;
+        hb.nx.kcam[i] = f.dkcam;
+        hb.nx.cam[i] = f.cam;
+    }
+    if (int rc = d->block_stage[b].upload(d->stream, db, &hb, sizeof(hb))) return rc;
+    *out = db;
     return RT_OK;
 }
 
@@ -1951,34 +1982,29 @@ static int batch_trace(rt_device d, int n, int m, bool last)
 {
     rt_compute cam = d->dq_cam, scr = d->dq_scr;
     Shader* s = scr->shader;
-    FrameTable ft{}, nx{};
+    rt_device_s::LaunchBlock hb{};
+    FrameTable& ft = hb.ft;
     for (int i = 0; i < n; ++i) {
         rt_device_s::FrameSlot& f = *d->slots[d->dq[i]];
         const bool out = last && i == n - 1;
-        ft.k[i] = f.k;
-        ft.kcam[i] = f.kcam;
+        ft.k[i] = f.dk;
+        ft.kcam[i] = f.dkcam;
         ft.cam[i] = f.cam;
         ft.cells[i] = out ? (float2*)s->array("CellDistance")->dev_ptr : f.cells;
         ft.out8[i] = out ? d->fb8 : f.fb8;
         ft.out32[i] = out ? d->fb32 : f.fb32;
     }
-    for (int i = 0; i < m; ++i) {
-        rt_device_s::FrameSlot& f = *d->slots[d->dq[n + i]];
-        nx.k[i] = f.k;
-        nx.kcam[i] = f.kcam;
-        nx.cam[i] = f.cam;
-    }
     if (int rc = ensure_split_buffers(d, s->aa, s->ao, n)) return rc;
+    rt_device_s::LaunchBlock* db = nullptr;
+    if (int rc = block_upload(d, hb, n, m, &db)) return rc;
     RtLaunch a = make_launch(d, s);
     a.consts = ft.k[0];
-    if (int rc = upload_frames(d, d->table, ft)) return rc;
-    a.frames = d->table.d;
+    a.frames = &db->ft;
     a.frames_host = ft;
     a.n_frames = (uint32_t)n;
     a.cells_from_cam = 1;
     if (m > 0) {
-        if (int rc = upload_frames(d, d->fuse_table, nx)) return rc;
-        a.fuse_next = FusedPrepass{d->fuse_table.d, d->fctl, (uint32_t)m * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
+        a.fuse_next = FusedPrepass{&db->nx, d->fctl, (uint32_t)m * (uint32_t)RT_FUSE_TASKS_PER_FRAME};
         d->deferred_fused += (unsigned long long)m;
     }
     // (as terrain_render_batch: hit pixels finish in k_trace with one sample, <= 1 AO ray and no float output)
@@ -2002,18 +2028,13 @@ static int batch_trace(rt_device d, int n, int m, bool last)
 // the standalone prepass of the first n queued frames (nothing queued before them runs a trace to fuse it into)
 static int batch_prepass(rt_device d, int n)
 {
-    FrameTable sub{};
-    for (int i = 0; i < n; ++i) {
-        rt_device_s::FrameSlot& f = *d->slots[d->dq[i]];
-        sub.k[i] = f.k;
-        sub.kcam[i] = f.kcam;
-        sub.cam[i] = f.cam;
-    }
+    rt_device_s::LaunchBlock hb{};
+    rt_device_s::LaunchBlock* db = nullptr;
+    if (int rc = block_upload(d, hb, 0, n, &db)) return rc;
     RtLaunch a = make_launch(d, d->dq_cam->shader);
-    a.consts = sub.kcam[0];
-    if (int rc = upload_frames(d, d->pre_table, sub)) return rc;
-    a.frames = d->pre_table.d;
-    a.frames_host = sub;
+    a.consts = hb.nx.kcam[0];
+    a.frames = &db->nx;
+    a.frames_host = hb.nx;
     a.n_frames = (uint32_t)n;
     rt_launch_camerarays_batch(a);
     HIP_TRY(hipGetLastError());
@@ -2039,9 +2060,10 @@ static int defer_flush_batch(rt_device d)
     return RT_OK;
 }
 
-// rt_terrain_render with K >= 2 frames to a deferred launch: queue this frame (its constant blocks into its
-// slot); the K-th queued frame beyond a launch-ready group launches that group with this group's prepasses
-// fused.  Slots are reused by stream order: a slot's next upload follows the launch that read it.
+// rt_terrain_render with K >= 2 frames to a deferred launch: queue this frame (its constant blocks snapshotted in
+// its slot); the K-th queued frame beyond a launch-ready group launches that group with this group's prepasses
+// fused.  Slots are reused by stream order: a slot's buffers are next written by launches behind the one that
+// read them.
 static int deferred_render_batch(rt_device d, rt_compute cam, rt_compute scr)
 {
     const int K = d->defer_k;
@@ -2064,13 +2086,11 @@ static int deferred_render_batch(rt_device d, rt_compute cam, rt_compute scr)
     rt_device_s::FrameSlot* f = nullptr;
     if (int rc = slot_get(d, slot, &f)) return rc;
     {
-        std::lock_guard<std::mutex> lk(g_cb_mu);
-        RtConsts kc, ks;
-        build_consts(*sc, *d, kc);
-        build_consts(*ss, *d, ks);
-        if (int rc = f->stage_kcam.upload(d->stream, f->kcam, &kc, sizeof(RtConsts))) return rc;
-        if (int rc = f->stage_k.upload(d->stream, f->k, &ks, sizeof(RtConsts))) return rc;
+        std::lock_guard<std::mutex> lk(g_cb_mu); // (a snapshot: they go up with the launch that runs its prepass)
+        build_consts(*sc, *d, f->hkcam);
+        build_consts(*ss, *d, f->hk);
     }
+    f->dk = f->dkcam = nullptr;
     d->dq.push_back(slot);
     if (d->dq_pre == 0 && (int)d->dq.size() == K) return batch_prepass(d, K); // the first group: nothing to ride on
     if (d->dq_pre == K && (int)d->dq.size() == 2 * K) return batch_trace(d, K, K, false);
