@@ -305,3 +305,29 @@ def test_deferred_differential_sequence():
     dd.check()
     dp.destroy()
     dd.destroy()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_deferred_recorder_frames(tmp_path, k):
+    """The recorder on a deferred device: present() while recording launches the pending frames first, so every
+    recorded frame is the one just rendered.  Four frames alternating between two golden poses, 1 or 2 frames to
+    a launch: the video holds the four golden frames in order (the recorder's BGRX rows)."""
+    import gpgpuraytrace_amd as G
+    import oracle_lib as O
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev.defer_batch(k)
+    path = str(tmp_path / "out.rgb32")
+    rec = G.RecorderFactory.construct(dev, 25, True, path)
+    rec.start()
+    for i in range(4):
+        _pose(ter, cams[i % 2])
+        ter.render_device()
+        dev.present()
+    rec.stop()
+    rec.destroy()
+    vid, _ = G.read_recording(path, w, h)
+    assert vid.shape == (4, h, w)
+    for i in range(4):
+        assert np.array_equal(vid[i], O.bgrx(gold[keys[i % 2] + "_rgba8"])), i
+    dev.destroy()
