@@ -93,8 +93,9 @@ def parse():
     ap.add_argument("--frames-in-flight", type=int, default=2,
                     help="batches (slot groups, one HIP stream each) kept in flight; 1 = one batch at a time")
     ap.add_argument("--batch", type=int, default=None,
-                    help="max frames per rt_terrain_render_batch launch sequence (1..24; default 12, 24 for C1 whose "
-                         "256x256 frames underfill the chip at 12: 855-871 against 703 Mray/s, DESIGN.md section 5); "
+                    help="max frames per rt_terrain_render_batch launch sequence (1..24; default 12, and 24 at 8 ranks or "
+                         "more or for C1 whose 256x256 frames underfill the chip at 12: 855-871 against 703 Mray/s, "
+                         "DESIGN.md section 5); "
                          "the --steps frames are split into ceil(steps / batch) batches of near-equal size")
     ap.add_argument("--split-prepass", type=int, default=0,
                     help="N>1: 1 = each rank runs the prepass of B/N frames of a batch and an all-gather shares "
@@ -136,7 +137,11 @@ def parse():
         if getattr(a, key) is None:
             setattr(a, key, preset[key])
     if a.batch is None:
-        a.batch = preset.get("batch", 12)
+        # 12; 24 from 8 ranks on, where a 12-frame batch leaves each rank 1.5 frames of trace per launch and its
+        # prepass, tail and gather dominate: the N = 8 coupled shard model 0.4327 -> 0.4189 ms/frame at 20 frames
+        # (N = 2 / 4 prefer 12; N = 1 equal; profiles/r06/batch_by_ranks.md)
+        ranks = int(os.environ.get("WORLD_SIZE", a.gpus))
+        a.batch = preset.get("batch", 24 if ranks >= 8 else 12)
     if a.graph is None:
         a.graph = 1 if a.config == "c5" else 0
     if a.lookahead and a.graph:
