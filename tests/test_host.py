@@ -184,3 +184,29 @@ def test_capi_errors_are_reported_not_crashes():
     assert L.rt_compute_run(None, 1, 1, 1) < 0
     out = C.c_void_p()
     assert L.rt_device_create(0, 0, 0, 0, C.byref(out)) < 0
+
+
+def header_enum(name):
+    txt = open(os.path.join(ROOT, "include", "frosttrace.h")).read()
+    m = re.search(r"\b" + name + r"\s*=\s*(\d+)u?\b", txt)
+    assert m, name
+    return int(m.group(1))
+
+
+def test_deferred_device_binding():
+    """ABI 9's deferred submission as the binding sees it, without a GPU: the flag value matches the header,
+    Device(deferred=True) sets it (and only it beside the others asked for), rt_device_defer_batch and
+    rt_debug_defer_slot reject a null device, and the info key matches the header."""
+    import gpgpuraytrace_amd as G
+    from gpgpuraytrace_amd import _native
+    assert _native.RT_DEVICE_DEFERRED == header_enum("RT_DEVICE_DEFERRED") == 1024
+    assert header_enum("RT_INFO_DEFERRED_FUSED") == 3
+    d = G.engine.Device(64, 48, deferred=True)
+    assert d.flags == _native.RT_DEVICE_DEFERRED
+    d2 = G.engine.Device(64, 48, float_output=True, deferred=True)
+    assert d2.flags == _native.RT_DEVICE_DEFERRED | _native.RT_DEVICE_FLOAT_OUTPUT
+    assert G.engine.Device(64, 48).flags & _native.RT_DEVICE_DEFERRED == 0
+    L = G.lib()
+    assert L.rt_device_defer_batch(None, 2) < 0 and b"null" in L.rt_last_error()
+    p = C.c_void_p()
+    assert L.rt_debug_defer_slot(None, 0, C.byref(p), C.byref(p), C.byref(p)) < 0
