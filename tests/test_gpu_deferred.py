@@ -331,3 +331,29 @@ def test_deferred_recorder_frames(tmp_path, k):
     for i in range(4):
         assert np.array_equal(vid[i], O.bgrx(gold[keys[i % 2] + "_rgba8"])), i
     dev.destroy()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("spec", [2, 3, 8, 9, 11, 12, 10], ids=["aa4", "ms64", "ao1", "ms512-ao4", "aa8", "aa16-ao1",
+                                                                  "greenrocks-aa2-ao2"])
+@pytest.mark.parametrize("float_output", [False, True], ids=["rgba8", "rgba32f"])
+def test_deferred_golden_specs(spec, k, float_output):
+    """The golden frames of every macro set on a deferred device: AA 4/8/16 (k_finish's per-sample sums), a
+    64- and a 512-step cap, 1 and 4 AO rays (fit, fitm), and a landscape without a fused prepass (greenrocks,
+    rendered in line).  Three renders of the frame, 1 or 2 to a launch, then a readback: the golden RGBA8 (and
+    RGBA32F) frame."""
+    gold = GI.load()
+    land, pose, w, h, aa, ms, ao = GI.unpack(GI.FRAMES[spec])
+    key = GI.frame_key(land, pose, w, h, aa, ms, ao)
+    c = GI.consts(w, h, pose)
+    dev, ter = make(c, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, deferred=True)
+    dev.defer_batch(k)
+    for _ in range(3):
+        _pose(ter, c)
+        ter.render_device()
+    assert np.array_equal(dev.readback(), gold[key + "_rgba8"])
+    if float_output:
+        assert np.array_equal(dev.readback_float().view(np.uint32), gold[key + "_rgba32f"].view(np.uint32))
+    if land == "nomadplains":  # all but the first k frames prepass inside a trace
+        assert dev.deferred_fused() == 3 - k
+    dev.destroy()
