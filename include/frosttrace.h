@@ -83,7 +83,8 @@ enum {
  * call that launches on, reads, waits on or reconfigures the device -- rt_device_flush, _synchronize,
  * _readback*, _stats*, _kernel_time, _set_stream, _wait_event, _record_event, _check, _framebuffer, _stream,
  * _destroy, rt_device_present while recording, any other render, prepass or shard call, a map / unmap / write
- * of its arrays, a compute run / swap / destroy / set_texture, a texture init / destroy -- launches a pending
+ * or device pointer of its arrays, a compute run / swap / destroy / set_texture, a texture init / destroy,
+ * rt_device_defer_batch -- launches a pending
  * frame first.  rt_device_present without a recorder launches nothing (there is no display): a caller that
  * reads the framebuffer through its own stream calls rt_device_flush or rt_device_record_event first.  Same
  * bits as without the flag. */
