@@ -83,7 +83,7 @@ DeviceHIP::~DeviceHIP() { rt_device_destroy(dev); }
 bool DeviceHIP::create()
 {
     const WindowSettings& ws = getWindow()->getWindowSettings();
-    return rt_device_create(ws.gpu < 0 ? 0 : ws.gpu, ws.width, ws.height, 0, &dev) == RT_OK;
+    return rt_device_create(ws.gpu < 0 ? 0 : ws.gpu, ws.width, ws.height, flags, &dev) == RT_OK;
 }
 
 void DeviceHIP::present()

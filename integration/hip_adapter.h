@@ -100,9 +100,13 @@ public:
     bool readback(void* dst, size_t rowPitch) const;
     rt_device handle() const { return dev; }
     void setRecorder(class RecorderHIP* r) { recorder = r; } // DeviceDirect3D::setRecorder (:229-232)
+    // (adapter extension, before create) rt_device_create's flags, e.g. RT_DEVICE_DEFERRED (ABI 9): the reference's
+    // IDevice::create takes none
+    void setFlags(unsigned f) { flags = f; }
 
 private:
     rt_device dev = nullptr;
+    unsigned flags = 0;
     class RecorderHIP* recorder = nullptr;
 };
 

@@ -13,7 +13,7 @@
 //
 // The frame constants come from a file the test writes (the engine's Camera output as the
 // cbuffer bytes Terrain writes), so the driver needs no camera maths.
-//   usage: terrain_driver <consts.bin> <out.bin> <landscape> <aa> <max_steps> <ao> <mode: ref|device>
+//   usage: terrain_driver <consts.bin> <out.bin> <landscape> <aa> <max_steps> <ao> <mode: ref|device|deferred>
 //   consts.bin: int32 W, H; float ViewInverse[16] (cbuffer bytes), Eye[4], Projection[16]
 //               (cbuffer bytes), SunDirection[3]
 //   out.bin:    W*H*4 bytes RGBA8 (IDevice readback), then 1024 float4 CameraResults
@@ -108,7 +108,7 @@ Timer* Timer::get()
 int main(int argc, char** argv)
 {
     if (argc != 8) {
-        std::fprintf(stderr, "usage: %s consts.bin out.bin landscape aa max_steps ao ref|device\n", argv[0]);
+        std::fprintf(stderr, "usage: %s consts.bin out.bin landscape aa max_steps ao ref|device|deferred\n", argv[0]);
         return 2;
     }
     Consts k;
@@ -124,6 +124,7 @@ int main(int argc, char** argv)
     DriverWindow window(ws);
     DeviceHIP device(&window);
     IDevice* dev = &device;
+    if (mode == "deferred") device.setFlags(RT_DEVICE_DEFERRED); // (the frame loop with deferred submission)
     if (!dev->create()) {
         std::fprintf(stderr, "device: %s\n", rt_last_error());
         return 1;
@@ -192,12 +193,17 @@ int main(int argc, char** argv)
     if (varSun) varSun->write(k.sun);
 
     std::vector<float> cameraView(kCameraViewRes * kCameraViewRes * 4, 0.0f);
-    if (mode == "device") {
-        // the one-call device path: prepass, device setTargetDepths, trace
-        if (rt_terrain_render(static_cast<ComputeHIP*>(cameraCompute)->handle(),
-                              static_cast<ComputeHIP*>(compute)->handle(), 0, 1) != RT_OK) {
-            std::fprintf(stderr, "render: %s\n", rt_last_error());
-            return 1;
+    if (mode == "device" || mode == "deferred") {
+        // the one-call device path: prepass, device setTargetDepths, trace.  Deferred:
+        // three frames of the Raytracer loop (render, present), each launched by the next render, the last by the
+        // CameraResults map
+        for (int i = 0; i < (mode == "deferred" ? 3 : 1); ++i) {
+            if (rt_terrain_render(static_cast<ComputeHIP*>(cameraCompute)->handle(),
+                                  static_cast<ComputeHIP*>(compute)->handle(), 0, 1) != RT_OK) {
+                std::fprintf(stderr, "render: %s\n", rt_last_error());
+                return 1;
+            }
+            if (mode == "deferred" && i < 2) dev->present();
         }
         void* cr = varCamResults ? varCamResults->map() : nullptr;
         if (cr) {

@@ -261,7 +261,7 @@ DRIVER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
                       "terrain_driver")
 
 
-@pytest.mark.parametrize("mode", ["ref", "device"])
+@pytest.mark.parametrize("mode", ["ref", "device", "deferred"])
 @pytest.mark.parametrize("spec", [GI.FRAMES[0], GI.FRAMES[1], GI.FRAMES[4], GI.FRAMES[9]],
                          ids=["np_reset", "np_down", "testing", "np_down_ms512_ao4"])
 def test_cpp_adapter_terrain_sequence(spec, mode, tmp_path):
@@ -269,8 +269,9 @@ def test_cpp_adapter_terrain_sequence(spec, mode, tmp_path):
     ShaderArrayHIP, TextureHIP) driven through the reference's own interfaces by
     integration/terrain_driver.cpp, which replays Terrain::create / reload / updateShaders /
     render (Terrain.cpp:55-206: run(2,2,1) -> CameraResults map/unmap -> setTargetDepths ->
-    CellDistance write -> per tile ThreadOffset write + run + flush -> present) or the one-call
-    device path; the RGBA8 readback and CameraResults equal the golden frame's."""
+    CellDistance write -> per tile ThreadOffset write + run + flush -> present), the one-call
+    device path, or that path on an RT_DEVICE_DEFERRED device (DeviceHIP::setFlags) over three frames;
+    the RGBA8 readback and CameraResults equal the golden frame's."""
     assert os.path.exists(DRIVER), "integration/_build/terrain_driver not built (make -C integration, needs " \
                                    "the reference headers: __graft_entry__.build() in the build container)"
     import subprocess
