@@ -717,7 +717,8 @@ def main():
                 "fused_prepasses": deferred_fused[kdef],
                 "how": (f"the same loop on an RT_DEVICE_DEFERRED device (ABI 9): each rt_terrain_render launches the "
                         f"previous frame's setTargetDepths + trace with its own frame's prepass inside that trace "
-                        f"kernel, the last frame by rt_device_synchronize, {a.steps} frames") if kdef == 1 else
+                        f"kernel, the last frame by rt_device_synchronize (a frame under 1280x720 pixels renders as "
+                        f"without the flag: fused_prepasses 0), {a.steps} frames") if kdef == 1 else
                        (f"the same loop on an RT_DEVICE_DEFERRED device tracing 2 frames to a launch "
                         f"(rt_device_defer_batch(2)): every second rt_terrain_render launches the two oldest queued "
                         f"frames' setTargetDepths + trace with the next two frames' prepasses inside it; every frame "

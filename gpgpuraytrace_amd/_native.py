@@ -22,6 +22,7 @@ RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64  # ABI 7: a fusing trace runs none of the nex
 RT_DEVICE_GATED = 128  # ABI 7 (opt-in): the prepass inside the trace kernel, units gated on their cells' rays
 RT_DEVICE_DEBUG_GATE_STRESS = 512  # ABI 8, diagnostic: L1-warm consumers and a late CellDistance (gated hand-off test)
 RT_DEVICE_DEFERRED = 1024  # ABI 9: a render's trace launches with the next render (which fuses its prepass into it)
+RT_DEVICE_DEBUG_DEFER_SMALL = 2048  # ABI 9, diagnostic: the one-frame deferral below 1280x720 pixels too (tests)
 ABI_VERSION = 9  # include/frosttrace.h RT_ABI_VERSION this binding's structs and signatures match
 RT_TEXTURE_2D = 1
 RT_FORMAT_R8G8B8A8_UINT = 3

@@ -33,6 +33,10 @@
 #include "rt_math.h"
 #include "rt_noise.h"
 
+// RT_DEVICE_DEFERRED with one frame to a launch: frames of fewer pixels render as without the flag (at 256x256 the
+// fused prepass outlasts the frame's trace: 0.642 against 0.585 ms a frame; neutral at 1280x720)
+#define RT_DEFER_FUSE_MIN_PIXELS ((size_t)1280 * 720)
+
 namespace {
 
 thread_local std::string g_err;
@@ -815,7 +819,7 @@ int rt_device_create(int ordinal, int width, int height, unsigned flags, rt_devi
     *out = nullptr;
     const unsigned known = RT_DEVICE_FLOAT_OUTPUT | RT_DEVICE_STATS | RT_DEVICE_GRAPH | RT_DEVICE_DEBUG_SMALL_RINGS |
                            RT_DEVICE_DEBUG_WITHHOLD_FUSE | RT_DEVICE_GATED | RT_DEVICE_DEBUG_GATE_STRESS |
-                           RT_DEVICE_DEFERRED;
+                           RT_DEVICE_DEFERRED | RT_DEVICE_DEBUG_DEFER_SMALL;
     if (flags & ~known) return fail(RT_ERR_INVALID, "unknown device flags 0x%x (8 and 16 were retired in ABI 6)", flags & ~known);
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -1460,11 +1464,17 @@ static int terrain_render_batch(const rt_compute* cams, const rt_compute* scrs, 
 // frame after anything else read this device's CameraResults on its stream (a feed render, an ahead or
 // fused prepass, a batch), prepass in line; so do the instrumented, graph and gated devices.
 static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shard_rank, int shard_count);
+static int serial_render(rt_device d, rt_compute cam, rt_compute scr, int shard_rank, int shard_count);
 
 int rt_terrain_render(rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
 {
     rt_device d = (cam && scr && scr->dev && cam->dev == scr->dev) ? scr->dev : nullptr;
     if (d && (d->flags & RT_DEVICE_DEFERRED)) return deferred_render(d, cam, scr, shard_rank, shard_count);
+    return serial_render(d, cam, scr, shard_rank, shard_count);
+}
+
+static int serial_render(rt_device d, rt_compute cam, rt_compute scr, int shard_rank, int shard_count)
+{
     const bool plain = d && !(d->flags & (RT_DEVICE_GRAPH | RT_DEVICE_STATS | RT_DEVICE_GATED)) && d->stream &&
                        !d->ahead_pending && !d->ahead_in_pending && d->fuse_state == rt_device_s::FUSE_NONE;
     if (!plain) {
@@ -1898,6 +1908,12 @@ static int deferred_render(rt_device d, rt_compute cam, rt_compute scr, int shar
         return deferred_render_batch(d, cam, scr);
     }
     if (int rc = defer_flush_batch(d)) return rc; // (frames queued for a batch, then a sharded render: they go first)
+    if ((size_t)d->width * (size_t)d->height < RT_DEFER_FUSE_MIN_PIXELS && !(d->flags & RT_DEVICE_DEBUG_DEFER_SMALL)) {
+        // a small frame's trace is shorter than the prepass it would carry (profiles/r06/deferred.md): it renders
+        // as without the flag, its prepass on the prepass stream in the previous frame's trace tail
+        if (int rc = defer_flush(d)) return rc;
+        return serial_render(d, cam, scr, shard_rank, shard_count);
+    }
     const rt_device_s::Deferred p = d->defer;
     // the pending frame's trace must run a k_trace (a single frame's shard past the last tile launches none)
     // with the noise tables this prepass reads
@@ -2068,6 +2084,7 @@ static int deferred_render_batch(rt_device d, rt_compute cam, rt_compute scr)
 {
     const int K = d->defer_k;
     Shader *sc = cam->shader, *ss = scr->shader;
+    d->serial_ok = false; // (its launches read the device's CameraResults: a later serial render prepasses in line)
     // another compute pair, or new noise tables: what is queued goes first, then the tables go up
     if (!d->dq.empty() && (cam != d->dq_cam || scr != d->dq_scr || sc->grad_dirty || ss->grad_dirty))
         if (int rc = defer_flush_batch(d)) return rc;

@@ -160,7 +160,8 @@ class Device:
     """IDevice over rt_device (DeviceDirect3D's role)."""
 
     def __init__(self, width, height, gpu=0, float_output=False, stats=False, graph=False, small_rings=False,
-                 debug_withhold_fuse=False, gated=False, debug_gate_stress=False, deferred=False):
+                 debug_withhold_fuse=False, gated=False, debug_gate_stress=False, deferred=False,
+                 debug_defer_small=False):
         """small_rings: diagnostic RT_DEVICE_DEBUG_SMALL_RINGS (k_trace's LDS long-ray ring holds 64
         entries and its fin pool 8 slots, so queued long rays take the per-block spill rings and long
         shadows the fin[t] fallback; same bits).  debug_withhold_fuse: diagnostic
@@ -169,7 +170,9 @@ class Device:
         RT_DEVICE_GATED (the gated launch: the prepass inside the trace kernel instead of its own launch
         before it; same bits, measured slower).  deferred: RT_DEVICE_DEFERRED (ABI 9; a render's trace
         launches with the next render, which runs its own frame's prepass inside that trace kernel; every
-        other call that launches on or reads the device launches a pending frame first)."""
+        other call that launches on or reads the device launches a pending frame first; one frame to a launch, a
+        device under 1280x720 pixels renders as without it).  debug_defer_small: diagnostic
+        RT_DEVICE_DEBUG_DEFER_SMALL (the one-frame deferral at every size, for tests on small frames)."""
         self.width, self.height, self.gpu = int(width), int(height), int(gpu)
         self.flags = ((_native.RT_DEVICE_FLOAT_OUTPUT if float_output else 0) | (_native.RT_DEVICE_STATS if stats else 0)
                       | (_native.RT_DEVICE_GRAPH if graph else 0)
@@ -177,7 +180,8 @@ class Device:
                       | (_native.RT_DEVICE_DEBUG_WITHHOLD_FUSE if debug_withhold_fuse else 0)
                       | (_native.RT_DEVICE_GATED if gated else 0)
                       | (_native.RT_DEVICE_DEBUG_GATE_STRESS if debug_gate_stress else 0)
-                      | (_native.RT_DEVICE_DEFERRED if deferred else 0))
+                      | (_native.RT_DEVICE_DEFERRED if deferred else 0)
+                      | (_native.RT_DEVICE_DEBUG_DEFER_SMALL if debug_defer_small else 0))
         self._h = None
 
     def create(self):

@@ -51,7 +51,8 @@ enum {
     RT_DEVICE_DEBUG_WITHHOLD_FUSE = 64u,
     RT_DEVICE_GATED = 128u,
     RT_DEVICE_DEBUG_GATE_STRESS = 512u,
-    RT_DEVICE_DEFERRED = 1024u
+    RT_DEVICE_DEFERRED = 1024u,
+    RT_DEVICE_DEBUG_DEFER_SMALL = 2048u
 };
 /* RT_DEVICE_GRAPH: rt_terrain_render / rt_terrain_render_feed capture the frame's launches
  * into two hipGraphs (prepass + setTargetDepths, tracescreen) on first use and replay them
@@ -87,7 +88,11 @@ enum {
  * rt_device_defer_batch -- launches a pending
  * frame first.  rt_device_present without a recorder launches nothing (there is no display): a caller that
  * reads the framebuffer through its own stream calls rt_device_flush or rt_device_record_event first.  Same
- * bits as without the flag. */
+ * bits as without the flag.  One frame to a launch (the default; rt_device_defer_batch), a device of fewer than
+ * 1280 x 720 pixels renders every frame as without the flag: its trace is shorter than the prepass it would carry
+ * (profiles/r06/deferred.md).
+ * RT_DEVICE_DEBUG_DEFER_SMALL (ABI 9, diagnostic, with RT_DEVICE_DEFERRED): the one-frame deferral at every frame
+ * size, so that tests run it on small frames. */
 
 /* ITexture.h:7-33 enum values */
 enum { RT_TEXTURE_1D = 0, RT_TEXTURE_2D = 1, RT_TEXTURE_3D = 2 };

@@ -12,6 +12,10 @@ from test_gpu_parity import FixedCamera, _config_rows, _device_cells, _hip, make
 
 pytestmark = pytest.mark.gpu
 
+# the one-frame deferral at every frame size (RT_DEVICE_DEBUG_DEFER_SMALL): without it a device under 1280x720
+# pixels renders as without RT_DEVICE_DEFERRED at one frame to a launch (test_deferred_small_frames_serial)
+DEFER = dict(deferred=True, debug_defer_small=True)
+
 
 def _pose(ter, consts):
     ter.set_camera(FixedCamera(consts))
@@ -39,7 +43,7 @@ def test_deferred_serial_frames_golden(float_output):
     import torch
     import gpgpuraytrace_amd as G
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, **DEFER)
     stream = G.lib().rt_device_stream(dev._h)
     fb = G.lib().rt_device_framebuffer(dev._h)
     assert stream and fb
@@ -78,7 +82,7 @@ def test_deferred_flush_points():
     import torch
     import gpgpuraytrace_amd as G
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     A, B = 0, 1
 
     def render(i):
@@ -129,12 +133,47 @@ def test_deferred_other_landscape_renders_in_line():
     """A landscape whose trace kernel has no fused prepass (testing): a deferred device renders every frame in
     line (a flush, then the full render), so each frame is complete when the call returns."""
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair(4, 5)
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     for k in range(3):
         _pose(ter, cams[k % 2])
         ter.render_device()
     assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
     assert dev.deferred_fused() == 0 and dev.launch_info() == (0, 3)
+    dev.destroy()
+
+
+def test_deferred_small_frames_serial():
+    """A deferred device under 1280x720 pixels at one frame to a launch (the product setting, no
+    RT_DEVICE_DEBUG_DEFER_SMALL) renders as a plain device: no prepass fused, every render after the first with
+    its prepass on the prepass stream.  Five frames alternating between two golden poses, each read back equal to
+    its golden frame, then two frames to a launch (fused) and back to one (serial again)."""
+    gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
+    assert w * h < 1280 * 720
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    for k in range(5):
+        _pose(ter, cams[k % 2])
+        ter.render_device()
+        if k % 2:
+            assert np.array_equal(dev.readback(), gold[keys[1] + "_rgba8"]), k
+    assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
+    assert dev.deferred_fused() == 0
+    assert dev.launch_info() == (0, 5) and dev.prestream_renders() == 4
+    dev.defer_batch(2)
+    for k in range(3):
+        _pose(ter, cams[k % 2])
+        ter.render_device()
+    assert np.array_equal(dev.readback(), gold[keys[0] + "_rgba8"])
+    assert dev.deferred_fused() == 1
+    dev.defer_batch(1)
+    for k in range(3):
+        _pose(ter, cams[(k + 1) % 2])
+        ter.render_device()
+    assert np.array_equal(dev.readback(), gold[keys[1] + "_rgba8"])
+    assert dev.deferred_fused() == 1 and dev.prestream_renders() == 6  # (the first after the batch: in line)
+    ter.get_camera_results()
+    assert np.array_equal(ter.camera_view, gold[keys[1] + "_camera_results"])
+    assert np.array_equal(_device_cells(ter), gold[keys[1] + "_cell_distance"])
+    dev.check()
     dev.destroy()
 
 
@@ -178,7 +217,7 @@ def test_deferred_batch_sequences_golden(k):
     frame, CameraResults and CellDistance equal its pose's golden arrays.  All but the first k frames of a
     sequence prepass inside a trace; each sequence launches one prepass of its own."""
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     dev.defer_batch(k)
     fused = 0
     for L in range(1, 2 * k + 2):
@@ -230,7 +269,7 @@ def test_deferred_batch_intermediate_frames_golden():
     the device's own buffers; frames 2 and 6 share a pose).  Every one equals its pose's golden arrays."""
     import gpgpuraytrace_amd as G
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     dev.defer_batch(2)
     n = 7
     for i in range(n):
@@ -255,16 +294,19 @@ def test_deferred_batch_intermediate_frames_golden():
     dev.destroy()
 
 
-def test_deferred_differential_sequence():
+@pytest.mark.parametrize("small", [True, False], ids=["fused-small", "serial-small"])
+def test_deferred_differential_sequence(small):
     """A seeded random sequence of 60 operations, applied to a plain device and to a deferred one: renders
     with the camera, sun and time changing, readbacks, CameraResults maps, CellDistance reads, flushes,
     synchronisations and changes of the frames traced to a launch (1, 2, 3, 4).  At every observation the
-    deferred device shows what the plain device shows, bit for bit (RGBA8 and RGBA32F)."""
+    deferred device shows what the plain device shows, bit for bit (RGBA8 and RGBA32F).  Without
+    RT_DEVICE_DEBUG_DEFER_SMALL the small frame's one-frame renders take the serial path (prepass on the prepass
+    stream), interleaved with the K >= 2 launches."""
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
     suns = [np.asarray(cams[0]["sun"], np.float32), np.asarray(cams[1]["sun"], np.float32),
             np.asarray([0.3, 0.8, -0.52], np.float32)]
     dp, tp = make(cams[0], land, aa=aa, max_steps=ms, ao=1, float_output=True)
-    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=1, float_output=True, deferred=True)
+    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=1, float_output=True, deferred=True, debug_defer_small=small)
     rng = np.random.default_rng(7)
     renders = observed = 0
     for step in range(60):
@@ -301,7 +343,8 @@ def test_deferred_differential_sequence():
             dd.defer_batch(int(rng.integers(1, 5)))
     assert np.array_equal(dd.readback(), dp.readback())
     assert observed >= 8 and renders >= 20, (observed, renders)
-    assert dd.deferred_fused() > 0
+    assert dd.deferred_fused() > 0 or not small
+    assert small or dd.prestream_renders() > 0
     dd.check()
     dp.destroy()
     dd.destroy()
@@ -315,7 +358,7 @@ def test_deferred_recorder_frames(tmp_path, k):
     import gpgpuraytrace_amd as G
     import oracle_lib as O
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
-    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dev, ter = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     dev.defer_batch(k)
     path = str(tmp_path / "out.rgb32")
     rec = G.RecorderFactory.construct(dev, 25, True, path)
@@ -346,7 +389,7 @@ def test_deferred_golden_specs(spec, k, float_output):
     land, pose, w, h, aa, ms, ao = GI.unpack(GI.FRAMES[spec])
     key = GI.frame_key(land, pose, w, h, aa, ms, ao)
     c = GI.consts(w, h, pose)
-    dev, ter = make(c, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, deferred=True)
+    dev, ter = make(c, land, aa=aa, max_steps=ms, ao=ao, float_output=float_output, **DEFER)
     dev.defer_batch(k)
     for _ in range(3):
         _pose(ter, c)
@@ -367,7 +410,7 @@ def test_deferred_sharded_renders_match_plain(k):
     deferral."""
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
     dp, tp = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False)
-    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True)
+    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
     dd.defer_batch(k)
     for i, (r, n) in enumerate([(1, 3), (2, 3), (1, 3), (7, 9), (0, 1), (2, 3)]):
         for ter in (tp, td):

@@ -206,6 +206,9 @@ def test_deferred_device_binding():
     d2 = G.engine.Device(64, 48, float_output=True, deferred=True)
     assert d2.flags == _native.RT_DEVICE_DEFERRED | _native.RT_DEVICE_FLOAT_OUTPUT
     assert G.engine.Device(64, 48).flags & _native.RT_DEVICE_DEFERRED == 0
+    assert _native.RT_DEVICE_DEBUG_DEFER_SMALL == header_enum("RT_DEVICE_DEBUG_DEFER_SMALL") == 2048
+    d3 = G.engine.Device(64, 48, deferred=True, debug_defer_small=True)
+    assert d3.flags == _native.RT_DEVICE_DEFERRED | _native.RT_DEVICE_DEBUG_DEFER_SMALL
     L = G.lib()
     assert L.rt_device_defer_batch(None, 2) < 0 and b"null" in L.rt_last_error()
     p = C.c_void_p()
