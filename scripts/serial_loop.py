@@ -1,7 +1,7 @@
 """The reference's frame loop (Terrain::render, then IDevice::present) on one device, timed: the C3 workload
 at 1920x1080 (512-step cap, 1 AO ray), --frames frames after 3 warm-up frames.  Under `rocprofv3
 --kernel-trace` the launches' timeline shows where a serial frame's time goes (scripts/serial_timeline.py).
-Usage: python scripts/serial_loop.py [--frames 20] [--defer K]"""
+Usage: python scripts/serial_loop.py [--frames 20] [--defer K] [--reserve N]"""
 import argparse
 import os
 import sys
@@ -18,12 +18,16 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--defer", type=int, default=0,
                     help="0: the plain device; K >= 1: RT_DEVICE_DEFERRED with K frames to a launch")
+    ap.add_argument("--reserve", type=int, default=0,
+                    help="rt_device_reserve_cus: the trace kernel leaves N CUs free (for the prepass stream's kernel)")
     a = ap.parse_args()
     import gpgpuraytrace_amd as G
     W, H = a.width, a.height
     dev = G.DeviceFactory.construct(G.DeviceAPI.HIP, W, H, deferred=a.defer > 0)
     if a.defer > 0:
         dev.defer_batch(a.defer)
+    if a.reserve:
+        dev.reserve_cus(a.reserve)
     ter = G.Terrain(dev, "nomadplains", max_steps=512, ao_samples=1)
     ter.create()
     assert ter.reload()
@@ -38,7 +42,8 @@ def main():
         ter.render_device()
         dev.present()
     dev.synchronize()
-    print(f"serial{'' if a.defer == 0 else f' (deferred, {a.defer} frames to a launch)'}: "
+    print(f"serial{'' if a.defer == 0 else f' (deferred, {a.defer} frames to a launch)'}"
+          f"{f', {a.reserve} CUs reserved' if a.reserve else ''}: "
           f"{(time.perf_counter() - t0) / a.frames * 1e3:.4f} ms/frame", flush=True)
     dev.destroy()
 
