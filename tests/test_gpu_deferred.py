@@ -402,15 +402,17 @@ def test_deferred_golden_specs(spec, k, float_output):
     dev.destroy()
 
 
+@pytest.mark.parametrize("small", [True, False], ids=["fused-small", "serial-small"])
 @pytest.mark.parametrize("k", [1, 2])
-def test_deferred_sharded_renders_match_plain(k):
+def test_deferred_sharded_renders_match_plain(k, small):
     """Sharded renders on a deferred device and on a plain one, the camera alternating: shards 1 and 2 of 3, shard
     7 of 9 (past the 64x48 frame's 6 tiles: no trace kernel, so nothing may be fused into it) and the whole frame.
     Every readback is equal.  A sharded render on a device tracing K >= 2 frames to a launch takes the one-frame
-    deferral."""
+    deferral; without RT_DEVICE_DEBUG_DEFER_SMALL the small frame's one-frame renders (sharded too) take the
+    serial path, mixed with the K = 2 batches."""
     gold, land, w, h, aa, ms, ao, cams, keys = _golden_pair()
     dp, tp = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False)
-    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, **DEFER)
+    dd, td = make(cams[0], land, aa=aa, max_steps=ms, ao=ao, float_output=False, deferred=True, debug_defer_small=small)
     dd.defer_batch(k)
     for i, (r, n) in enumerate([(1, 3), (2, 3), (1, 3), (7, 9), (0, 1), (2, 3)]):
         for ter in (tp, td):
