@@ -88,7 +88,7 @@ enum {
  * rt_device_defer_batch -- launches a pending
  * frame first.  rt_device_present without a recorder launches nothing (there is no display): a caller that
  * reads the framebuffer through its own stream calls rt_device_flush or rt_device_record_event first.  Same
- * bits as without the flag.  One frame to a launch (the default; rt_device_defer_batch), a device of fewer than
+ * bits as without the flag.  At one frame to a launch (the default; rt_device_defer_batch), a device of fewer than
  * 1280 x 720 pixels renders every frame as without the flag: its trace is shorter than the prepass it would carry
  * (profiles/r06/deferred.md).
  * RT_DEVICE_DEBUG_DEFER_SMALL (ABI 9, diagnostic, with RT_DEVICE_DEFERRED): the one-frame deferral at every frame
